@@ -1,0 +1,209 @@
+/*
+ * kaolin_dibr.h -- C ABI of the MI355X (gfx950) DIB-R rasterization hot path.
+ *
+ * Plain C: pointers are DEVICE pointers (hipMalloc / torch caching allocator) unless noted,
+ * sizes are plain integers, `stream` is a hipStream_t passed as void*.  Every function is
+ * asynchronous on `stream`, never synchronises the host, never allocates, never frees and never
+ * keeps a pointer past its return.  Every output element is written (no pre-fill needed).
+ * Return value: KD_OK (0) or a KD_ERR_* code; kd_last_error() gives the message (thread-local).
+ *
+ * Layouts are the reference's (contiguous row-major):
+ *   face_vertices_z      (B, F, 3)        face_vertices_image (B, F, 3, 2)
+ *   face_features        (B, F, 3, D)     face_idx            (B, H, W) int64, -1 = empty
+ *   interpolated_features(B, H, W, D)     weights             (B, H, W, 3)
+ *   soft_mask            (B, H, W)        close_face_{prob,idx,dist_type} (B, H, W, K)
+ * "packed" inputs are the reference's packed layout: faces of view b are rows
+ * [first_idx[b], first_idx[b+1]) of (Fp, ...) arrays; first_idx (B+1) int64 lives on the device.
+ *
+ * The `_f32` / `_f64` suffix is the scalar type (reference: AT_DISPATCH float / double).
+ */
+#ifndef KAOLIN_DIBR_H_
+#define KAOLIN_DIBR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KD_OK 0
+#define KD_ERR_INVALID_ARGUMENT 1
+#define KD_ERR_LAUNCH 2
+#define KD_ERR_WORKSPACE 3
+
+/* Workspace kinds for kd_workspace_size(). */
+#define KD_WS_RASTER_PACKED 1 /* kd_packed_rasterize_forward_*      */
+#define KD_WS_RASTER 2        /* kd_rasterize_forward_*             */
+#define KD_WS_SOFT_MASK 3     /* kd_dibr_soft_mask_forward*_*       */
+#define KD_WS_GATHER_BWD 4    /* kd_*_backward_gather_*             */
+
+/* Bytes of device workspace the call of `kind` needs.  num_faces_total = rows of the face arrays
+ * (Fp for the packed layout, B*F otherwise); max_faces_per_view = the largest per-view count
+ * (Fp when unknown on the host, F otherwise). */
+size_t kd_workspace_size(int kind, int batch, int height, int width, int64_t num_faces_total,
+                         int64_t max_faces_per_view);
+
+const char *kd_last_error(void);
+int kd_version(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Packed rasterize forward.  Replaces _C.render.mesh.packed_rasterize_forward_cuda
+ * (reference kaolin/csrc/bindings.cpp:77 -> kaolin/csrc/render/mesh/rasterization.cpp:49-104,
+ * kernel rasterization_cuda.cu:43-192).  fvi and bboxes are already multiplied by `multiplier`
+ * (rasterization.py:337-344).  face_idx receives the PACKED-LOCAL index (row - first_idx[b]).
+ * ------------------------------------------------------------------------------------------- */
+int kd_packed_rasterize_forward_f32(int batch, int height, int width, int64_t num_faces,
+                                    int feat_dim, const float *fvz, const float *fvi,
+                                    const float *bboxes, const float *feat,
+                                    const int64_t *first_idx, float multiplier, float eps,
+                                    float *interp, int64_t *face_idx, float *weights,
+                                    void *workspace, size_t workspace_bytes, void *stream);
+int kd_packed_rasterize_forward_f64(int batch, int height, int width, int64_t num_faces,
+                                    int feat_dim, const double *fvz, const double *fvi,
+                                    const double *bboxes, const double *feat,
+                                    const int64_t *first_idx, float multiplier, float eps,
+                                    double *interp, int64_t *face_idx, double *weights,
+                                    void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Batched rasterize forward (no packing, no host sync).  Replaces RasterizeCuda.forward
+ * (kaolin/render/mesh/rasterization.py:289-369: torch.where packing, x multiplier, bboxes,
+ * packed->original remap) fused with the packed kernel.  fvi is NOT scaled; `valid` (B, F) uint8
+ * may be NULL (all faces valid).  face_idx receives the ORIGINAL face index, exactly as
+ * rasterize() returns it.  `multiplier` is the Python value (scaling is done in the scalar type
+ * like torch's `tensor * multiplier`; pixel centres use (float)multiplier like the kernel).
+ * ------------------------------------------------------------------------------------------- */
+int kd_rasterize_forward_f32(int batch, int height, int width, int64_t num_faces, int feat_dim,
+                             const float *fvz, const float *fvi, const float *feat,
+                             const uint8_t *valid, double multiplier, float eps, float *interp,
+                             int64_t *face_idx, float *weights, void *workspace,
+                             size_t workspace_bytes, void *stream);
+int kd_rasterize_forward_f64(int batch, int height, int width, int64_t num_faces, int feat_dim,
+                             const double *fvz, const double *fvi, const double *feat,
+                             const uint8_t *valid, double multiplier, float eps, double *interp,
+                             int64_t *face_idx, double *weights, void *workspace,
+                             size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rasterize backward, general form.  Replaces _C.render.mesh.rasterize_backward_cuda
+ * (bindings.cpp:78 -> rasterization.cpp:106-168, kernel rasterization_cuda.cu:238-402).  Any
+ * face_idx is accepted (original index, -1 = none).  fvi is NOT scaled.  grad_feat may be NULL.
+ * Float atomics: the summation order, hence the last bits, vary run to run (as in the reference).
+ * ------------------------------------------------------------------------------------------- */
+int kd_rasterize_backward_f32(int batch, int height, int width, int64_t num_faces, int feat_dim,
+                              const float *grad_interp, const int64_t *face_idx,
+                              const float *weights, const float *fvi, const float *feat,
+                              float eps, float *grad_fvi, float *grad_feat, void *stream);
+int kd_rasterize_backward_f64(int batch, int height, int width, int64_t num_faces, int feat_dim,
+                              const double *grad_interp, const int64_t *face_idx,
+                              const double *weights, const double *fvi, const double *feat,
+                              float eps, double *grad_fvi, double *grad_feat, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rasterize backward, face-gather form (deterministic, no atomics): each face sums the pixels of
+ * its own pixel footprint.  Valid only for a face_idx produced by kd_rasterize_forward_* with the
+ * same fvi / valid / multiplier (every pixel of face f lies inside f's bounding box); this is the
+ * autograd path of rasterize().  Same math as kd_rasterize_backward_*.  grad_feat may be NULL.
+ * ------------------------------------------------------------------------------------------- */
+int kd_rasterize_backward_gather_f32(int batch, int height, int width, int64_t num_faces,
+                                     int feat_dim, const float *grad_interp,
+                                     const int64_t *face_idx, const float *weights,
+                                     const float *fvi, const float *feat, const uint8_t *valid,
+                                     double multiplier, float eps, float *grad_fvi,
+                                     float *grad_feat, void *workspace, size_t workspace_bytes,
+                                     void *stream);
+int kd_rasterize_backward_gather_f64(int batch, int height, int width, int64_t num_faces,
+                                     int feat_dim, const double *grad_interp,
+                                     const int64_t *face_idx, const double *weights,
+                                     const double *fvi, const double *feat, const uint8_t *valid,
+                                     double multiplier, float eps, double *grad_fvi,
+                                     double *grad_feat, void *workspace, size_t workspace_bytes,
+                                     void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * DIB-R soft mask forward.  Replaces _C.render.mesh.dibr_soft_mask_forward_cuda
+ * (bindings.cpp:79 -> kaolin/csrc/render/mesh/dibr_soft_mask.cpp:48-108, kernel
+ * dibr_soft_mask_cuda.cu:27-184).  fvi_scaled = fvi * multiplier, large_bboxes (B, F, 4) as
+ * computed by DibrSoftMaskCuda.forward (dibr.py:31-39).  face_idx (B, H, W): >= 0 = covered.
+ * close_face_idx receives the face index within the view, -1 padded.
+ * ------------------------------------------------------------------------------------------- */
+int kd_dibr_soft_mask_forward_f32(int batch, int height, int width, int64_t num_faces, int knum,
+                                  const float *fvi_scaled, const float *large_bboxes,
+                                  const int64_t *face_idx, float sigmainv, float multiplier,
+                                  float *soft_mask, float *close_face_prob,
+                                  int64_t *close_face_idx, uint8_t *close_face_dist_type,
+                                  void *workspace, size_t workspace_bytes, void *stream);
+int kd_dibr_soft_mask_forward_f64(int batch, int height, int width, int64_t num_faces, int knum,
+                                  const double *fvi_scaled, const double *large_bboxes,
+                                  const int64_t *face_idx, float sigmainv, float multiplier,
+                                  double *soft_mask, double *close_face_prob,
+                                  int64_t *close_face_idx, uint8_t *close_face_dist_type,
+                                  void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * DIB-R soft mask forward from UNSCALED fvi (DibrSoftMaskCuda.forward dibr.py:29-55 fused: the
+ * x multiplier and the +-boxlen*multiplier bounding boxes are computed in the kernel).
+ * close_last (B, H, W) int32 receives, per uncovered pixel, the K-th close face when the list is
+ * full, else -1 (what kd_dibr_soft_mask_backward_gather_* needs).  The three close_face_* lists
+ * may all be NULL (then they are not materialised); close_last may be NULL.
+ * ------------------------------------------------------------------------------------------- */
+int kd_dibr_soft_mask_forward_fused_f32(int batch, int height, int width, int64_t num_faces,
+                                        int knum, const float *fvi, double multiplier,
+                                        double boxlen, const int64_t *face_idx, float sigmainv,
+                                        float *soft_mask, float *close_face_prob,
+                                        int64_t *close_face_idx, uint8_t *close_face_dist_type,
+                                        int32_t *close_last, void *workspace,
+                                        size_t workspace_bytes, void *stream);
+int kd_dibr_soft_mask_forward_fused_f64(int batch, int height, int width, int64_t num_faces,
+                                        int knum, const double *fvi, double multiplier,
+                                        double boxlen, const int64_t *face_idx, float sigmainv,
+                                        double *soft_mask, double *close_face_prob,
+                                        int64_t *close_face_idx, uint8_t *close_face_dist_type,
+                                        int32_t *close_last, void *workspace,
+                                        size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * DIB-R soft mask backward, general form.  Replaces _C.render.mesh.dibr_soft_mask_backward_cuda
+ * (bindings.cpp:80 -> dibr_soft_mask.cpp:110-183, kernel dibr_soft_mask_cuda.cu:230-353).
+ * Returns the gradient w.r.t. the unscaled coordinates, like the reference op.  Float atomics.
+ * ------------------------------------------------------------------------------------------- */
+int kd_dibr_soft_mask_backward_f32(int batch, int height, int width, int64_t num_faces, int knum,
+                                   const float *grad_soft_mask, const float *soft_mask,
+                                   const int64_t *face_idx, const float *close_face_prob,
+                                   const int64_t *close_face_idx,
+                                   const uint8_t *close_face_dist_type, const float *fvi_scaled,
+                                   float sigmainv, float multiplier, float *grad_fvi,
+                                   void *stream);
+int kd_dibr_soft_mask_backward_f64(int batch, int height, int width, int64_t num_faces, int knum,
+                                   const double *grad_soft_mask, const double *soft_mask,
+                                   const int64_t *face_idx, const double *close_face_prob,
+                                   const int64_t *close_face_idx,
+                                   const uint8_t *close_face_dist_type, const double *fvi_scaled,
+                                   float sigmainv, float multiplier, double *grad_fvi,
+                                   void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * DIB-R soft mask backward, face-gather form (deterministic, no atomics, no close lists): each
+ * face re-derives, for the uncovered pixels of its enlarged box, whether it is among the pixel's
+ * first K close faces (close_last from the fused forward) and its distance type / probability
+ * (bit-identical recomputation), and sums its own gradient.  Same math as the general form.
+ * ------------------------------------------------------------------------------------------- */
+int kd_dibr_soft_mask_backward_gather_f32(int batch, int height, int width, int64_t num_faces,
+                                          const float *grad_soft_mask, const float *soft_mask,
+                                          const int64_t *face_idx, const int32_t *close_last,
+                                          const float *fvi, double multiplier, double boxlen,
+                                          float sigmainv, float *grad_fvi, void *workspace,
+                                          size_t workspace_bytes, void *stream);
+int kd_dibr_soft_mask_backward_gather_f64(int batch, int height, int width, int64_t num_faces,
+                                          const double *grad_soft_mask, const double *soft_mask,
+                                          const int64_t *face_idx, const int32_t *close_last,
+                                          const double *fvi, double multiplier, double boxlen,
+                                          float sigmainv, double *grad_fvi, void *workspace,
+                                          size_t workspace_bytes, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KAOLIN_DIBR_H_ */

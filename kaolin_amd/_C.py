@@ -1,0 +1,328 @@
+"""Drop-in for the reference's native module ``kaolin._C.render.mesh`` (hot path only).
+
+Reference binding: kaolin/csrc/bindings.cpp:75-80.  Same four function names, positional
+signatures, return tuples, output allocation and error class (RuntimeError) as the reference
+wrappers kaolin/csrc/render/mesh/rasterization.cpp:49-168 and dibr_soft_mask.cpp:48-183.
+Each call validates its arguments like ``at::checkAllSameGPU`` / ``checkAllContiguous`` /
+``checkSize``, allocates the outputs with ``torch.empty`` (the kernels write every element, so the
+reference's ``at::full(-1)`` / ``at::zeros`` pre-fills are not needed) and launches on the
+current HIP stream of the inputs' device.
+
+Extra entry points (used by kaolin_amd.render.mesh's autograd functions, not in the reference):
+``rasterize_forward_fused``, ``rasterize_backward_gather``, ``dibr_soft_mask_forward_fused``,
+``dibr_soft_mask_backward_gather``.
+"""
+import types
+
+import torch
+
+from . import _lib
+
+_SFX = {torch.float32: 'f32', torch.float64: 'f64'}
+
+
+def _sfx(t, fname):
+    try:
+        return _SFX[t.dtype]
+    except KeyError:
+        raise RuntimeError(f'"{fname}" not implemented for \'{t.dtype}\'') from None
+
+
+def _check_same_gpu(fname, **tensors):
+    dev = None
+    for name, t in tensors.items():
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError(f'{fname}: expected tensor for argument "{name}" to be on a GPU '
+                               f'(got {t.device})')
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise RuntimeError(f'{fname}: expected all tensors to be on the same GPU, but found '
+                               f'{dev} and {t.device} (argument "{name}")')
+    return dev
+
+
+def _check_contiguous(fname, **tensors):
+    for name, t in tensors.items():
+        if t is not None and not t.is_contiguous():
+            raise RuntimeError(f'{fname}: expected contiguous tensor for argument "{name}"')
+
+
+def _check_size(fname, name, t, size):
+    if tuple(t.shape) != tuple(size):
+        raise RuntimeError(f'{fname}: expected tensor for argument "{name}" to have size '
+                           f'{list(size)}, but got {list(t.shape)}')
+
+
+def _check_dtype(fname, ref, **tensors):
+    for name, t in tensors.items():
+        if t is not None and t.dtype != ref.dtype:
+            raise RuntimeError(f'{fname}: expected {name} to have dtype {ref.dtype}, '
+                               f'got {t.dtype}')
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _workspace(kind, dev, B, H, W, n_total, max_per_view):
+    nb = _lib.workspace_size(kind, B, H, W, n_total, max_per_view)
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+    return ws, nb
+
+
+# -------------------------------------------------------------------------------------------
+# the reference's four operators
+# -------------------------------------------------------------------------------------------
+def packed_rasterize_forward_cuda(height, width, face_vertices_z, face_vertices_image,
+                                  face_bboxes, face_features, first_idx_face_per_mesh,
+                                  multiplier, eps):
+    """rasterization.cpp:49-104 -> [interpolated_features, selected_face_idx, output_weights]"""
+    fn = 'packed_rasterize_forward_cuda'
+    dev = _check_same_gpu(fn, face_vertices_z=face_vertices_z,
+                          face_vertices_image=face_vertices_image, face_bboxes=face_bboxes,
+                          face_features=face_features,
+                          first_idx_face_per_mesh=first_idx_face_per_mesh)
+    _check_contiguous(fn, face_vertices_z=face_vertices_z,
+                      face_vertices_image=face_vertices_image, face_bboxes=face_bboxes,
+                      face_features=face_features,
+                      first_idx_face_per_mesh=first_idx_face_per_mesh)
+    num_faces = face_vertices_z.shape[0]
+    batch_size = first_idx_face_per_mesh.shape[0] - 1
+    feat_dim = face_features.shape[2]
+    _check_size(fn, 'face_vertices_z', face_vertices_z, (num_faces, 3))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (num_faces, 3, 2))
+    _check_size(fn, 'face_bboxes', face_bboxes, (num_faces, 4))
+    _check_size(fn, 'face_features', face_features, (num_faces, 3, feat_dim))
+    _check_size(fn, 'first_idx_face_per_mesh', first_idx_face_per_mesh, (batch_size + 1,))
+    sfx = _sfx(face_vertices_z, fn)
+    _check_dtype(fn, face_vertices_z, face_vertices_image=face_vertices_image,
+                 face_bboxes=face_bboxes, face_features=face_features)
+    if first_idx_face_per_mesh.dtype != torch.int64:
+        raise RuntimeError(f'{fn}: first_idx_face_per_mesh must be int64')
+    opts = dict(device=dev, dtype=face_vertices_z.dtype)
+    interp = torch.empty((batch_size, height, width, feat_dim), **opts)
+    face_idx = torch.empty((batch_size, height, width), device=dev, dtype=torch.long)
+    weights = torch.empty((batch_size, height, width, 3), **opts)
+    ws, nb = _workspace(_lib.KD_WS_RASTER_PACKED, dev, batch_size, height, width, num_faces,
+                        num_faces)
+    _lib.call(f'kd_packed_rasterize_forward_{sfx}', batch_size, height, width, num_faces,
+              feat_dim, _ptr(face_vertices_z), _ptr(face_vertices_image), _ptr(face_bboxes),
+              _ptr(face_features), _ptr(first_idx_face_per_mesh), float(multiplier), float(eps),
+              _ptr(interp), _ptr(face_idx), _ptr(weights), _ptr(ws), nb, _stream(dev))
+    return [interp, face_idx, weights]
+
+
+def rasterize_backward_cuda(grad_interpolated_features, interpolated_features,
+                            selected_face_idx, output_weights, face_vertices_image,
+                            face_features, eps):
+    """rasterization.cpp:106-168 -> [grad_face_vertices_image, grad_face_features]"""
+    fn = 'rasterize_backward_cuda'
+    dev = _check_same_gpu(fn, grad_interpolated_features=grad_interpolated_features,
+                          interpolated_features=interpolated_features,
+                          selected_face_idx=selected_face_idx, output_weights=output_weights,
+                          face_vertices_image=face_vertices_image, face_features=face_features)
+    _check_contiguous(fn, grad_interpolated_features=grad_interpolated_features,
+                      interpolated_features=interpolated_features,
+                      selected_face_idx=selected_face_idx, output_weights=output_weights,
+                      face_vertices_image=face_vertices_image, face_features=face_features)
+    B, H, W, D = grad_interpolated_features.shape
+    F = face_vertices_image.shape[1]
+    _check_size(fn, 'interpolated_features', interpolated_features, (B, H, W, D))
+    _check_size(fn, 'selected_face_idx', selected_face_idx, (B, H, W))
+    _check_size(fn, 'output_weights', output_weights, (B, H, W, 3))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'face_features', face_features, (B, F, 3, D))
+    sfx = _sfx(grad_interpolated_features, fn)
+    _check_dtype(fn, grad_interpolated_features, output_weights=output_weights,
+                 face_vertices_image=face_vertices_image, face_features=face_features)
+    gfvi = torch.empty_like(face_vertices_image)
+    gfeat = torch.empty_like(face_features)
+    _lib.call(f'kd_rasterize_backward_{sfx}', B, H, W, F, D, _ptr(grad_interpolated_features),
+              _ptr(selected_face_idx), _ptr(output_weights), _ptr(face_vertices_image),
+              _ptr(face_features), float(eps), _ptr(gfvi), _ptr(gfeat), _stream(dev))
+    return [gfvi, gfeat]
+
+
+def dibr_soft_mask_forward_cuda(face_vertices_image, face_large_bboxes, selected_face_idx,
+                                sigmainv, knum, multiplier):
+    """dibr_soft_mask.cpp:48-108 ->
+    [soft_mask, close_face_prob, close_face_idx, close_face_dist_type]"""
+    fn = 'dibr_soft_mask_forward_cuda'
+    dev = _check_same_gpu(fn, face_vertices_image=face_vertices_image,
+                          face_large_bboxes=face_large_bboxes,
+                          selected_face_idx=selected_face_idx)
+    _check_contiguous(fn, face_vertices_image=face_vertices_image,
+                      face_large_bboxes=face_large_bboxes, selected_face_idx=selected_face_idx)
+    B, F = face_vertices_image.shape[:2]
+    H, W = selected_face_idx.shape[1:3]
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'face_bboxes', face_large_bboxes, (B, F, 4))
+    _check_size(fn, 'selected_face_idx', selected_face_idx, (B, H, W))
+    sfx = _sfx(face_vertices_image, fn)
+    _check_dtype(fn, face_vertices_image, face_large_bboxes=face_large_bboxes)
+    knum = int(knum)
+    if knum < 1:
+        raise RuntimeError(f'{fn}: knum must be >= 1, got {knum}')
+    opts = dict(device=dev, dtype=face_vertices_image.dtype)
+    soft = torch.empty((B, H, W), **opts)
+    prob = torch.empty((B, H, W, knum), **opts)
+    cidx = torch.empty((B, H, W, knum), device=dev, dtype=torch.long)
+    ctype = torch.empty((B, H, W, knum), device=dev, dtype=torch.uint8)
+    ws, nb = _workspace(_lib.KD_WS_SOFT_MASK, dev, B, H, W, B * F, F)
+    _lib.call(f'kd_dibr_soft_mask_forward_{sfx}', B, H, W, F, knum, _ptr(face_vertices_image),
+              _ptr(face_large_bboxes), _ptr(selected_face_idx), float(sigmainv),
+              float(multiplier), _ptr(soft), _ptr(prob), _ptr(cidx), _ptr(ctype), _ptr(ws), nb,
+              _stream(dev))
+    return [soft, prob, cidx, ctype]
+
+
+def dibr_soft_mask_backward_cuda(grad_soft_mask, soft_mask, selected_face_idx, close_face_prob,
+                                 close_face_idx, close_face_dist_type, face_vertices_image,
+                                 sigmainv, multiplier):
+    """dibr_soft_mask.cpp:110-183 -> grad_face_vertices_image"""
+    fn = 'dibr_soft_mask_backward_cuda'
+    dev = _check_same_gpu(fn, grad_soft_mask=grad_soft_mask, soft_mask=soft_mask,
+                          close_face_idx=close_face_idx,
+                          close_face_dist_type=close_face_dist_type,
+                          close_face_prob=close_face_prob,
+                          face_vertices_image=face_vertices_image)
+    _check_contiguous(fn, grad_soft_mask=grad_soft_mask, soft_mask=soft_mask,
+                      close_face_prob=close_face_prob, close_face_idx=close_face_idx,
+                      close_face_dist_type=close_face_dist_type,
+                      face_vertices_image=face_vertices_image)
+    B, F = face_vertices_image.shape[:2]
+    H, W = selected_face_idx.shape[1:3]
+    K = close_face_idx.shape[-1]
+    _check_size(fn, 'grad_soft_mask', grad_soft_mask, (B, H, W))
+    _check_size(fn, 'soft_mask', soft_mask, (B, H, W))
+    _check_size(fn, 'selected_face_idx', selected_face_idx, (B, H, W))
+    _check_size(fn, 'close_face_prob', close_face_prob, (B, H, W, K))
+    _check_size(fn, 'close_face_idx', close_face_idx, (B, H, W, K))
+    _check_size(fn, 'close_face_dist_type', close_face_dist_type, (B, H, W, K))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    sfx = _sfx(face_vertices_image, fn)
+    _check_dtype(fn, face_vertices_image, grad_soft_mask=grad_soft_mask, soft_mask=soft_mask,
+                 close_face_prob=close_face_prob)
+    selected_face_idx = selected_face_idx.contiguous()
+    g = torch.empty_like(face_vertices_image)
+    _lib.call(f'kd_dibr_soft_mask_backward_{sfx}', B, H, W, F, K, _ptr(grad_soft_mask),
+              _ptr(soft_mask), _ptr(selected_face_idx), _ptr(close_face_prob),
+              _ptr(close_face_idx), _ptr(close_face_dist_type), _ptr(face_vertices_image),
+              float(sigmainv), float(multiplier), _ptr(g), _stream(dev))
+    return g
+
+
+# -------------------------------------------------------------------------------------------
+# fused entry points used by the autograd functions of kaolin_amd.render.mesh
+# -------------------------------------------------------------------------------------------
+def rasterize_forward_fused(height, width, face_vertices_z, face_vertices_image, face_features,
+                            valid_faces, multiplier, eps):
+    """RasterizeCuda.forward (rasterization.py:289-369) with packing / scaling / bbox / remap in
+    the kernel.  Inputs contiguous (B,F,3), (B,F,3,2), (B,F,3,D); valid_faces (B,F) bool/uint8 or
+    None.  Returns (interp, face_idx [original index], weights)."""
+    fn = 'rasterize'
+    dev = _check_same_gpu(fn, face_vertices_z=face_vertices_z,
+                          face_vertices_image=face_vertices_image, face_features=face_features,
+                          valid_faces=valid_faces)
+    B, F = face_vertices_z.shape[:2]
+    D = face_features.shape[-1]
+    _check_size(fn, 'face_vertices_z', face_vertices_z, (B, F, 3))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'face_features', face_features, (B, F, 3, D))
+    sfx = _sfx(face_vertices_z, fn)
+    _check_dtype(fn, face_vertices_z, face_vertices_image=face_vertices_image,
+                 face_features=face_features)
+    if valid_faces is not None:
+        _check_size(fn, 'valid_faces', valid_faces, (B, F))
+        valid_faces = valid_faces.contiguous()
+        if valid_faces.dtype != torch.uint8:
+            valid_faces = valid_faces.to(torch.uint8) if valid_faces.dtype != torch.bool \
+                else valid_faces.view(torch.uint8)
+    opts = dict(device=dev, dtype=face_vertices_z.dtype)
+    interp = torch.empty((B, height, width, D), **opts)
+    face_idx = torch.empty((B, height, width), device=dev, dtype=torch.long)
+    weights = torch.empty((B, height, width, 3), **opts)
+    ws, nb = _workspace(_lib.KD_WS_RASTER, dev, B, height, width, B * F, F)
+    _lib.call(f'kd_rasterize_forward_{sfx}', B, height, width, F, D, _ptr(face_vertices_z),
+              _ptr(face_vertices_image), _ptr(face_features), _ptr(valid_faces),
+              float(multiplier), float(eps), _ptr(interp), _ptr(face_idx), _ptr(weights),
+              _ptr(ws), nb, _stream(dev))
+    return interp, face_idx, weights, valid_faces
+
+
+def rasterize_backward_gather(grad_interp, face_idx, weights, face_vertices_image,
+                              face_features, valid_faces, multiplier, eps, need_feat=True):
+    dev = grad_interp.device
+    B, H, W, D = grad_interp.shape
+    F = face_vertices_image.shape[1]
+    sfx = _sfx(face_vertices_image, 'rasterize_backward')
+    gfvi = torch.empty_like(face_vertices_image)
+    gfeat = torch.empty_like(face_features) if need_feat else None
+    _lib.call(f'kd_rasterize_backward_gather_{sfx}', B, H, W, F, D, _ptr(grad_interp),
+              _ptr(face_idx), _ptr(weights), _ptr(face_vertices_image), _ptr(face_features),
+              _ptr(valid_faces), float(multiplier), float(eps), _ptr(gfvi), _ptr(gfeat), None, 0,
+              _stream(dev))
+    return gfvi, gfeat
+
+
+def dibr_soft_mask_forward_fused(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum,
+                                 multiplier, with_lists=False):
+    """DibrSoftMaskCuda.forward (dibr.py:29-55) with the x multiplier and the enlarged boxes in
+    the kernel.  Returns (soft, close_last, prob, cidx, ctype) (lists None unless with_lists)."""
+    fn = 'dibr_soft_mask'
+    dev = _check_same_gpu(fn, face_vertices_image=face_vertices_image,
+                          selected_face_idx=selected_face_idx)
+    B, F = face_vertices_image.shape[:2]
+    H, W = selected_face_idx.shape[1:3]
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'selected_face_idx', selected_face_idx, (B, H, W))
+    sfx = _sfx(face_vertices_image, fn)
+    knum = int(knum)
+    if knum < 1:
+        raise RuntimeError(f'{fn}: knum must be >= 1, got {knum}')
+    opts = dict(device=dev, dtype=face_vertices_image.dtype)
+    soft = torch.empty((B, H, W), **opts)
+    last = torch.empty((B, H, W), device=dev, dtype=torch.int32)
+    prob = cidx = ctype = None
+    if with_lists:
+        prob = torch.empty((B, H, W, knum), **opts)
+        cidx = torch.empty((B, H, W, knum), device=dev, dtype=torch.long)
+        ctype = torch.empty((B, H, W, knum), device=dev, dtype=torch.uint8)
+    ws, nb = _workspace(_lib.KD_WS_SOFT_MASK, dev, B, H, W, B * F, F)
+    _lib.call(f'kd_dibr_soft_mask_forward_fused_{sfx}', B, H, W, F, knum,
+              _ptr(face_vertices_image), float(multiplier), float(boxlen),
+              _ptr(selected_face_idx), float(sigmainv), _ptr(soft), _ptr(prob), _ptr(cidx),
+              _ptr(ctype), _ptr(last), _ptr(ws), nb, _stream(dev))
+    return soft, last, prob, cidx, ctype
+
+
+def dibr_soft_mask_backward_gather(grad_soft, soft, selected_face_idx, close_last,
+                                   face_vertices_image, multiplier, boxlen, sigmainv):
+    dev = grad_soft.device
+    B, F = face_vertices_image.shape[:2]
+    H, W = selected_face_idx.shape[1:3]
+    sfx = _sfx(face_vertices_image, 'dibr_soft_mask_backward')
+    g = torch.empty_like(face_vertices_image)
+    _lib.call(f'kd_dibr_soft_mask_backward_gather_{sfx}', B, H, W, F, _ptr(grad_soft), _ptr(soft),
+              _ptr(selected_face_idx), _ptr(close_last), _ptr(face_vertices_image),
+              float(multiplier), float(boxlen), float(sigmainv), _ptr(g), None, 0, _stream(dev))
+    return g
+
+
+render = types.SimpleNamespace(mesh=types.SimpleNamespace(
+    packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
+    rasterize_backward_cuda=rasterize_backward_cuda,
+    dibr_soft_mask_forward_cuda=dibr_soft_mask_forward_cuda,
+    dibr_soft_mask_backward_cuda=dibr_soft_mask_backward_cuda,
+    rasterize_forward_fused=rasterize_forward_fused,
+    rasterize_backward_gather=rasterize_backward_gather,
+    dibr_soft_mask_forward_fused=dibr_soft_mask_forward_fused,
+    dibr_soft_mask_backward_gather=dibr_soft_mask_backward_gather,
+))

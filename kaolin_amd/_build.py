@@ -1,0 +1,67 @@
+"""Builds kaolin_amd/lib/libkaolin_dibr.so (the C-ABI library, HIP for gfx950) in-tree.
+
+hipcc cross-compiles for gfx950 without a GPU.  Flags that are part of the numerics contract:
+  -ffp-contract=off  no FMA contraction (the reference expressions are evaluated as written)
+  no -ffast-math, no -fgpu-flush-denormals-to-zero
+"""
+import concurrent.futures
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, 'csrc')
+LIBDIR = os.path.join(PKG, 'lib')
+LIB = os.path.join(LIBDIR, 'libkaolin_dibr.so')
+OBJDIR = os.path.join(PKG, 'build')
+
+SOURCES = ['kd_capi.cpp', 'kd_binning.hip', 'kd_raster.hip', 'kd_softmask.hip']
+HEADERS = ['kd_common.hpp', 'kd_binning.hpp', 'kd_capi.hpp']
+ARCH = os.environ.get('KAOLIN_AMD_ARCH', 'gfx950')
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', f'--offload-arch={ARCH}',
+         '-Wall', '-Wno-unused-function', '-Wno-unused-result']
+
+
+def _stale(target, deps):
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def _compile(src):
+    path = os.path.join(CSRC, src)
+    obj = os.path.join(OBJDIR, src + '.o')
+    deps = [path, os.path.join(ROOT, 'include', 'kaolin_dibr.h')] + \
+        [os.path.join(CSRC, h) for h in HEADERS]
+    if _stale(obj, deps):
+        lang = ['-x', 'hip'] if src.endswith('.cpp') else []
+        cmd = [HIPCC, *FLAGS, *lang, '-c', path, '-o', obj + '.tmp']
+        subprocess.check_call(cmd)
+        os.replace(obj + '.tmp', obj)
+    return obj
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OBJDIR, exist_ok=True)
+    os.makedirs(LIBDIR, exist_ok=True)
+    if force:
+        for s in SOURCES:
+            o = os.path.join(OBJDIR, s + '.o')
+            if os.path.exists(o):
+                os.remove(o)
+    with concurrent.futures.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(_compile, SOURCES))
+    if force or _stale(LIB, objs):
+        tmp = LIB + f'.{os.getpid()}.tmp'
+        subprocess.check_call([HIPCC, '-shared', f'--offload-arch={ARCH}', *objs, '-o', tmp])
+        os.replace(tmp, LIB)
+        if verbose:
+            print(f'[kaolin_amd] built {LIB}', file=sys.stderr)
+    return LIB
+
+
+if __name__ == '__main__':
+    build(force='--force' in sys.argv)

@@ -1,0 +1,90 @@
+"""ctypes binding of the C ABI in include/kaolin_dibr.h (kaolin_amd/lib/libkaolin_dibr.so).
+
+The library is loaded from the package tree (never from site-packages).  There is no fallback:
+if the library is missing or a call fails, a RuntimeError is raised.
+"""
+import ctypes
+import os
+import re
+import threading
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, 'lib', 'libkaolin_dibr.so')
+HEADER = os.path.join(os.path.dirname(_PKG), 'include', 'kaolin_dibr.h')
+
+KD_OK = 0
+KD_WS_RASTER_PACKED = 1
+KD_WS_RASTER = 2
+KD_WS_SOFT_MASK = 3
+KD_WS_GATHER_BWD = 4
+
+_lib = None
+_lock = threading.Lock()
+
+c_int, c_float, c_double, c_i64, c_size, c_p = (ctypes.c_int, ctypes.c_float, ctypes.c_double,
+                                                ctypes.c_int64, ctypes.c_size_t, ctypes.c_void_p)
+
+# argument signatures (everything pointer-like is c_void_p)
+_SIGS = {
+    'kd_packed_rasterize_forward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
+                                    c_float, c_float, c_p, c_p, c_p, c_p, c_size, c_p],
+    'kd_rasterize_forward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_double,
+                             c_float, c_p, c_p, c_p, c_p, c_size, c_p],
+    'kd_rasterize_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
+                              c_float, c_p, c_p, c_p],
+    'kd_rasterize_backward_gather': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
+                                     c_p, c_double, c_float, c_p, c_p, c_p, c_size, c_p],
+    'kd_dibr_soft_mask_forward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_float,
+                                  c_float, c_p, c_p, c_p, c_p, c_p, c_size, c_p],
+    'kd_dibr_soft_mask_forward_fused': [c_int, c_int, c_int, c_i64, c_int, c_p, c_double,
+                                        c_double, c_p, c_float, c_p, c_p, c_p, c_p, c_p, c_p,
+                                        c_size, c_p],
+    'kd_dibr_soft_mask_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
+                                   c_p, c_p, c_float, c_float, c_p, c_p],
+    'kd_dibr_soft_mask_backward_gather': [c_int, c_int, c_int, c_i64, c_p, c_p, c_p, c_p, c_p,
+                                          c_double, c_double, c_float, c_p, c_p, c_size, c_p],
+}
+
+
+def load():
+    """Load (once) and return the ctypes library; raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f'kaolin_amd: native library {LIB_PATH} is missing; build it with '
+                    f'`python -c "import __graft_entry__ as g; g.build()"` (hipcc, gfx950)')
+            lib = ctypes.CDLL(LIB_PATH)
+            lib.kd_workspace_size.argtypes = [c_int, c_int, c_int, c_int, c_i64, c_i64]
+            lib.kd_workspace_size.restype = c_size
+            lib.kd_last_error.argtypes = []
+            lib.kd_last_error.restype = ctypes.c_char_p
+            lib.kd_version.restype = c_int
+            for base, sig in _SIGS.items():
+                for sfx in ('f32', 'f64'):
+                    fn = getattr(lib, f'{base}_{sfx}')
+                    fn.argtypes = sig
+                    fn.restype = c_int
+            _lib = lib
+    return _lib
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    if rc != KD_OK:
+        msg = load().kd_last_error().decode(errors='replace')
+        raise RuntimeError(f'{name} failed ({rc}): {msg}')
+
+
+def workspace_size(kind, B, H, W, n_total, max_per_view):
+    return int(load().kd_workspace_size(kind, B, H, W, n_total, max_per_view))
+
+
+def declared_symbols():
+    """Every function name declared in include/kaolin_dibr.h."""
+    with open(HEADER) as f:
+        text = f.read()
+    return sorted(set(re.findall(r'\b(kd_[a-z0-9_]+)\s*\(', text)))

@@ -1,0 +1,263 @@
+// kd_common.hpp -- shared device/host helpers for the gfx950 DIB-R kernels.
+//
+// Numerics contract: every kernel is compiled with -ffp-contract=off and
+// without fast-math, so `a*b - c*d` is two rounded products and a rounded difference, exactly as
+// the reference expressions are written (and as the C oracle evaluates them); fp32 division is
+// IEEE correctly rounded (hipcc default); pixel centres are computed in fp32 even for fp64 data
+// (rasterization_cuda.cu:85-86, dibr_soft_mask_cuda.cu:75-76).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cmath>
+
+namespace kd {
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;      // 4 waves
+constexpr int kTile = 16;        // fine tile: 16x16 pixels per workgroup, 8x8 per wave
+constexpr int kChunk = 256;      // faces per binning workgroup
+constexpr int kMaxCtiles = 1024; // coarse tiles per view (LDS bound of the binning kernels)
+
+// ------------------------------------------------------------------------------------------
+// pixel centres, identical to the reference expression `multiplier / width * (2*w + 1 - width)`
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float px_cx(float M, int W, int w) {
+  return M / (float)W * (float)(2 * w + 1 - W);
+}
+__device__ __forceinline__ float px_cy(float M, int H, int h) {
+  return M / (float)H * (float)(H - 2 * h - 1);
+}
+
+// NaN-propagating min / max of three (torch.min / torch.max over a dim propagate NaN).
+template <typename T>
+__device__ __forceinline__ T nmin3(T a, T b, T c) {
+  T m = (b < a || isnan(b)) ? b : a;
+  if (isnan(m)) return m;
+  return (c < m || isnan(c)) ? c : m;
+}
+template <typename T>
+__device__ __forceinline__ T nmax3(T a, T b, T c) {
+  T m = (b > a || isnan(b)) ? b : a;
+  if (isnan(m)) return m;
+  return (c > m || isnan(c)) ? c : m;
+}
+
+// ------------------------------------------------------------------------------------------
+// Exact pixel span of a half-open box test.  The reference rejects a pixel when
+//   x0 < xmin || x0 >= xmax || y0 < ymin || y0 >= ymax
+// with x0 / y0 the fp32 centres widened to T.  Centres are monotone in the pixel index, so the
+// accepted pixels form [a, b] x [c, d]; a NaN bound rejects nothing on its side (every
+// comparison with NaN is false), exactly like the reference.  Estimate in double, then settle
+// the boundary with the exact centre formula.
+// ------------------------------------------------------------------------------------------
+struct Span {
+  short x0, x1, y0, y1;  // inclusive; empty when x0 > x1 or y0 > y1
+};
+
+template <typename T>
+__device__ inline void span_x(T lo, T hi, float M, int W, int &a, int &b) {
+  const float s = M / (float)W;
+  if (!(s > 0.f) || !isfinite(s)) {  // degenerate multiplier: be conservative
+    a = 0;
+    b = W - 1;
+    return;
+  }
+  if (isnan(lo)) {
+    a = 0;
+  } else {
+    double t = ((double)lo / (double)s + (double)(W - 1)) * 0.5;
+    t = fmin(fmax(t, -1.0), (double)W);
+    a = (int)ceil(t);
+    a = a < 0 ? 0 : (a > W ? W : a);
+    while (a > 0 && (T)px_cx(M, W, a - 1) >= lo) --a;
+    while (a < W && (T)px_cx(M, W, a) < lo) ++a;
+  }
+  if (isnan(hi)) {
+    b = W - 1;
+  } else {
+    double t = ((double)hi / (double)s + (double)(W - 1)) * 0.5;
+    t = fmin(fmax(t, -1.0), (double)W + 1.0);
+    b = (int)ceil(t) - 1;
+    b = b < -1 ? -1 : (b > W - 1 ? W - 1 : b);
+    while (b < W - 1 && (T)px_cx(M, W, b + 1) < hi) ++b;
+    while (b >= 0 && (T)px_cx(M, W, b) >= hi) --b;
+  }
+}
+
+template <typename T>
+__device__ inline void span_y(T lo, T hi, float M, int H, int &c, int &d) {
+  const float s = M / (float)H;
+  if (!(s > 0.f) || !isfinite(s)) {
+    c = 0;
+    d = H - 1;
+    return;
+  }
+  // rows accepted: !(cy < lo) && !(cy >= hi); cy decreases with h.
+  if (isnan(hi)) {
+    c = 0;
+  } else {  // first h with cy(h) < hi
+    double t = ((double)(H - 1) - (double)hi / (double)s) * 0.5;
+    t = fmin(fmax(t, -2.0), (double)H);
+    c = (int)floor(t) + 1;
+    c = c < 0 ? 0 : (c > H ? H : c);
+    while (c > 0 && (T)px_cy(M, H, c - 1) < hi) --c;
+    while (c < H && (T)px_cy(M, H, c) >= hi) ++c;
+  }
+  if (isnan(lo)) {
+    d = H - 1;
+  } else {  // last h with cy(h) >= lo
+    double t = ((double)(H - 1) - (double)lo / (double)s) * 0.5;
+    t = fmin(fmax(t, -2.0), (double)H);
+    d = (int)floor(t);
+    d = d < -1 ? -1 : (d > H - 1 ? H - 1 : d);
+    while (d < H - 1 && (T)px_cy(M, H, d + 1) >= lo) ++d;
+    while (d >= 0 && (T)px_cy(M, H, d) < lo) --d;
+  }
+}
+
+template <typename T>
+__device__ inline Span make_span(T xmin, T ymin, T xmax, T ymax, float M, int H, int W) {
+  int a, b, c, d;
+  span_x<T>(xmin, xmax, M, W, a, b);
+  span_y<T>(ymin, ymax, M, H, c, d);
+  Span s;
+  if (a > b || c > d) {
+    s.x0 = 1;
+    s.x1 = 0;
+    s.y0 = 1;
+    s.y1 = 0;
+  } else {
+    s.x0 = (short)a;
+    s.x1 = (short)b;
+    s.y0 = (short)c;
+    s.y1 = (short)d;
+  }
+  return s;
+}
+
+__device__ __forceinline__ bool span_empty(Span s) { return s.x0 > s.x1 || s.y0 > s.y1; }
+__device__ __forceinline__ bool span_overlaps(Span s, int x0, int x1, int y0, int y1) {
+  return !(s.x1 < x0 || s.x0 > x1 || s.y1 < y0 || s.y0 > y1 || span_empty(s));
+}
+
+// ------------------------------------------------------------------------------------------
+// Face sets: where the faces of view b are, how to get a face's (scaled) corners and box.
+// ------------------------------------------------------------------------------------------
+template <typename T>
+struct FaceSet {
+  int B, H, W;
+  int64_t N;                 // rows of the face arrays
+  int64_t F;                 // faces per view when first_idx == nullptr
+  const int64_t *first_idx;  // packed layout (device), or nullptr
+  const T *fvi;              // (N, 3, 2)
+  T scale;                   // corners are fvi * scale (1 for already-scaled input)
+  const T *bbox;             // (N, 4) explicit box in scaled space, or nullptr
+  T margin;                  // computed box enlarged by +-margin when has_margin
+  int has_margin;
+  const uint8_t *valid;      // (N) uint8 or nullptr
+  float M;                   // float multiplier of the pixel centres
+};
+
+template <typename T>
+__device__ __forceinline__ void view_range(const FaceSet<T> &fs, int b, int64_t &lo,
+                                           int64_t &hi) {
+  if (fs.first_idx) {
+    lo = fs.first_idx[b];
+    hi = fs.first_idx[b + 1];
+  } else {
+    lo = (int64_t)b * fs.F;
+    hi = lo + fs.F;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void load_corners(const FaceSet<T> &fs, int64_t i, T v[6]) {
+  const T *p = fs.fvi + i * 6;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) v[k] = p[k] * fs.scale;
+}
+
+// Box exactly as the reference host code builds it: min / max over the three scaled corners
+// (rasterization.py:342-344), optionally -+ boxlen*multiplier (dibr.py:34-39).
+template <typename T>
+__device__ __forceinline__ void face_box(const FaceSet<T> &fs, int64_t i, const T v[6], T box[4]) {
+  if (fs.bbox) {
+    const T *p = fs.bbox + i * 4;
+    box[0] = p[0];
+    box[1] = p[1];
+    box[2] = p[2];
+    box[3] = p[3];
+    return;
+  }
+  box[0] = nmin3(v[0], v[2], v[4]);
+  box[1] = nmin3(v[1], v[3], v[5]);
+  box[2] = nmax3(v[0], v[2], v[4]);
+  box[3] = nmax3(v[1], v[3], v[5]);
+  if (fs.has_margin) {
+    box[0] = box[0] - fs.margin;
+    box[1] = box[1] - fs.margin;
+    box[2] = box[2] + fs.margin;
+    box[3] = box[3] + fs.margin;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// wave helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ __forceinline__ int mbcnt(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+__device__ __forceinline__ int rdlane_i(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+__device__ __forceinline__ float rdlane(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double rdlane(double v, int l) {
+  const long long x = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(x & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+  return __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+}
+
+// Workgroup-wide ordered compaction (256 threads): position of this thread's item among the
+// items of lower threads, and the total.  s_cnt: 4 ints of LDS.
+__device__ __forceinline__ int wg_compact(bool pred, int *s_cnt, int &total) {
+  const uint64_t m = __ballot(pred);
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) s_cnt[w] = __popcll(m);
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / kWave; ++k) {
+    const int c = s_cnt[k];
+    off += (k < w) ? c : 0;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return pred ? off + mbcnt(m) : -1;
+}
+
+// ------------------------------------------------------------------------------------------
+// coarse-bin geometry shared by host and device
+// ------------------------------------------------------------------------------------------
+struct BinGeom {
+  int ct;        // coarse tile edge in pixels (multiple of kTile)
+  int nctx, ncty;
+  __host__ __device__ int nct() const { return nctx * ncty; }
+};
+
+__host__ __device__ inline BinGeom bin_geom(int H, int W) {
+  int m = H > W ? H : W;
+  int ct = 64;
+  while (((m + ct - 1) / ct) > 32) ct *= 2;
+  BinGeom g;
+  g.ct = ct;
+  g.nctx = (W + ct - 1) / ct;
+  g.ncty = (H + ct - 1) / ct;
+  return g;
+}
+
+}  // namespace kd

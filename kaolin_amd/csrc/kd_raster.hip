@@ -1,0 +1,522 @@
+// kd_raster.hip -- rasterize forward / backward for gfx950.
+//
+// Forward (replaces packed_rasterize_forward_cuda_kernel, rasterization_cuda.cu:43-192):
+//   one 256-thread workgroup per 16x16 pixel tile, one wave per 8x8 sub-tile.
+//   The workgroup walks its coarse bin (ascending face order), keeps the faces whose exact pixel
+//   span touches the tile (ballot compaction, order preserved) and stages their corners, depths
+//   and boxes in LDS (SoA).  Each wave then compacts the faces touching its 8x8 sub-tile and every
+//   lane (pixel) runs the reference's exact per-face test over that short list with LDS broadcast
+//   reads: the same sequence of faces the reference visits, minus faces whose box provably
+//   misses the pixel, so face_idx / weights / features are bit-identical.
+// Backward:
+//   kd_raster_bwd_atomic  -- general form (any face_idx), one thread per pixel, float atomics,
+//                            the per-pixel vertex terms summed over features in registers first.
+//   kd_raster_bwd_gather  -- autograd form: one thread per face sums the pixels of its own exact
+//                            pixel span (deterministic, no atomics, writes every output).
+#include "../../include/kaolin_dibr.h"
+#include "kd_binning.hpp"
+#include "kd_capi.hpp"
+
+namespace kd {
+
+template <typename T>
+struct RasterFwdArgs {
+  FaceSet<T> fs;
+  BinBuffers bb;
+  const T *fvz;
+  const T *feat;
+  int D;
+  float eps;
+  T *interp;
+  int64_t *face_idx;
+  T *weights;
+};
+
+template <typename T>
+struct RasterCap {
+  static constexpr int value = 512;
+};
+template <>
+struct RasterCap<double> {
+  static constexpr int value = 256;
+};
+
+// The reference per-face test (rasterization_cuda.cu:115-169) for one pixel.
+template <typename T>
+__device__ __forceinline__ bool raster_face_test(T x0, T y0, T ax, T ay, T bx, T by, T cx, T cy,
+                                                 T az, T bz, T cz, float eps, T &w0, T &w1,
+                                                 T &w2, T &z0) {
+  const T a_edge_x = ax - x0, a_edge_y = ay - y0;
+  const T b_edge_x = bx - x0, b_edge_y = by - y0;
+  const T c_edge_x = cx - x0, c_edge_y = cy - y0;
+  w0 = b_edge_x * c_edge_y - b_edge_y * c_edge_x;
+  w1 = c_edge_x * a_edge_y - c_edge_y * a_edge_x;
+  w2 = a_edge_x * b_edge_y - a_edge_y * b_edge_x;
+  T norm = w0 + w1 + w2;
+  norm = (T)((double)norm + copysign((double)eps, (double)norm));
+  w0 /= norm;
+  w1 /= norm;
+  w2 /= norm;
+  if (w0 < (T)0. || w1 < (T)0. || w2 < (T)0.) return false;
+  z0 = w0 * az + w1 * bz + w2 * cz;
+  return true;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
+  constexpr int CAP = RasterCap<T>::value;
+  __shared__ int s_f[CAP];
+  __shared__ Span s_span[CAP];
+  __shared__ T s_geo[13][CAP];  // ax ay bx by cx cy az bz cz xmin ymin xmax ymax
+  __shared__ unsigned short s_sub[4][CAP];
+  __shared__ int s_cnt[4];
+
+  const FaceSet<T> &fs = a.fs;
+  const int H = fs.H, W = fs.W;
+  const int b = blockIdx.y;
+  const int ntx = (W + kTile - 1) / kTile;
+  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  int64_t lo, hi;
+  view_range(fs, b, lo, hi);
+
+  const int X0 = tx * kTile, Y0 = ty * kTile;
+  const int X1 = min(X0 + kTile - 1, W - 1), Y1 = min(Y0 + kTile - 1, H - 1);
+  const int WX0 = X0 + (w & 1) * 8, WY0 = Y0 + (w >> 1) * 8;
+  const int WX1 = min(WX0 + 7, W - 1), WY1 = min(WY0 + 7, H - 1);
+  const int px = WX0 + (lane & 7), py = WY0 + (lane >> 3);
+  const bool inimg = px < W && py < H;
+  const T x0 = (T)px_cx(fs.M, W, px);
+  const T y0 = (T)px_cy(fs.M, H, py);
+
+  T max_z0 = (T)-INFINITY;
+  int best = -1;
+  T bw0 = 0., bw1 = 0., bw2 = 0.;
+
+  const BinGeom &g = a.bb.g;
+  const int ct = (Y0 / g.ct) * g.nctx + (X0 / g.ct);
+  const int n = a.bb.totals[(int64_t)b * g.nct() + ct];
+  const int *bin = a.bb.bins + (int64_t)ct * fs.N + lo;
+  const bool wave_live = WX0 < W && WY0 < H;
+
+  int cnt = 0;
+  for (int base = 0; base < n; base += kBlock) {
+    const int e = base + tid;
+    int f = 0;
+    bool ov = false;
+    Span sp;
+    if (e < n) {
+      f = bin[e];
+      sp = a.bb.spans[lo + f];
+      ov = span_overlaps(sp, X0, X1, Y0, Y1);
+    }
+    int tot;
+    const int pos = wg_compact(ov, s_cnt, tot);
+    if (ov) {
+      s_f[cnt + pos] = f;
+      s_span[cnt + pos] = sp;
+    }
+    cnt += tot;
+    if (cnt > CAP - kBlock || base + kBlock >= n) {
+      __syncthreads();
+      for (int k = tid; k < cnt; k += kBlock) {
+        const int64_t fi = lo + s_f[k];
+        T v[6], box[4];
+        load_corners(fs, fi, v);
+        face_box(fs, fi, v, box);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
+        const T *zz = a.fvz + fi * 3;
+        s_geo[6][k] = zz[0];
+        s_geo[7][k] = zz[1];
+        s_geo[8][k] = zz[2];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) s_geo[9 + q][k] = box[q];
+      }
+      int nsub = 0;
+      for (int k0 = 0; k0 < cnt; k0 += kWave) {
+        const int k = k0 + lane;
+        const bool ok = wave_live && k < cnt && span_overlaps(s_span[k], WX0, WX1, WY0, WY1);
+        const uint64_t m = __ballot(ok);
+        if (ok) s_sub[w][nsub + mbcnt(m)] = (unsigned short)k;
+        nsub += __popcll(m);
+      }
+      __syncthreads();
+      if (inimg) {
+        for (int j = 0; j < nsub; ++j) {
+          const int k = s_sub[w][j];
+          const T xmin = s_geo[9][k], ymin = s_geo[10][k], xmax = s_geo[11][k],
+                  ymax = s_geo[12][k];
+          if (x0 < xmin || x0 >= xmax || y0 < ymin || y0 >= ymax) continue;
+          T w0, w1, w2, z0;
+          if (!raster_face_test<T>(x0, y0, s_geo[0][k], s_geo[1][k], s_geo[2][k], s_geo[3][k],
+                                   s_geo[4][k], s_geo[5][k], s_geo[6][k], s_geo[7][k],
+                                   s_geo[8][k], a.eps, w0, w1, w2, z0))
+            continue;
+          if (z0 <= max_z0) continue;
+          max_z0 = z0;
+          best = s_f[k];
+          bw0 = w0;
+          bw1 = w1;
+          bw2 = w2;
+        }
+      }
+      __syncthreads();
+      cnt = 0;
+    }
+  }
+
+  if (!inimg) return;
+  const int64_t p = ((int64_t)b * H + py) * W + px;
+  a.face_idx[p] = best;
+  T *wo = a.weights + p * 3;
+  T *io = a.interp + p * a.D;
+  if (best >= 0) {
+    wo[0] = bw0;
+    wo[1] = bw1;
+    wo[2] = bw2;
+    const T *r = a.feat + (lo + best) * 3 * a.D;
+    for (int d = 0; d < a.D; ++d)
+      io[d] = bw0 * r[d] + bw1 * r[a.D + d] + bw2 * r[2 * a.D + d];
+  } else {
+    wo[0] = 0.;
+    wo[1] = 0.;
+    wo[2] = 0.;
+    for (int d = 0; d < a.D; ++d) io[d] = 0.;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Backward math of one covered pixel (rasterization_cuda.cu:271-399).  Adds the pixel's
+// contribution to the 6 vertex terms (summed over the D features) and calls feat_add(i, d, v)
+// for the 3*D feature terms.
+// ------------------------------------------------------------------------------------------
+template <typename T, typename FeatAdd>
+__device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], const T *g,
+                                                 const T *c, int D, float eps, T gv[6],
+                                                 FeatAdd feat_add) {
+#pragma unroll
+  for (int ii = 0; ii < 3; ++ii)
+    for (int d = 0; d < D; ++d) feat_add(ii, d, g[d] * wts[ii]);
+  const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
+  const T aw = wts[0], bw = wts[1], cw = wts[2];
+  const T x0 = aw * ax + bw * bx + cw * cx;
+  const T y0 = aw * ay + bw * by + cw * cy;
+  const T m = bx - ax, p = by - ay, n = cx - ax, q = cy - ay, s = x0 - ax, t = y0 - ay;
+  const T k1 = s * q - n * t;
+  const T k2 = m * t - s * p;
+  T k3 = m * q - n * p;
+  k3 = (T)((double)k3 + copysign((double)eps, (double)k3));
+  const T zero = (T)0;
+  const T dk1dm = zero, dk1dn = -t, dk1dp = zero, dk1dq = s, dk1ds = q, dk1dt = -n;
+  const T dk2dm = t, dk2dn = zero, dk2dp = -s, dk2dq = zero, dk2ds = -p, dk2dt = m;
+  const T dk3dm = q, dk3dn = -p, dk3dp = -n, dk3dq = m, dk3ds = zero, dk3dt = zero;
+  const T dw1dm = dk1dm * k3 - dk3dm * k1, dw1dn = dk1dn * k3 - dk3dn * k1;
+  const T dw1dp = dk1dp * k3 - dk3dp * k1, dw1dq = dk1dq * k3 - dk3dq * k1;
+  const T dw1ds = dk1ds * k3 - dk3ds * k1, dw1dt = dk1dt * k3 - dk3dt * k1;
+  const T dw2dm = dk2dm * k3 - dk3dm * k2, dw2dn = dk2dn * k3 - dk3dn * k2;
+  const T dw2dp = dk2dp * k3 - dk3dp * k2, dw2dq = dk2dq * k3 - dk3dq * k2;
+  const T dw2ds = dk2ds * k3 - dk3ds * k2, dw2dt = dk2dt * k3 - dk3dt * k2;
+  const T dw1[6] = {-(dw1dm + dw1dn + dw1ds), -(dw1dp + dw1dq + dw1dt), dw1dm, dw1dp, dw1dn,
+                    dw1dq};
+  const T dw2[6] = {-(dw2dm + dw2dn + dw2ds), -(dw2dp + dw2dq + dw2dt), dw2dm, dw2dp, dw2dn,
+                    dw2dq};
+  const T kk = k3 * k3;
+  for (int d = 0; d < D; ++d) {
+    const T c0 = c[d], c1 = c[D + d], c2 = c[2 * D + d];
+    const T dldI = g[d] / kk;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) gv[j] += dldI * ((c1 - c0) * dw1[j] + (c2 - c0) * dw2[j]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_raster_bwd_atomic(
+    int B, int H, int W, int64_t F, int D, const T *__restrict__ grad, const int64_t *face_idx,
+    const T *__restrict__ weights, const T *__restrict__ fvi, const T *__restrict__ feat,
+    float eps, T *grad_fvi, T *grad_feat) {
+  const int64_t P = (int64_t)H * W;
+  const int64_t total = (int64_t)B * P;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total;
+       p += (int64_t)gridDim.x * kBlock) {
+    const int64_t fi = face_idx[p];
+    if (fi < 0) continue;
+    const int64_t b = p / P;
+    const int64_t tf = b * F + fi;
+    const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
+    T gv[6] = {0, 0, 0, 0, 0, 0};
+    T *gf = grad_feat ? grad_feat + tf * 3 * D : nullptr;
+    raster_bwd_pixel<T>(fvi + tf * 6, wts, grad + p * D, feat + tf * 3 * D, D, eps, gv,
+                        [&](int ii, int d, T val) {
+                          if (gf) atomicAdd(gf + ii * D + d, val);
+                        });
+#pragma unroll
+    for (int j = 0; j < 6; ++j) atomicAdd(grad_fvi + tf * 6 + j, gv[j]);
+  }
+}
+
+template <typename T>
+__global__ void kd_zero(T *p, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    p[i] = (T)0;
+}
+
+constexpr int kGatherMaxD = 8;
+
+// One thread per (view, face): sums the covered pixels of the face's own exact pixel span.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_raster_bwd_gather(
+    FaceSet<T> fs, int D, const T *__restrict__ grad, const int64_t *__restrict__ face_idx,
+    const T *__restrict__ weights, const T *__restrict__ feat, float eps, T *grad_fvi,
+    T *grad_feat) {
+  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= fs.N) return;
+  const int b = (int)(i / fs.F);
+  const int64_t f = i - (int64_t)b * fs.F;
+  T gv[6] = {0, 0, 0, 0, 0, 0};
+  T gf[3 * kGatherMaxD];
+#pragma unroll
+  for (int k = 0; k < 3 * kGatherMaxD; ++k) gf[k] = 0;
+  const bool ok = !fs.valid || fs.valid[i];
+  if (ok) {
+    T v[6], box[4];
+    load_corners(fs, i, v);
+    face_box(fs, i, v, box);
+    const Span s = make_span<T>(box[0], box[1], box[2], box[3], fs.M, fs.H, fs.W);
+    if (!span_empty(s)) {
+      const T *uv = fs.fvi + i * 6;  // unscaled corners: the reference backward's frame
+      T u[6];
+#pragma unroll
+      for (int k = 0; k < 6; ++k) u[k] = uv[k];
+      const T *c = feat + i * 3 * D;
+      for (int y = s.y0; y <= s.y1; ++y) {
+        const int64_t row = ((int64_t)b * fs.H + y) * fs.W;
+        for (int x = s.x0; x <= s.x1; ++x) {
+          const int64_t p = row + x;
+          if (face_idx[p] != f) continue;
+          const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
+          raster_bwd_pixel<T>(u, wts, grad + p * D, c, D, eps, gv,
+                              [&](int ii, int d, T val) {
+#pragma unroll
+                                for (int q = 0; q < kGatherMaxD; ++q)
+                                  if (q == d) gf[ii * kGatherMaxD + q] += val;
+                              });
+        }
+      }
+    }
+  }
+  T *go = grad_fvi + i * 6;
+#pragma unroll
+  for (int k = 0; k < 6; ++k) go[k] = gv[k];
+  if (grad_feat) {
+    T *gfo = grad_feat + i * 3 * D;
+    for (int ii = 0; ii < 3; ++ii)
+#pragma unroll
+      for (int q = 0; q < kGatherMaxD; ++q)
+        if (q < D) gfo[ii * D + q] = gf[ii * kGatherMaxD + q];
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+template <typename T>
+int raster_forward(const FaceSet<T> &fs, int64_t max_per_view, const T *fvz, const T *feat,
+                   int D, float eps, T *interp, int64_t *face_idx, T *weights, void *ws,
+                   size_t ws_bytes, hipStream_t stream) {
+  const size_t need = bin_workspace_bytes(fs.B, fs.H, fs.W, fs.N, max_per_view);
+  if (ws_bytes < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", ws_bytes, need);
+  if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
+  size_t off = 0;
+  BinBuffers bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, max_per_view);
+  hipError_t e = bin_faces<T>(fs, bb, stream);
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
+  RasterFwdArgs<T> a{fs, bb, fvz, feat, D, eps, interp, face_idx, weights};
+  const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
+  hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+  e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster fwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template <typename T>
+int raster_backward(int B, int H, int W, int64_t F, int D, const T *grad, const int64_t *fidx,
+                    const T *weights, const T *fvi, const T *feat, float eps, T *gfvi, T *gfeat,
+                    hipStream_t stream) {
+  const int64_t nf = (int64_t)B * F;
+  if (nf > 0) {
+    hipLaunchKernelGGL(kd_zero<T>, dim3(1024), dim3(256), 0, stream, gfvi, nf * 6);
+    if (gfeat) hipLaunchKernelGGL(kd_zero<T>, dim3(1024), dim3(256), 0, stream, gfeat, nf * 3 * D);
+  }
+  const int64_t total = (int64_t)B * H * W;
+  if (total > 0 && nf > 0) {
+    const int64_t blocks = (total + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(kd_raster_bwd_atomic<T>, dim3((unsigned)(blocks < 65536 ? blocks : 65536)),
+                       dim3(kBlock), 0, stream, B, H, W, F, D, grad, fidx, weights, fvi, feat, eps,
+                       gfvi, gfeat);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster bwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template <typename T>
+int raster_backward_gather(int B, int H, int W, int64_t F, int D, const T *grad,
+                           const int64_t *fidx, const T *weights, const T *fvi, const T *feat,
+                           const uint8_t *valid, double M, float eps, T *gfvi, T *gfeat,
+                           hipStream_t stream) {
+  if (D > kGatherMaxD)  // wide features: the general form
+    return raster_backward<T>(B, H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
+                              stream);
+  FaceSet<T> fs{};
+  fs.B = B;
+  fs.H = H;
+  fs.W = W;
+  fs.N = (int64_t)B * F;
+  fs.F = F;
+  fs.fvi = fvi;
+  fs.scale = (T)M;
+  fs.valid = valid;
+  fs.M = (float)M;
+  if (fs.N > 0) {
+    hipLaunchKernelGGL(kd_raster_bwd_gather<T>, dim3((unsigned)((fs.N + kBlock - 1) / kBlock)),
+                       dim3(kBlock), 0, stream, fs, D, grad, fidx, weights, feat, eps, gfvi,
+                       gfeat);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return set_error(KD_ERR_LAUNCH, "raster bwd gather: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+}  // namespace kd
+
+// ==============================================================================================
+// C ABI
+// ==============================================================================================
+using namespace kd;
+
+template <typename T>
+static int packed_fwd(int B, int H, int W, int64_t Fp, int D, const T *fvz, const T *fvi,
+                      const T *bboxes, const T *feat, const int64_t *first_idx, float M, float eps,
+                      T *interp, int64_t *face_idx, T *weights, void *ws, size_t ws_bytes,
+                      void *stream) {
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && Fp >= 0 && D >= 0, "negative size");
+  KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG(Fp < (1ll << 31), "too many faces");
+  KD_CHECK_ARG(first_idx || B == 0, "first_idx is NULL");
+  FaceSet<T> fs{};
+  fs.B = B;
+  fs.H = H;
+  fs.W = W;
+  fs.N = Fp;
+  fs.F = 0;
+  fs.first_idx = first_idx;
+  fs.fvi = fvi;
+  fs.scale = (T)1;
+  fs.bbox = bboxes;
+  fs.M = M;
+  return raster_forward<T>(fs, Fp, fvz, feat, D, eps, interp, face_idx, weights, ws, ws_bytes,
+                           (hipStream_t)stream);
+}
+
+template <typename T>
+static int batched_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, const T *fvi,
+                       const T *feat, const uint8_t *valid, double M, float eps, T *interp,
+                       int64_t *face_idx, T *weights, void *ws, size_t ws_bytes, void *stream) {
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
+  KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
+  FaceSet<T> fs{};
+  fs.B = B;
+  fs.H = H;
+  fs.W = W;
+  fs.N = (int64_t)B * F;
+  fs.F = F;
+  fs.fvi = fvi;
+  fs.scale = (T)M;
+  fs.valid = valid;
+  fs.M = (float)M;
+  return raster_forward<T>(fs, F, fvz, feat, D, eps, interp, face_idx, weights, ws, ws_bytes,
+                           (hipStream_t)stream);
+}
+
+extern "C" {
+
+int kd_packed_rasterize_forward_f32(int B, int H, int W, int64_t Fp, int D, const float *fvz,
+                                    const float *fvi, const float *bboxes, const float *feat,
+                                    const int64_t *first_idx, float M, float eps, float *interp,
+                                    int64_t *face_idx, float *weights, void *ws, size_t wsb,
+                                    void *stream) {
+  return packed_fwd<float>(B, H, W, Fp, D, fvz, fvi, bboxes, feat, first_idx, M, eps, interp,
+                           face_idx, weights, ws, wsb, stream);
+}
+int kd_packed_rasterize_forward_f64(int B, int H, int W, int64_t Fp, int D, const double *fvz,
+                                    const double *fvi, const double *bboxes, const double *feat,
+                                    const int64_t *first_idx, float M, float eps, double *interp,
+                                    int64_t *face_idx, double *weights, void *ws, size_t wsb,
+                                    void *stream) {
+  return packed_fwd<double>(B, H, W, Fp, D, fvz, fvi, bboxes, feat, first_idx, M, eps, interp,
+                            face_idx, weights, ws, wsb, stream);
+}
+
+int kd_rasterize_forward_f32(int B, int H, int W, int64_t F, int D, const float *fvz,
+                             const float *fvi, const float *feat, const uint8_t *valid, double M,
+                             float eps, float *interp, int64_t *face_idx, float *weights,
+                             void *ws, size_t wsb, void *stream) {
+  return batched_fwd<float>(B, H, W, F, D, fvz, fvi, feat, valid, M, eps, interp, face_idx,
+                            weights, ws, wsb, stream);
+}
+int kd_rasterize_forward_f64(int B, int H, int W, int64_t F, int D, const double *fvz,
+                             const double *fvi, const double *feat, const uint8_t *valid,
+                             double M, float eps, double *interp, int64_t *face_idx,
+                             double *weights, void *ws, size_t wsb, void *stream) {
+  return batched_fwd<double>(B, H, W, F, D, fvz, fvi, feat, valid, M, eps, interp, face_idx,
+                             weights, ws, wsb, stream);
+}
+
+int kd_rasterize_backward_f32(int B, int H, int W, int64_t F, int D, const float *grad,
+                              const int64_t *fidx, const float *weights, const float *fvi,
+                              const float *feat, float eps, float *gfvi, float *gfeat,
+                              void *stream) {
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
+  return raster_backward<float>(B, H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
+                                (hipStream_t)stream);
+}
+int kd_rasterize_backward_f64(int B, int H, int W, int64_t F, int D, const double *grad,
+                              const int64_t *fidx, const double *weights, const double *fvi,
+                              const double *feat, float eps, double *gfvi, double *gfeat,
+                              void *stream) {
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
+  return raster_backward<double>(B, H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
+                                 (hipStream_t)stream);
+}
+
+int kd_rasterize_backward_gather_f32(int B, int H, int W, int64_t F, int D, const float *grad,
+                                     const int64_t *fidx, const float *weights, const float *fvi,
+                                     const float *feat, const uint8_t *valid, double M, float eps,
+                                     float *gfvi, float *gfeat, void *ws, size_t wsb,
+                                     void *stream) {
+  (void)ws;
+  (void)wsb;
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
+  KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  return raster_backward_gather<float>(B, H, W, F, D, grad, fidx, weights, fvi, feat, valid, M,
+                                       eps, gfvi, gfeat, (hipStream_t)stream);
+}
+int kd_rasterize_backward_gather_f64(int B, int H, int W, int64_t F, int D, const double *grad,
+                                     const int64_t *fidx, const double *weights,
+                                     const double *fvi, const double *feat, const uint8_t *valid,
+                                     double M, float eps, double *gfvi, double *gfeat, void *ws,
+                                     size_t wsb, void *stream) {
+  (void)ws;
+  (void)wsb;
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
+  KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  return raster_backward_gather<double>(B, H, W, F, D, grad, fidx, weights, fvi, feat, valid, M,
+                                        eps, gfvi, gfeat, (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,85 @@
+"""``dibr_soft_mask`` / ``dibr_rasterization`` -- drop-in for kaolin/render/mesh/dibr.py:75-209.
+
+The reference's ``DibrSoftMaskCuda`` (dibr.py:27-73) scales the coordinates, builds enlarged
+boxes, runs the per-pixel all-faces scan and saves the (B, H, W, K) close-face lists
+(prob / int64 idx / uint8 type, 13*K bytes per pixel) for its backward.  Here the scaling and
+boxes are computed in the kernel, the scan runs over ordered tile bins, and by default the lists
+are NOT materialised: the backward (face-gather, deterministic) re-derives each face's membership
+in a pixel's first-K list from one int32 per pixel (``close_last``) and recomputes the
+distance type / probability bit-identically.  Set ``SAVE_CLOSE_LISTS = True`` to materialise the
+lists and use the reference-structured atomic backward instead (same results to float-sum order).
+"""
+import torch
+from torch.autograd import Function
+
+from ... import _C
+from .rasterization import rasterize
+
+__all__ = ['dibr_soft_mask', 'dibr_rasterization']
+
+#: materialise the (B, H, W, K) close-face lists in the autograd path (reference structure)
+SAVE_CLOSE_LISTS = False
+
+
+class DibrSoftMaskCuda(Function):
+    """torch.autograd.Function for ``dibr_soft_mask`` (dibr.py:27-73)."""
+
+    @staticmethod
+    def forward(ctx, face_vertices_image, selected_face_idx, sigmainv, boxlen, knum,
+                multiplier):
+        face_vertices_image = face_vertices_image.contiguous()
+        selected_face_idx = selected_face_idx.contiguous()
+        lists = SAVE_CLOSE_LISTS
+        soft_mask, close_last, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
+            face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier,
+            with_lists=lists)
+        ctx.multiplier = multiplier
+        ctx.sigmainv = sigmainv
+        ctx.boxlen = boxlen
+        ctx.lists = lists
+        if lists:
+            ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, prob, cidx,
+                                  ctype)
+        else:
+            ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, close_last)
+        return soft_mask
+
+    @staticmethod
+    def backward(ctx, grad_soft_mask):
+        if not ctx.needs_input_grad[0]:
+            return None, None, None, None, None, None
+        grad_soft_mask = grad_soft_mask.contiguous()
+        if ctx.lists:
+            soft_mask, fvi, face_idx, prob, cidx, ctype = ctx.saved_tensors
+            grad = _C.render.mesh.dibr_soft_mask_backward_cuda(
+                grad_soft_mask, soft_mask, face_idx, prob, cidx, ctype,
+                (fvi * ctx.multiplier).contiguous(), ctx.sigmainv, ctx.multiplier)
+        else:
+            soft_mask, fvi, face_idx, close_last = ctx.saved_tensors
+            grad = _C.render.mesh.dibr_soft_mask_backward_gather(
+                grad_soft_mask, soft_mask, face_idx, close_last, fvi, ctx.multiplier,
+                ctx.boxlen, ctx.sigmainv)
+        return grad, None, None, None, None, None
+
+
+def dibr_soft_mask(face_vertices_image, selected_face_idx, sigmainv=7000, boxlen=0.02, knum=30,
+                   multiplier=1000.):
+    r"""Soft silhouette mask of DIB-R (dibr.py:75-117): ``1 - prod(1 - exp(-sigmainv d^2))`` over
+    the first ``knum`` faces (by index) whose box enlarged by ``boxlen`` holds the pixel; 1 on
+    covered pixels.  Returns (B, H, W)."""
+    return DibrSoftMaskCuda.apply(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum,
+                                  multiplier)
+
+
+def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face_features,
+                       face_normals_z, sigmainv=7000, boxlen=0.02, knum=30, multiplier=None,
+                       eps=None, rast_backend='cuda'):
+    r"""DIB-R renderer (dibr.py:119-209): rasterize the front faces (normal z >= 0), then the
+    soft mask over all faces.  Returns (interpolated_features, soft_mask, face_idx)."""
+    interpolated_features, face_idx = rasterize(
+        height, width, face_vertices_z, face_vertices_image, face_features,
+        face_normals_z >= 0., multiplier, eps, rast_backend)
+    _multiplier = 1000. if multiplier is None else multiplier
+    soft_mask = dibr_soft_mask(face_vertices_image, face_idx, sigmainv, boxlen, knum,
+                               _multiplier)
+    return interpolated_features, soft_mask, face_idx

@@ -1,0 +1,358 @@
+"""GPU parity: the gfx950 HIP path (through the C ABI) against the CPU oracle and the reference's
+golden vectors.  Run with ``pytest -m gpu`` on an MI355X.
+
+Bars (north_star): integer outputs (face_idx, close_face_idx, close_face_dist_type) bit-exact vs
+the oracle; the forward floats are also checked bit-exact where the arithmetic is the same
+IEEE-basic-op sequence (weights, interpolated features) and to 1e-6 relative where a
+transcendental is involved (close_face_prob, soft mask: device expf vs glibc expf); gradients
+(summed in a different order than the oracle) to rtol 1e-4 / atol 1e-5 in fp32 and 1e-10 in fp64.
+The reference's own test tolerances are used against its goldens.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import DTYPES, TORCH_DTYPES, iou_grad_soft, mask_iou, shifted_mask, sphere
+
+pytestmark = pytest.mark.gpu
+
+H, W = 35, 31
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _native():
+    import kaolin_amd  # noqa: F401  (fails loudly when the library is missing)
+    from kaolin_amd import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+
+
+def T(a, dtype=None):
+    t = torch.as_tensor(np.ascontiguousarray(a)).to(DEV)
+    return t if dtype is None else t.to(dtype)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def grad_tol(dname):
+    return dict(rtol=1e-4, atol=1e-5) if dname == 'f32' else dict(rtol=1e-9, atol=1e-10)
+
+
+# --------------------------------------------------------------------------------------------
+# rasterize
+# --------------------------------------------------------------------------------------------
+def _raster_case(fvz, fvi, feat, valid, h, w, dname, multiplier=1000, rows=None):
+    from kaolin_amd.render.mesh import rasterize
+    ri, rf, rw = oracle.rasterize(h, w, fvz, fvi, feat, valid, multiplier=multiplier, rows=rows)
+    tfvz, tfvi, tfeat = T(fvz), T(fvi), T(feat)
+    tfvi.requires_grad_(True)
+    tfeat.requires_grad_(True)
+    interp, face_idx = rasterize(h, w, tfvz, tfvi, tfeat,
+                                 None if valid is None else T(valid), multiplier=multiplier)
+    sl = slice(None) if rows is None else slice(rows[0], rows[1])
+    np.testing.assert_array_equal(N(face_idx)[:, sl], rf[:, sl])
+    np.testing.assert_array_equal(N(interp)[:, sl], ri[:, sl])
+    return tfvi, tfeat, interp, face_idx, rw
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+@pytest.mark.parametrize('with_valid', [0, 1])
+def test_rasterize_sphere_fwd_bwd(sphere_inputs, sphere_naive, dname, flip, with_valid):
+    s = sphere(sphere_inputs, dname, flip)
+    valid = s['valid'] if with_valid else None
+    tfvi, tfeat, interp, face_idx, rw = _raster_case(s['fvz'], s['fvi'], s['uvs'], valid, H, W,
+                                                     dname)
+    key = f'{dname}_flip{flip}_valid{with_valid}'
+    # the reference's own oracle test (test_rasterization.py:136-157)
+    np.testing.assert_array_equal(N(face_idx), sphere_naive[f'face_idx_{key}'])
+    np.testing.assert_allclose(N(interp), sphere_naive[f'interp_{key}'], rtol=1e-5, atol=1e-5)
+    grad_out = sphere_naive[f'grad_out_{key}']
+    interp.backward(T(grad_out))
+    gfvi, gfeat = oracle.rasterize_backward(grad_out, N(face_idx), rw, s['fvi'], s['uvs'], 1e-8)
+    np.testing.assert_allclose(N(tfvi.grad), gfvi, **grad_tol(dname))
+    np.testing.assert_allclose(N(tfeat.grad), gfeat, **grad_tol(dname))
+    # and the reference test's tolerances against autograd through the naive oracle
+    np.testing.assert_allclose(N(tfvi.grad), sphere_naive[f'grad_fvi_{key}'], rtol=1e-3,
+                               atol=1e-2)
+    np.testing.assert_allclose(N(tfeat.grad), sphere_naive[f'grad_feat_{key}'], rtol=1e-3,
+                               atol=1e-3)
+
+
+@pytest.mark.parametrize('i', [0, 1, 2])
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('with_valid', [0, 1])
+def test_rasterize_soup(soup_naive, i, dname, with_valid):
+    z = soup_naive
+    key = f'soup{i}_{dname}'
+    h, w = (int(v) for v in z[f'hw_{key}'])
+    valid = z[f'valid_{key}'] if with_valid else None
+    tfvi, tfeat, interp, face_idx, rw = _raster_case(z[f'fvz_{key}'], z[f'fvi_{key}'],
+                                                     z[f'feat_{key}'], valid, h, w, dname)
+    np.testing.assert_array_equal(N(face_idx), z[f'face_idx_{key}_valid{with_valid}'])
+    g = z[f'grad_out_{key}_valid{with_valid}']
+    interp.backward(T(g))
+    gfvi, gfeat = oracle.rasterize_backward(g, N(face_idx), rw, z[f'fvi_{key}'],
+                                            z[f'feat_{key}'], 1e-8)
+    np.testing.assert_allclose(N(tfvi.grad), gfvi, **grad_tol(dname))
+    np.testing.assert_allclose(N(tfeat.grad), gfeat, **grad_tol(dname))
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_packed_op_vs_oracle(sphere_inputs, dname):
+    """_C.render.mesh.packed_rasterize_forward_cuda on the reference's packed inputs."""
+    from kaolin_amd import _C
+    s = sphere(sphere_inputs, dname, 0)
+    valid = s['valid']
+    bi, fi = np.nonzero(valid)
+    counts = valid.sum(1)
+    first = np.zeros(len(counts) + 1, np.int64)
+    first[1:] = np.cumsum(counts)
+    pfvi = (s['fvi'][bi, fi] * 1000).astype(s['fvi'].dtype)
+    bbox = np.concatenate([pfvi.min(1), pfvi.max(1)], 1)
+    pfvz, pfeat = s['fvz'][bi, fi], s['uvs'][bi, fi]
+    ri, rf, rw = oracle.packed_rasterize_forward(H, W, pfvz, pfvi, bbox, pfeat, first, 1000, 1e-8)
+    interp, sel, weights = _C.render.mesh.packed_rasterize_forward_cuda(
+        H, W, T(pfvz), T(pfvi), T(bbox), T(pfeat), T(first), 1000, 1e-8)
+    np.testing.assert_array_equal(N(sel), rf)
+    np.testing.assert_array_equal(N(weights), rw)
+    np.testing.assert_array_equal(N(interp), ri)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_rasterize_backward_op_vs_oracle(sphere_inputs, dname):
+    """_C.render.mesh.rasterize_backward_cuda (general atomic form)."""
+    from kaolin_amd import _C
+    s = sphere(sphere_inputs, dname, 0)
+    ri, rf, rw = oracle.rasterize(H, W, s['fvz'], s['fvi'], s['uvs'])
+    g = np.random.default_rng(0).random(ri.shape).astype(ri.dtype)
+    gfvi, gfeat = _C.render.mesh.rasterize_backward_cuda(T(g), T(ri), T(rf), T(rw), T(s['fvi']),
+                                                         T(s['uvs']), 1e-8)
+    ofvi, ofeat = oracle.rasterize_backward(g, rf, rw, s['fvi'], s['uvs'], 1e-8)
+    np.testing.assert_allclose(N(gfvi), ofvi, **grad_tol(dname))
+    np.testing.assert_allclose(N(gfeat), ofeat, **grad_tol(dname))
+
+
+def test_rasterize_list_features(sphere_inputs):
+    """test_rasterization.py:159-187: list of features is concatenated then split."""
+    from kaolin_amd.render.mesh import rasterize
+    s = sphere(sphere_inputs, 'f32', 0)
+    uvs = T(s['uvs'])
+    (a, m), fi = rasterize(H, W, T(s['fvz']), T(s['fvi']), [uvs, torch.ones_like(uvs[..., :1])])
+    full, fi2 = rasterize(H, W, T(s['fvz']), T(s['fvi']),
+                          torch.cat([uvs, torch.ones_like(uvs[..., :1])], -1))
+    assert torch.equal(fi, fi2)
+    assert torch.equal(a, full[..., :2]) and torch.equal(m, full[..., 2:])
+    assert torch.allclose(m[..., 0], (fi >= 0).to(m.dtype), rtol=1e-5, atol=1e-5)
+
+
+def test_face_vertices_z_gets_no_grad(sphere_inputs):
+    from kaolin_amd.render.mesh import rasterize
+    s = sphere(sphere_inputs, 'f32', 0)
+    fvz = T(s['fvz']).requires_grad_(True)
+    fvi = T(s['fvi']).requires_grad_(True)
+    interp, _ = rasterize(H, W, fvz, fvi, T(s['uvs']))
+    interp.sum().backward()
+    assert fvz.grad is None or torch.all(fvz.grad == 0)
+    assert fvi.grad is not None
+
+
+# --------------------------------------------------------------------------------------------
+# soft mask
+# --------------------------------------------------------------------------------------------
+def _large_bbox(fvi_scaled, boxlen, multiplier):
+    pmin, pmax = fvi_scaled.min(-2), fvi_scaled.max(-2)
+    bl = boxlen * multiplier
+    return np.concatenate([pmin - bl, pmax + bl], -1).astype(fvi_scaled.dtype)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('sigmainv', [7000, 70])
+@pytest.mark.parametrize('boxlen', [0.02, 0.2])
+@pytest.mark.parametrize('multiplier', [1000, 100, 1])
+@pytest.mark.parametrize('knum', [30, 20])
+def test_simple_soft_mask_op(simple_golden, dname, sigmainv, boxlen, multiplier, knum):
+    """test_dibr.py:109-140 on the _C op, plus bit-exact vs the oracle."""
+    from kaolin_amd import _C
+    g = simple_golden
+    tag = f'{sigmainv}_{boxlen}'
+    fvi = g['simple_fvi'].astype(DTYPES[dname])
+    sfvi = (fvi * multiplier).astype(fvi.dtype)
+    bbox = _large_bbox(sfvi, boxlen, multiplier)
+    face_idx = g['simple_new_face_idx'].astype(np.int64)
+    soft, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_cuda(
+        T(sfvi), T(bbox), T(face_idx), sigmainv, knum, multiplier)
+    np.testing.assert_allclose(N(soft), g[f'simple_soft_{tag}'], atol=1e-5, rtol=1e-5)
+    np.testing.assert_array_equal(N(cidx), g[f'simple_close_idx_{tag}'][..., :knum])
+    np.testing.assert_allclose(N(prob), g[f'simple_close_prob_{tag}'][..., :knum], atol=1e-5,
+                               rtol=1e-5)
+    np.testing.assert_array_equal(N(ctype), g[f'simple_close_type_{tag}'][..., :knum])
+    osoft, oprob, ocidx, octype = oracle.soft_mask_forward_raw(sfvi, bbox, face_idx, sigmainv,
+                                                               knum, multiplier)
+    np.testing.assert_array_equal(N(cidx), ocidx)
+    np.testing.assert_array_equal(N(ctype), octype)
+    np.testing.assert_allclose(N(prob), oprob, rtol=1e-6, atol=1e-37)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('sigmainv', [7000, 70])
+@pytest.mark.parametrize('boxlen', [0.02, 0.2])
+@pytest.mark.parametrize('multiplier', [1000, 100, 1])
+@pytest.mark.parametrize('knum', [30, 20])
+@pytest.mark.parametrize('lists', [False, True])
+def test_simple_soft_mask_backward(simple_golden, dname, sigmainv, boxlen, multiplier, knum,
+                                   lists):
+    """test_dibr.py:167-191 through the autograd API (both saved-state modes)."""
+    from kaolin_amd.render.mesh import dibr, dibr_soft_mask
+    g = simple_golden
+    tag = f'{sigmainv}_{boxlen}'
+    fvi = T(g['simple_fvi'].astype(DTYPES[dname])).requires_grad_(True)
+    face_idx = T(g['simple_new_face_idx'].astype(np.int64))
+    old = dibr.SAVE_CLOSE_LISTS
+    dibr.SAVE_CLOSE_LISTS = lists
+    try:
+        soft = dibr_soft_mask(fvi, face_idx, sigmainv, boxlen, knum, multiplier)
+        loss = mask_iou(soft, shifted_mask(face_idx))
+        loss.backward()
+    finally:
+        dibr.SAVE_CLOSE_LISTS = old
+    np.testing.assert_allclose(N(soft), g[f'simple_soft_{tag}'], atol=1e-5, rtol=1e-5)
+    np.testing.assert_allclose(N(fvi.grad), g[f'simple_grad_{tag}'], rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('sigmainv', [7000, 70])
+@pytest.mark.parametrize('boxlen', [0.02, 0.01])
+@pytest.mark.parametrize('knum', [30, 40])
+@pytest.mark.parametrize('multiplier', [1000, 100])
+def test_sphere_soft_mask(sphere_inputs, sphere_softmask, dname, sigmainv, boxlen, knum,
+                          multiplier):
+    """test_dibr.py:309-394 plus bit-exact vs the oracle, forward (op + API) and backward."""
+    from kaolin_amd import _C
+    from kaolin_amd.render.mesh import dibr_soft_mask, rasterize
+    s = sphere(sphere_inputs, dname, 0)
+    gz = sphere_softmask
+    tag = f'{sigmainv}_{boxlen}'
+    feat = T(np.zeros(s['fvz'].shape + (1,), s['fvz'].dtype))
+    _, face_idx = rasterize(H, W, T(s['fvz']), T(s['fvi']), feat)
+    fi = N(face_idx)
+    sfvi = (s['fvi'] * multiplier).astype(s['fvi'].dtype)
+    bbox = _large_bbox(sfvi, boxlen, multiplier)
+    soft, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_cuda(
+        T(sfvi), T(bbox), face_idx, sigmainv, knum, multiplier)
+    np.testing.assert_allclose(N(soft), gz[f'soft_{tag}'], atol=1e-5, rtol=1e-5)
+    np.testing.assert_array_equal(N(cidx), gz[f'close_idx_{tag}'][..., :knum])
+    np.testing.assert_allclose(N(prob), gz[f'close_prob_{tag}'][..., :knum], atol=1e-5,
+                               rtol=1e-5)
+    assert np.mean(N(ctype) != gz[f'close_type_{tag}'][..., :knum]) <= 0.01
+    osoft, oprob, ocidx, octype = oracle.soft_mask_forward_raw(sfvi, bbox, fi, sigmainv, knum,
+                                                               multiplier)
+    np.testing.assert_array_equal(N(cidx), ocidx)
+    np.testing.assert_array_equal(N(ctype), octype)
+    np.testing.assert_allclose(N(prob), oprob, rtol=1e-6, atol=1e-37)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+    # autograd API (fused forward, face-gather backward)
+    tfvi = T(s['fvi']).requires_grad_(True)
+    asoft = dibr_soft_mask(tfvi, face_idx, sigmainv, boxlen, knum, multiplier)
+    np.testing.assert_allclose(N(asoft), osoft, rtol=1e-6, atol=1e-7)
+    gsoft = iou_grad_soft(N(asoft), fi)
+    asoft.backward(T(gsoft))
+    ograd = oracle.soft_mask_backward(gsoft, osoft, fi, oprob, ocidx, octype, sfvi, sigmainv,
+                                      multiplier)
+    np.testing.assert_allclose(N(tfvi.grad), ograd, **grad_tol(dname))
+    np.testing.assert_allclose(N(tfvi.grad), gz[f'grad_{tag}'], rtol=1e-1, atol=1e-1)
+    # general op backward on the op's own lists
+    gop = _C.render.mesh.dibr_soft_mask_backward_cuda(T(gsoft), soft, face_idx, prob, cidx, ctype,
+                                                      T(sfvi), sigmainv, multiplier)
+    np.testing.assert_allclose(N(gop), ograd, **grad_tol(dname))
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('flip', [0, 1])
+def test_dibr_rasterization_composition(sphere_inputs, dname, flip):
+    """test_dibr.py:482-529: dibr_rasterization == rasterize(normals_z >= 0) + dibr_soft_mask."""
+    from kaolin_amd.render.mesh import dibr_rasterization, dibr_soft_mask, rasterize
+    s = sphere(sphere_inputs, dname, flip)
+    fvz, fvi, uvs, nz = T(s['fvz']), T(s['fvi']), T(s['uvs']), T(s['normals_z'])
+    for sig, box, knum, mult in ((7000, 0.02, 30, 1000), (70, 0.01, 40, 100)):
+        gi, gf = rasterize(H, W, fvz, fvi, uvs, nz >= 0., mult)
+        gs = dibr_soft_mask(fvi, gf, sig, box, knum, mult)
+        i, sm, f = dibr_rasterization(H, W, fvz, fvi, uvs, nz, sig, box, knum, mult)
+        assert torch.equal(i, gi) and torch.equal(sm, gs) and torch.equal(f, gf)
+
+
+# --------------------------------------------------------------------------------------------
+# larger scale: bit-exact rows of full-size images, determinism, edge cases
+# --------------------------------------------------------------------------------------------
+@pytest.mark.parametrize('cfg', [(20, 26, 128, 128, 1), (100, 51, 256, 256, 2),
+                                 (250, 101, 512, 512, 2)])
+def test_uv_sphere_rows_vs_oracle(cfg):
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import dibr_rasterization
+    n_lon, n_lat, h, w, B = cfg
+    v = workloads.sphere_views(n_lon, n_lat, h, w, B, DEV)
+    fvz, fvi, feats, nz = v['fvz'], v['fvi'], v['feats'], v['normals_z']
+    interp, soft, face_idx = dibr_rasterization(h, w, fvz, fvi, feats, nz)
+    interp2, soft2, face_idx2 = dibr_rasterization(h, w, fvz, fvi, feats, nz)
+    assert torch.equal(interp, interp2) and torch.equal(soft, soft2)  # deterministic
+    assert torch.equal(face_idx, face_idx2)
+    # rows through the silhouette band and the centre
+    rows = sorted({h // 2, h // 2 + 1, int(h * 0.12), int(h * 0.88), int(h * 0.3)})
+    valid = (N(nz) >= 0)
+    for r in rows:
+        ri, rf, _ = oracle.rasterize(h, w, N(fvz), N(fvi), N(feats), valid, rows=(r, r + 1))
+        np.testing.assert_array_equal(N(face_idx)[:, r], rf[:, r])
+        np.testing.assert_array_equal(N(interp)[:, r], ri[:, r])
+        osoft, _, _, _, _ = oracle.soft_mask_forward(N(fvi), N(face_idx), rows=(r, r + 1))
+        np.testing.assert_allclose(N(soft)[:, r], osoft[:, r], rtol=1e-6, atol=1e-7)
+
+
+def test_dense_tile_overflow():
+    """More faces on one tile than the LDS list holds (the CAP overflow path): 3000 large
+    overlapping triangles on a 48x40 image."""
+    from kaolin_amd.render.mesh import dibr_soft_mask, rasterize
+    rng = np.random.default_rng(5)
+    Fn, h, w = 3000, 48, 40
+    c = rng.normal(0, 0.2, (1, Fn, 1, 2))
+    fvi = (c + rng.uniform(-0.6, 0.6, (1, Fn, 3, 2))).astype(np.float32)
+    fvz = (-2 - rng.uniform(0, 1, (1, Fn, 3))).astype(np.float32)
+    feat = rng.random((1, Fn, 3, 2)).astype(np.float32)
+    interp, face_idx = rasterize(h, w, T(fvz), T(fvi), T(feat))
+    ri, rf, _ = oracle.rasterize(h, w, fvz, fvi, feat)
+    np.testing.assert_array_equal(N(face_idx), rf)
+    np.testing.assert_array_equal(N(interp), ri)
+    empty = T(np.full((1, h, w), -1, np.int64))
+    soft = dibr_soft_mask(T(fvi), empty, 7000, 0.05, 100, 1000.)
+    osoft, _, _, _, _ = oracle.soft_mask_forward(fvi, np.full((1, h, w), -1, np.int64), 7000,
+                                                 0.05, 100, 1000.)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+
+
+def test_edge_cases():
+    from kaolin_amd.render.mesh import dibr_rasterization, rasterize
+    # no faces at all
+    z = torch.zeros((2, 0, 3), device=DEV)
+    i, f = rasterize(17, 13, z, torch.zeros((2, 0, 3, 2), device=DEV),
+                     torch.zeros((2, 0, 3, 4), device=DEV))
+    assert torch.all(f == -1) and torch.all(i == 0) and i.shape == (2, 17, 13, 4)
+    # all faces culled, odd sizes, degenerate (zero area) and NaN faces
+    fvi = np.array([[[[-0.5, -0.5], [0.5, -0.5], [0., 0.5]],
+                     [[0.1, 0.1], [0.1, 0.1], [0.1, 0.1]],
+                     [[np.nan, 0.], [0.5, 0.5], [0.2, 0.9]],
+                     [[-0.9, -0.9], [0.9, -0.9], [0.9, 0.9]]]], np.float32)
+    fvz = np.array([[[-2., -2., -2.], [-1., -1., -1.], [-3., -3., -3.], [-2.5, -2.5, -2.5]]],
+                   np.float32)
+    feat = np.random.default_rng(1).random((1, 4, 3, 3)).astype(np.float32)
+    for valid in (None, np.array([[True, True, True, True]]), np.array([[0, 0, 0, 0]], bool),
+                  np.array([[1, 0, 1, 0]], bool)):
+        ti, tf = rasterize(19, 23, T(fvz), T(fvi), T(feat), None if valid is None else T(valid))
+        ri, rf, _ = oracle.rasterize(19, 23, fvz, fvi, feat, valid)
+        np.testing.assert_array_equal(N(tf), rf)
+        np.testing.assert_array_equal(N(ti), ri)
+    nz = T(np.array([[1., 1., 1., -1.]], np.float32))
+    dibr_rasterization(19, 23, T(fvz), T(fvi), T(feat), nz)
