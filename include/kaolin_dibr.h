@@ -35,8 +35,7 @@ extern "C" {
 /* Workspace kinds for kd_workspace_size(). */
 #define KD_WS_RASTER_PACKED 1 /* kd_packed_rasterize_forward_*      */
 #define KD_WS_RASTER 2        /* kd_rasterize_forward_*             */
-#define KD_WS_SOFT_MASK 3     /* kd_dibr_soft_mask_forward*_*       */
-#define KD_WS_GATHER_BWD 4    /* kd_*_backward_gather_*             */
+#define KD_WS_SOFT_MASK 3     /* kd_dibr_soft_mask_forward*_* / _backward_binned_* */
 
 /* Bytes of device workspace the call of `kind` needs.  num_faces_total = rows of the face arrays
  * (Fp for the packed layout, B*F otherwise); max_faces_per_view = the largest per-view count
@@ -46,6 +45,15 @@ size_t kd_workspace_size(int kind, int batch, int height, int width, int64_t num
 
 const char *kd_last_error(void);
 int kd_version(void);
+
+/* In-library kernel timing (HIP events recorded around every launch on the launch stream).
+ * kd_profile_enable(1) starts recording; kd_profile_collect() waits for the recorded events,
+ * adds each kernel's elapsed milliseconds / launch count into total_ms[id] / launches[id]
+ * (arrays of n entries), clears the records and returns the number of kernel ids.
+ * kd_profile_kernel_name(id) names them.  Not for use under stream capture. */
+void kd_profile_enable(int on);
+int kd_profile_collect(double *total_ms, int64_t *launches, int n);
+const char *kd_profile_kernel_name(int id);
 
 /* ---------------------------------------------------------------------------------------------
  * Packed rasterize forward.  Replaces _C.render.mesh.packed_rasterize_forward_cuda
@@ -89,7 +97,8 @@ int kd_rasterize_forward_f64(int batch, int height, int width, int64_t num_faces
  * Rasterize backward, general form.  Replaces _C.render.mesh.rasterize_backward_cuda
  * (bindings.cpp:78 -> rasterization.cpp:106-168, kernel rasterization_cuda.cu:238-402).  Any
  * face_idx is accepted (original index, -1 = none).  fvi is NOT scaled.  grad_feat may be NULL.
- * Float atomics: the summation order, hence the last bits, vary run to run (as in the reference).
+ * Pixels of one face are summed per 16x16 tile in LDS, then added with float atomics: the
+ * summation order, hence the last bits, vary run to run (as in the reference).
  * ------------------------------------------------------------------------------------------- */
 int kd_rasterize_backward_f32(int batch, int height, int width, int64_t num_faces, int feat_dim,
                               const float *grad_interp, const int64_t *face_idx,
@@ -99,27 +108,6 @@ int kd_rasterize_backward_f64(int batch, int height, int width, int64_t num_face
                               const double *grad_interp, const int64_t *face_idx,
                               const double *weights, const double *fvi, const double *feat,
                               float eps, double *grad_fvi, double *grad_feat, void *stream);
-
-/* ---------------------------------------------------------------------------------------------
- * Rasterize backward, face-gather form (deterministic, no atomics): each face sums the pixels of
- * its own pixel footprint.  Valid only for a face_idx produced by kd_rasterize_forward_* with the
- * same fvi / valid / multiplier (every pixel of face f lies inside f's bounding box); this is the
- * autograd path of rasterize().  Same math as kd_rasterize_backward_*.  grad_feat may be NULL.
- * ------------------------------------------------------------------------------------------- */
-int kd_rasterize_backward_gather_f32(int batch, int height, int width, int64_t num_faces,
-                                     int feat_dim, const float *grad_interp,
-                                     const int64_t *face_idx, const float *weights,
-                                     const float *fvi, const float *feat, const uint8_t *valid,
-                                     double multiplier, float eps, float *grad_fvi,
-                                     float *grad_feat, void *workspace, size_t workspace_bytes,
-                                     void *stream);
-int kd_rasterize_backward_gather_f64(int batch, int height, int width, int64_t num_faces,
-                                     int feat_dim, const double *grad_interp,
-                                     const int64_t *face_idx, const double *weights,
-                                     const double *fvi, const double *feat, const uint8_t *valid,
-                                     double multiplier, float eps, double *grad_fvi,
-                                     double *grad_feat, void *workspace, size_t workspace_bytes,
-                                     void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * DIB-R soft mask forward.  Replaces _C.render.mesh.dibr_soft_mask_forward_cuda
@@ -144,9 +132,9 @@ int kd_dibr_soft_mask_forward_f64(int batch, int height, int width, int64_t num_
 /* ---------------------------------------------------------------------------------------------
  * DIB-R soft mask forward from UNSCALED fvi (DibrSoftMaskCuda.forward dibr.py:29-55 fused: the
  * x multiplier and the +-boxlen*multiplier bounding boxes are computed in the kernel).
- * close_last (B, H, W) int32 receives, per uncovered pixel, the K-th close face when the list is
- * full, else -1 (what kd_dibr_soft_mask_backward_gather_* needs).  The three close_face_* lists
- * may all be NULL (then they are not materialised); close_last may be NULL.
+ * close_last (B, H, W) int32, if not NULL, receives per pixel the K-th close face when the list
+ * is full, else -1.  The three close_face_* lists may all be NULL (then they are not
+ * materialised).  Keep `workspace` for kd_dibr_soft_mask_backward_binned_* (bins_ready = 1).
  * ------------------------------------------------------------------------------------------- */
 int kd_dibr_soft_mask_forward_fused_f32(int batch, int height, int width, int64_t num_faces,
                                         int knum, const float *fvi, double multiplier,
@@ -184,23 +172,26 @@ int kd_dibr_soft_mask_backward_f64(int batch, int height, int width, int64_t num
                                    void *stream);
 
 /* ---------------------------------------------------------------------------------------------
- * DIB-R soft mask backward, face-gather form (deterministic, no atomics, no close lists): each
- * face re-derives, for the uncovered pixels of its enlarged box, whether it is among the pixel's
- * first K close faces (close_last from the fused forward) and its distance type / probability
- * (bit-identical recomputation), and sums its own gradient.  Same math as the general form.
+ * DIB-R soft mask backward, recompute form (the autograd path of dibr_soft_mask): no close
+ * lists.  For every uncovered pixel the first K close faces and their distance types /
+ * probabilities are re-derived bit-identically from the same tile bins as the forward, the
+ * reference's gradient terms (dibr_soft_mask_cuda.cu:281-348) are summed per face and tile in
+ * LDS and added with float atomics.  `workspace` is the fused forward's workspace: with
+ * bins_ready != 0 its bins (same fvi / multiplier / boxlen) are reused, else they are rebuilt.
+ * fvi is NOT scaled; grad_fvi is the gradient w.r.t. fvi.
  * ------------------------------------------------------------------------------------------- */
-int kd_dibr_soft_mask_backward_gather_f32(int batch, int height, int width, int64_t num_faces,
-                                          const float *grad_soft_mask, const float *soft_mask,
-                                          const int64_t *face_idx, const int32_t *close_last,
+int kd_dibr_soft_mask_backward_binned_f32(int batch, int height, int width, int64_t num_faces,
+                                          int knum, const float *grad_soft_mask,
+                                          const float *soft_mask, const int64_t *face_idx,
                                           const float *fvi, double multiplier, double boxlen,
                                           float sigmainv, float *grad_fvi, void *workspace,
-                                          size_t workspace_bytes, void *stream);
-int kd_dibr_soft_mask_backward_gather_f64(int batch, int height, int width, int64_t num_faces,
-                                          const double *grad_soft_mask, const double *soft_mask,
-                                          const int64_t *face_idx, const int32_t *close_last,
+                                          size_t workspace_bytes, int bins_ready, void *stream);
+int kd_dibr_soft_mask_backward_binned_f64(int batch, int height, int width, int64_t num_faces,
+                                          int knum, const double *grad_soft_mask,
+                                          const double *soft_mask, const int64_t *face_idx,
                                           const double *fvi, double multiplier, double boxlen,
                                           float sigmainv, double *grad_fvi, void *workspace,
-                                          size_t workspace_bytes, void *stream);
+                                          size_t workspace_bytes, int bins_ready, void *stream);
 
 #ifdef __cplusplus
 }

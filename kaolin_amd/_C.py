@@ -9,8 +9,8 @@ reference's ``at::full(-1)`` / ``at::zeros`` pre-fills are not needed) and launc
 current HIP stream of the inputs' device.
 
 Extra entry points (used by kaolin_amd.render.mesh's autograd functions, not in the reference):
-``rasterize_forward_fused``, ``rasterize_backward_gather``, ``dibr_soft_mask_forward_fused``,
-``dibr_soft_mask_backward_gather``.
+``rasterize_forward_fused``, ``rasterize_backward_autograd``, ``dibr_soft_mask_forward_fused``,
+``dibr_soft_mask_backward_binned``.
 """
 import types
 
@@ -257,25 +257,26 @@ def rasterize_forward_fused(height, width, face_vertices_z, face_vertices_image,
     return interp, face_idx, weights, valid_faces
 
 
-def rasterize_backward_gather(grad_interp, face_idx, weights, face_vertices_image,
-                              face_features, valid_faces, multiplier, eps, need_feat=True):
+def rasterize_backward_autograd(grad_interp, face_idx, weights, face_vertices_image,
+                                face_features, eps, need_feat=True):
+    """RasterizeCuda.backward: the tile kernel, grad of the features only when needed."""
     dev = grad_interp.device
     B, H, W, D = grad_interp.shape
     F = face_vertices_image.shape[1]
     sfx = _sfx(face_vertices_image, 'rasterize_backward')
     gfvi = torch.empty_like(face_vertices_image)
     gfeat = torch.empty_like(face_features) if need_feat else None
-    _lib.call(f'kd_rasterize_backward_gather_{sfx}', B, H, W, F, D, _ptr(grad_interp),
-              _ptr(face_idx), _ptr(weights), _ptr(face_vertices_image), _ptr(face_features),
-              _ptr(valid_faces), float(multiplier), float(eps), _ptr(gfvi), _ptr(gfeat), None, 0,
-              _stream(dev))
+    _lib.call(f'kd_rasterize_backward_{sfx}', B, H, W, F, D, _ptr(grad_interp), _ptr(face_idx),
+              _ptr(weights), _ptr(face_vertices_image), _ptr(face_features), float(eps),
+              _ptr(gfvi), _ptr(gfeat), _stream(dev))
     return gfvi, gfeat
 
 
 def dibr_soft_mask_forward_fused(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum,
                                  multiplier, with_lists=False):
     """DibrSoftMaskCuda.forward (dibr.py:29-55) with the x multiplier and the enlarged boxes in
-    the kernel.  Returns (soft, close_last, prob, cidx, ctype) (lists None unless with_lists)."""
+    the kernel.  Returns (soft, workspace, prob, cidx, ctype) (lists None unless with_lists); the
+    workspace holds the tile bins the backward reuses."""
     fn = 'dibr_soft_mask'
     dev = _check_same_gpu(fn, face_vertices_image=face_vertices_image,
                           selected_face_idx=selected_face_idx)
@@ -289,7 +290,6 @@ def dibr_soft_mask_forward_fused(face_vertices_image, selected_face_idx, sigmain
         raise RuntimeError(f'{fn}: knum must be >= 1, got {knum}')
     opts = dict(device=dev, dtype=face_vertices_image.dtype)
     soft = torch.empty((B, H, W), **opts)
-    last = torch.empty((B, H, W), device=dev, dtype=torch.int32)
     prob = cidx = ctype = None
     if with_lists:
         prob = torch.empty((B, H, W, knum), **opts)
@@ -299,20 +299,22 @@ def dibr_soft_mask_forward_fused(face_vertices_image, selected_face_idx, sigmain
     _lib.call(f'kd_dibr_soft_mask_forward_fused_{sfx}', B, H, W, F, knum,
               _ptr(face_vertices_image), float(multiplier), float(boxlen),
               _ptr(selected_face_idx), float(sigmainv), _ptr(soft), _ptr(prob), _ptr(cidx),
-              _ptr(ctype), _ptr(last), _ptr(ws), nb, _stream(dev))
-    return soft, last, prob, cidx, ctype
+              _ptr(ctype), None, _ptr(ws), nb, _stream(dev))
+    return soft, ws, prob, cidx, ctype
 
 
-def dibr_soft_mask_backward_gather(grad_soft, soft, selected_face_idx, close_last,
-                                   face_vertices_image, multiplier, boxlen, sigmainv):
+def dibr_soft_mask_backward_binned(grad_soft, soft, selected_face_idx, face_vertices_image,
+                                   multiplier, boxlen, sigmainv, knum, workspace):
+    """DibrSoftMaskCuda.backward without close lists (recompute over the forward's bins)."""
     dev = grad_soft.device
     B, F = face_vertices_image.shape[:2]
     H, W = selected_face_idx.shape[1:3]
     sfx = _sfx(face_vertices_image, 'dibr_soft_mask_backward')
     g = torch.empty_like(face_vertices_image)
-    _lib.call(f'kd_dibr_soft_mask_backward_gather_{sfx}', B, H, W, F, _ptr(grad_soft), _ptr(soft),
-              _ptr(selected_face_idx), _ptr(close_last), _ptr(face_vertices_image),
-              float(multiplier), float(boxlen), float(sigmainv), _ptr(g), None, 0, _stream(dev))
+    _lib.call(f'kd_dibr_soft_mask_backward_binned_{sfx}', B, H, W, F, int(knum), _ptr(grad_soft),
+              _ptr(soft), _ptr(selected_face_idx), _ptr(face_vertices_image), float(multiplier),
+              float(boxlen), float(sigmainv), _ptr(g), _ptr(workspace), workspace.numel(), 1,
+              _stream(dev))
     return g
 
 
@@ -322,7 +324,7 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     dibr_soft_mask_forward_cuda=dibr_soft_mask_forward_cuda,
     dibr_soft_mask_backward_cuda=dibr_soft_mask_backward_cuda,
     rasterize_forward_fused=rasterize_forward_fused,
-    rasterize_backward_gather=rasterize_backward_gather,
+    rasterize_backward_autograd=rasterize_backward_autograd,
     dibr_soft_mask_forward_fused=dibr_soft_mask_forward_fused,
-    dibr_soft_mask_backward_gather=dibr_soft_mask_backward_gather,
+    dibr_soft_mask_backward_binned=dibr_soft_mask_backward_binned,
 ))

@@ -16,7 +16,6 @@ KD_OK = 0
 KD_WS_RASTER_PACKED = 1
 KD_WS_RASTER = 2
 KD_WS_SOFT_MASK = 3
-KD_WS_GATHER_BWD = 4
 
 _lib = None
 _lock = threading.Lock()
@@ -32,8 +31,6 @@ _SIGS = {
                              c_float, c_p, c_p, c_p, c_p, c_size, c_p],
     'kd_rasterize_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
                               c_float, c_p, c_p, c_p],
-    'kd_rasterize_backward_gather': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
-                                     c_p, c_double, c_float, c_p, c_p, c_p, c_size, c_p],
     'kd_dibr_soft_mask_forward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_float,
                                   c_float, c_p, c_p, c_p, c_p, c_p, c_size, c_p],
     'kd_dibr_soft_mask_forward_fused': [c_int, c_int, c_int, c_i64, c_int, c_p, c_double,
@@ -41,8 +38,9 @@ _SIGS = {
                                         c_size, c_p],
     'kd_dibr_soft_mask_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
                                    c_p, c_p, c_float, c_float, c_p, c_p],
-    'kd_dibr_soft_mask_backward_gather': [c_int, c_int, c_int, c_i64, c_p, c_p, c_p, c_p, c_p,
-                                          c_double, c_double, c_float, c_p, c_p, c_size, c_p],
+    'kd_dibr_soft_mask_backward_binned': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,
+                                          c_double, c_double, c_float, c_p, c_p, c_size, c_int,
+                                          c_p],
 }
 
 
@@ -63,6 +61,12 @@ def load():
             lib.kd_last_error.argtypes = []
             lib.kd_last_error.restype = ctypes.c_char_p
             lib.kd_version.restype = c_int
+            lib.kd_profile_enable.argtypes = [c_int]
+            lib.kd_profile_enable.restype = None
+            lib.kd_profile_collect.argtypes = [c_p, c_p, c_int]
+            lib.kd_profile_collect.restype = c_int
+            lib.kd_profile_kernel_name.argtypes = [c_int]
+            lib.kd_profile_kernel_name.restype = ctypes.c_char_p
             for base, sig in _SIGS.items():
                 for sfx in ('f32', 'f64'):
                     fn = getattr(lib, f'{base}_{sfx}')
@@ -81,6 +85,21 @@ def call(name, *args):
 
 def workspace_size(kind, B, H, W, n_total, max_per_view):
     return int(load().kd_workspace_size(kind, B, H, W, n_total, max_per_view))
+
+
+def profile_enable(on=True):
+    """Record HIP events around every library launch (see kd_profile_enable)."""
+    load().kd_profile_enable(1 if on else 0)
+
+
+def profile_collect():
+    """{kernel name: (total ms, launches)} for the launches recorded since the last collect."""
+    lib = load()
+    n = 32
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_int64 * n)()
+    k = lib.kd_profile_collect(ctypes.cast(ms, c_p), ctypes.cast(cnt, c_p), n)
+    return {lib.kd_profile_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(k) if cnt[i]}
 
 
 def declared_symbols():

@@ -1,6 +1,8 @@
 // kd_binning.hip -- see kd_binning.hpp for the algorithm.
 #include "kd_binning.hpp"
 
+#include "kd_capi.hpp"
+
 namespace kd {
 
 size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view) {
@@ -153,10 +155,19 @@ hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t str
                           stream);
   }
   const dim3 grid_c(bb.nchunk, fs.B), grid_t(bb.g.nct(), fs.B);
-  hipLaunchKernelGGL(kd_bin_count<T>, grid_c, dim3(kBlock), 0, stream, fs, bb);
-  hipLaunchKernelGGL(kd_bin_scan, grid_t, dim3(kBlock), 0, stream, bb, fs.B);
-  hipLaunchKernelGGL(kd_bin_scatter<T>, grid_c, dim3(kBlock),
-                     sizeof(uint32_t) * 8 * bb.g.nct(), stream, fs, bb);
+  {
+    ProfScope prof(K_BIN_COUNT, stream);
+    hipLaunchKernelGGL(kd_bin_count<T>, grid_c, dim3(kBlock), 0, stream, fs, bb);
+  }
+  {
+    ProfScope prof(K_BIN_SCAN, stream);
+    hipLaunchKernelGGL(kd_bin_scan, grid_t, dim3(kBlock), 0, stream, bb, fs.B);
+  }
+  {
+    ProfScope prof(K_BIN_SCATTER, stream);
+    hipLaunchKernelGGL(kd_bin_scatter<T>, grid_c, dim3(kBlock),
+                       sizeof(uint32_t) * 8 * bb.g.nct(), stream, fs, bb);
+  }
   return hipGetLastError();
 }
 

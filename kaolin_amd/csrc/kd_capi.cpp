@@ -3,10 +3,41 @@
 
 #include "kd_binning.hpp"
 
+#include <atomic>
+#include <mutex>
+#include <vector>
+
 namespace kd {
 char *error_buffer() {
   static thread_local char buf[512] = {0};
   return buf;
+}
+
+namespace {
+std::atomic<bool> g_prof{false};
+std::mutex g_prof_mu;
+struct Rec {
+  int id;
+  hipEvent_t start, stop;
+};
+std::vector<Rec> g_recs;
+const char *kNames[K_NUM_KERNELS] = {
+    "kd_bin_count", "kd_bin_scan", "kd_bin_scatter", "kd_raster_fwd", "kd_soft_fwd",
+    "kd_raster_bwd_tile", "kd_soft_bwd_tile", "kd_raster_bwd_atomic", "kd_soft_bwd_atomic",
+    "kd_zero"};
+}  // namespace
+
+ProfScope::ProfScope(int id_, hipStream_t s) : id(id_), stream(s), on(g_prof.load()) {
+  if (on) {
+    on = hipEventCreate(&start) == hipSuccess && hipEventCreate(&stop) == hipSuccess &&
+         hipEventRecord(start, stream) == hipSuccess;
+  }
+}
+ProfScope::~ProfScope() {
+  if (!on) return;
+  if (hipEventRecord(stop, stream) != hipSuccess) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  g_recs.push_back({id, start, stop});
 }
 }  // namespace kd
 
@@ -20,8 +51,6 @@ size_t kd_workspace_size(int kind, int B, int H, int W, int64_t num_faces_total,
     case KD_WS_RASTER:
     case KD_WS_SOFT_MASK:
       return kd::bin_workspace_bytes(B, H, W, num_faces_total, max_faces_per_view);
-    case KD_WS_GATHER_BWD:
-      return 0;
     default:
       return 0;
   }
@@ -30,5 +59,30 @@ size_t kd_workspace_size(int kind, int B, int H, int W, int64_t num_faces_total,
 const char *kd_last_error(void) { return kd::error_buffer(); }
 
 int kd_version(void) { return 1; }
+
+void kd_profile_enable(int on) { kd::g_prof.store(on != 0); }
+
+int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
+  std::vector<kd::Rec> recs;
+  {
+    std::lock_guard<std::mutex> lk(kd::g_prof_mu);
+    recs.swap(kd::g_recs);
+  }
+  for (auto &r : recs) {
+    float ms = 0.f;
+    if (hipEventSynchronize(r.stop) == hipSuccess &&
+        hipEventElapsedTime(&ms, r.start, r.stop) == hipSuccess && r.id < n) {
+      if (total_ms) total_ms[r.id] += ms;
+      if (launches) launches[r.id] += 1;
+    }
+    (void)hipEventDestroy(r.start);
+    (void)hipEventDestroy(r.stop);
+  }
+  return kd::K_NUM_KERNELS;
+}
+
+const char *kd_profile_kernel_name(int id) {
+  return (id >= 0 && id < kd::K_NUM_KERNELS) ? kd::kNames[id] : "";
+}
 
 }  // extern "C"

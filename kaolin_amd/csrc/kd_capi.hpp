@@ -4,11 +4,37 @@
 #include <stdarg.h>
 #include <stdio.h>
 
+#include <hip/hip_runtime.h>
+
 #include "../../include/kaolin_dibr.h"
 
 namespace kd {
 
 char *error_buffer();  // thread-local, 512 bytes
+
+enum KernelId {
+  K_BIN_COUNT = 0,
+  K_BIN_SCAN,
+  K_BIN_SCATTER,
+  K_RASTER_FWD,
+  K_SOFT_FWD,
+  K_RASTER_BWD_TILE,
+  K_SOFT_BWD_TILE,
+  K_RASTER_BWD_ATOMIC,
+  K_SOFT_BWD_ATOMIC,
+  K_ZERO,
+  K_NUM_KERNELS
+};
+
+// Records a HIP event pair around the launches in its scope when profiling is enabled.
+struct ProfScope {
+  ProfScope(int id, hipStream_t s);
+  ~ProfScope();
+  int id;
+  hipStream_t stream;
+  hipEvent_t start, stop;
+  bool on;
+};
 
 inline int set_error(int code, const char *fmt, ...) {
   va_list ap;

@@ -8,11 +8,12 @@
 //   lane (pixel) runs the reference's exact per-face test over that short list with LDS broadcast
 //   reads: the same sequence of faces the reference visits, minus faces whose box provably
 //   misses the pixel, so face_idx / weights / features are bit-identical.
-// Backward:
-//   kd_raster_bwd_atomic  -- general form (any face_idx), one thread per pixel, float atomics,
-//                            the per-pixel vertex terms summed over features in registers first.
-//   kd_raster_bwd_gather  -- autograd form: one thread per face sums the pixels of its own exact
-//                            pixel span (deterministic, no atomics, writes every output).
+// Backward (replaces rasterize_backward_cuda_kernel, rasterization_cuda.cu:238-402):
+//   kd_raster_bwd_tile    -- one workgroup per 16x16 tile; a pixel's terms (6 corner terms summed
+//                            over the features, 3*D feature terms) are summed per face in an LDS
+//                            hash table, then flushed with one float atomic per (tile, face, term).
+//                            Accepts any face_idx (the reference op's contract).
+//   kd_raster_bwd_atomic  -- the same per pixel for wide features (D > 8).
 #include "../../include/kaolin_dibr.h"
 #include "kd_binning.hpp"
 #include "kd_capi.hpp"
@@ -187,17 +188,21 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Backward math of one covered pixel (rasterization_cuda.cu:271-399).  Adds the pixel's
-// contribution to the 6 vertex terms (summed over the D features) and calls feat_add(i, d, v)
-// for the 3*D feature terms.
+// Backward terms of one covered pixel (rasterization_cuda.cu:271-399) into out[]: out[0..5]
+// the 6 corner terms summed over the D features, out[6 + ii*DMAX + d] the feature terms
+// (register array, static indices only).
 // ------------------------------------------------------------------------------------------
-template <typename T, typename FeatAdd>
+template <typename T, int DMAX>
 __device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], const T *g,
-                                                 const T *c, int D, float eps, T gv[6],
-                                                 FeatAdd feat_add) {
+                                                 const T *c, int D, float eps,
+                                                 T out[6 + 3 * DMAX]) {
+  T gd[DMAX];
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) gd[d] = d < D ? g[d] : (T)0;
 #pragma unroll
   for (int ii = 0; ii < 3; ++ii)
-    for (int d = 0; d < D; ++d) feat_add(ii, d, g[d] * wts[ii]);
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) out[6 + ii * DMAX + d] = gd[d] * wts[ii];
   const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
   const T aw = wts[0], bw = wts[1], cw = wts[2];
   const T x0 = aw * ax + bw * bx + cw * cx;
@@ -222,14 +227,20 @@ __device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], con
   const T dw2[6] = {-(dw2dm + dw2dn + dw2ds), -(dw2dp + dw2dq + dw2dt), dw2dm, dw2dp, dw2dn,
                     dw2dq};
   const T kk = k3 * k3;
-  for (int d = 0; d < D; ++d) {
-    const T c0 = c[d], c1 = c[D + d], c2 = c[2 * D + d];
-    const T dldI = g[d] / kk;
 #pragma unroll
-    for (int j = 0; j < 6; ++j) gv[j] += dldI * ((c1 - c0) * dw1[j] + (c2 - c0) * dw2[j]);
+  for (int j = 0; j < 6; ++j) out[j] = (T)0;
+#pragma unroll
+  for (int d = 0; d < DMAX; ++d) {
+    if (d < D) {
+      const T c0 = c[d], c1 = c[D + d], c2 = c[2 * D + d];
+      const T dldI = gd[d] / kk;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) out[j] += dldI * ((c1 - c0) * dw1[j] + (c2 - c0) * dw2[j]);
+    }
   }
 }
 
+// General per-pixel form for wide features (D > 8): one thread per pixel, float atomics.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_raster_bwd_atomic(
     int B, int H, int W, int64_t F, int D, const T *__restrict__ grad, const int64_t *face_idx,
@@ -240,81 +251,115 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_atomic(
   for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total;
        p += (int64_t)gridDim.x * kBlock) {
     const int64_t fi = face_idx[p];
-    if (fi < 0) continue;
+    if (fi < 0 || fi >= F) continue;
     const int64_t b = p / P;
     const int64_t tf = b * F + fi;
     const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
+    const T *g = grad + p * D;
+    if (grad_feat)
+      for (int ii = 0; ii < 3; ++ii)
+        for (int d = 0; d < D; ++d) atomicAdd(grad_feat + tf * 3 * D + ii * D + d, g[d] * wts[ii]);
+    const T *v = fvi + tf * 6;
+    const T *c = feat + tf * 3 * D;
+    // same terms as raster_bwd_pixel, features streamed one at a time
+    const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
+    const T x0 = wts[0] * ax + wts[1] * bx + wts[2] * cx;
+    const T y0 = wts[0] * ay + wts[1] * by + wts[2] * cy;
+    const T m = bx - ax, pp = by - ay, n = cx - ax, q = cy - ay, s = x0 - ax, t = y0 - ay;
+    const T k1 = s * q - n * t, k2 = m * t - s * pp;
+    T k3 = m * q - n * pp;
+    k3 = (T)((double)k3 + copysign((double)eps, (double)k3));
+    const T zero = (T)0;
+    const T dw1dm = zero * k3 - q * k1, dw1dn = -t * k3 - (-pp) * k1;
+    const T dw1dp = zero * k3 - (-n) * k1, dw1dq = s * k3 - m * k1;
+    const T dw1ds = q * k3 - zero * k1, dw1dt = -n * k3 - zero * k1;
+    const T dw2dm = t * k3 - q * k2, dw2dn = zero * k3 - (-pp) * k2;
+    const T dw2dp = -s * k3 - (-n) * k2, dw2dq = zero * k3 - m * k2;
+    const T dw2ds = -pp * k3 - zero * k2, dw2dt = m * k3 - zero * k2;
+    const T dw1[6] = {-(dw1dm + dw1dn + dw1ds), -(dw1dp + dw1dq + dw1dt), dw1dm, dw1dp, dw1dn,
+                      dw1dq};
+    const T dw2[6] = {-(dw2dm + dw2dn + dw2ds), -(dw2dp + dw2dq + dw2dt), dw2dm, dw2dp, dw2dn,
+                      dw2dq};
     T gv[6] = {0, 0, 0, 0, 0, 0};
-    T *gf = grad_feat ? grad_feat + tf * 3 * D : nullptr;
-    raster_bwd_pixel<T>(fvi + tf * 6, wts, grad + p * D, feat + tf * 3 * D, D, eps, gv,
-                        [&](int ii, int d, T val) {
-                          if (gf) atomicAdd(gf + ii * D + d, val);
-                        });
+    for (int d = 0; d < D; ++d) {
+      const T c0 = c[d], c1 = c[D + d], c2 = c[2 * D + d];
+      const T dldI = g[d] / (k3 * k3);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) gv[j] += dldI * ((c1 - c0) * dw1[j] + (c2 - c0) * dw2[j]);
+    }
 #pragma unroll
     for (int j = 0; j < 6; ++j) atomicAdd(grad_fvi + tf * 6 + j, gv[j]);
   }
 }
 
-template <typename T>
-__global__ void kd_zero(T *p, int64_t n) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    p[i] = (T)0;
-}
-
-constexpr int kGatherMaxD = 8;
-
-// One thread per (view, face): sums the covered pixels of the face's own exact pixel span.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_raster_bwd_gather(
-    FaceSet<T> fs, int D, const T *__restrict__ grad, const int64_t *__restrict__ face_idx,
-    const T *__restrict__ weights, const T *__restrict__ feat, float eps, T *grad_fvi,
+// One workgroup per 16x16 tile: pixels of the same face are summed in an LDS hash table
+// (ds_add), then one float atomic per (tile, face, term) with the lanes of a face's terms
+// adjacent (its 6 corner terms and its 3*D feature terms are contiguous in memory).
+template <typename T, int DMAX>
+__global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
+    int B, int H, int W, int64_t F, int D, const T *__restrict__ grad,
+    const int64_t *__restrict__ face_idx, const T *__restrict__ weights,
+    const T *__restrict__ fvi, const T *__restrict__ feat, float eps, T *grad_fvi,
     T *grad_feat) {
-  const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= fs.N) return;
-  const int b = (int)(i / fs.F);
-  const int64_t f = i - (int64_t)b * fs.F;
-  T gv[6] = {0, 0, 0, 0, 0, 0};
-  T gf[3 * kGatherMaxD];
+  constexpr int SMAX = 6 + 3 * DMAX;
+  constexpr int HT = kBlock;  // table entries >= distinct faces of a tile
+  __shared__ int s_key[HT];
+  __shared__ T s_acc[SMAX][HT];
+  __shared__ int s_list[HT];
+  __shared__ int s_cnt[4];
+  const int S = 6 + 3 * D;
+  const int tid = threadIdx.x;
+  const int b = blockIdx.y;
+  const int ntx = (W + kTile - 1) / kTile;
+  const int px = (blockIdx.x % ntx) * kTile + (tid & 15);
+  const int py = (blockIdx.x / ntx) * kTile + (tid >> 4);
+  s_key[tid] = -1;
 #pragma unroll
-  for (int k = 0; k < 3 * kGatherMaxD; ++k) gf[k] = 0;
-  const bool ok = !fs.valid || fs.valid[i];
-  if (ok) {
-    T v[6], box[4];
-    load_corners(fs, i, v);
-    face_box(fs, i, v, box);
-    const Span s = make_span<T>(box[0], box[1], box[2], box[3], fs.M, fs.H, fs.W);
-    if (!span_empty(s)) {
-      const T *uv = fs.fvi + i * 6;  // unscaled corners: the reference backward's frame
-      T u[6];
-#pragma unroll
-      for (int k = 0; k < 6; ++k) u[k] = uv[k];
-      const T *c = feat + i * 3 * D;
-      for (int y = s.y0; y <= s.y1; ++y) {
-        const int64_t row = ((int64_t)b * fs.H + y) * fs.W;
-        for (int x = s.x0; x <= s.x1; ++x) {
-          const int64_t p = row + x;
-          if (face_idx[p] != f) continue;
-          const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
-          raster_bwd_pixel<T>(u, wts, grad + p * D, c, D, eps, gv,
-                              [&](int ii, int d, T val) {
-#pragma unroll
-                                for (int q = 0; q < kGatherMaxD; ++q)
-                                  if (q == d) gf[ii * kGatherMaxD + q] += val;
-                              });
-        }
+  for (int j = 0; j < SMAX; ++j) s_acc[j][tid] = (T)0;
+  __syncthreads();
+  if (px < W && py < H) {
+    const int64_t p = ((int64_t)b * H + py) * W + px;
+    const int64_t f = face_idx[p];
+    if (f >= 0 && f < F) {
+      unsigned h = ((unsigned)f * 2654435761u) >> 24;
+      for (;;) {  // <= 256 keys in 256 slots: terminates
+        const int old = atomicCAS(&s_key[h], -1, (int)f);
+        if (old == -1 || old == (int)f) break;
+        h = (h + 1) & (HT - 1);
       }
+      const int64_t tf = (int64_t)b * F + f;
+      const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
+      T c[SMAX];
+#pragma unroll
+      for (int j = 0; j < SMAX; ++j) c[j] = (T)0;
+      raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, grad + p * D, feat + tf * 3 * D, D, eps, c);
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (c[j] != (T)0) atomicAdd(&s_acc[j][h], c[j]);
+#pragma unroll
+      for (int ii = 0; ii < 3; ++ii)
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          if (d < D && c[6 + ii * DMAX + d] != (T)0)
+            atomicAdd(&s_acc[6 + ii * D + d][h], c[6 + ii * DMAX + d]);
     }
   }
-  T *go = grad_fvi + i * 6;
-#pragma unroll
-  for (int k = 0; k < 6; ++k) go[k] = gv[k];
-  if (grad_feat) {
-    T *gfo = grad_feat + i * 3 * D;
-    for (int ii = 0; ii < 3; ++ii)
-#pragma unroll
-      for (int q = 0; q < kGatherMaxD; ++q)
-        if (q < D) gfo[ii * D + q] = gf[ii * kGatherMaxD + q];
+  __syncthreads();
+  int nocc;
+  const bool occ = s_key[tid] >= 0;
+  const int pos = wg_compact(occ, s_cnt, nocc);
+  if (occ) s_list[pos] = tid;
+  __syncthreads();
+  for (int idx = tid; idx < nocc * S; idx += kBlock) {
+    const int i = idx / S, j = idx - i * S;
+    const int slot = s_list[i];
+    const T v = s_acc[j][slot];
+    if (v == (T)0) continue;
+    const int64_t row = (int64_t)b * F + s_key[slot];
+    if (j < 6)
+      atomicAdd(grad_fvi + row * 6 + j, v);
+    else if (grad_feat)
+      atomicAdd(grad_feat + row * 3 * D + (j - 6), v);
   }
 }
 
@@ -335,7 +380,10 @@ int raster_forward(const FaceSet<T> &fs, int64_t max_per_view, const T *fvz, con
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> a{fs, bb, fvz, feat, D, eps, interp, face_idx, weights};
   const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
-  hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+  {
+    ProfScope prof(K_RASTER_FWD, stream);
+    hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster fwd: %s", hipGetErrorString(e));
   return KD_OK;
@@ -347,47 +395,31 @@ int raster_backward(int B, int H, int W, int64_t F, int D, const T *grad, const 
                     hipStream_t stream) {
   const int64_t nf = (int64_t)B * F;
   if (nf > 0) {
-    hipLaunchKernelGGL(kd_zero<T>, dim3(1024), dim3(256), 0, stream, gfvi, nf * 6);
-    if (gfeat) hipLaunchKernelGGL(kd_zero<T>, dim3(1024), dim3(256), 0, stream, gfeat, nf * 3 * D);
+    hipError_t e = hipMemsetAsync(gfvi, 0, sizeof(T) * nf * 6, stream);
+    if (e == hipSuccess && gfeat) e = hipMemsetAsync(gfeat, 0, sizeof(T) * nf * 3 * D, stream);
+    if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
   }
   const int64_t total = (int64_t)B * H * W;
   if (total > 0 && nf > 0) {
-    const int64_t blocks = (total + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(kd_raster_bwd_atomic<T>, dim3((unsigned)(blocks < 65536 ? blocks : 65536)),
-                       dim3(kBlock), 0, stream, B, H, W, F, D, grad, fidx, weights, fvi, feat, eps,
-                       gfvi, gfeat);
+    const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    if (D <= 4) {
+      ProfScope prof(K_RASTER_BWD_TILE, stream);
+      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 4>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
+                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat);
+    } else if (D <= 8) {
+      ProfScope prof(K_RASTER_BWD_TILE, stream);
+      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 8>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
+                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat);
+    } else {
+      const int64_t blocks = (total + kBlock - 1) / kBlock;
+      ProfScope prof(K_RASTER_BWD_ATOMIC, stream);
+      hipLaunchKernelGGL(kd_raster_bwd_atomic<T>,
+                         dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(kBlock), 0,
+                         stream, B, H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat);
+    }
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster bwd: %s", hipGetErrorString(e));
-  return KD_OK;
-}
-
-template <typename T>
-int raster_backward_gather(int B, int H, int W, int64_t F, int D, const T *grad,
-                           const int64_t *fidx, const T *weights, const T *fvi, const T *feat,
-                           const uint8_t *valid, double M, float eps, T *gfvi, T *gfeat,
-                           hipStream_t stream) {
-  if (D > kGatherMaxD)  // wide features: the general form
-    return raster_backward<T>(B, H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
-                              stream);
-  FaceSet<T> fs{};
-  fs.B = B;
-  fs.H = H;
-  fs.W = W;
-  fs.N = (int64_t)B * F;
-  fs.F = F;
-  fs.fvi = fvi;
-  fs.scale = (T)M;
-  fs.valid = valid;
-  fs.M = (float)M;
-  if (fs.N > 0) {
-    hipLaunchKernelGGL(kd_raster_bwd_gather<T>, dim3((unsigned)((fs.N + kBlock - 1) / kBlock)),
-                       dim3(kBlock), 0, stream, fs, D, grad, fidx, weights, feat, eps, gfvi,
-                       gfeat);
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess)
-    return set_error(KD_ERR_LAUNCH, "raster bwd gather: %s", hipGetErrorString(e));
   return KD_OK;
 }
 
@@ -492,31 +524,6 @@ int kd_rasterize_backward_f64(int B, int H, int W, int64_t F, int D, const doubl
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
   return raster_backward<double>(B, H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
                                  (hipStream_t)stream);
-}
-
-int kd_rasterize_backward_gather_f32(int B, int H, int W, int64_t F, int D, const float *grad,
-                                     const int64_t *fidx, const float *weights, const float *fvi,
-                                     const float *feat, const uint8_t *valid, double M, float eps,
-                                     float *gfvi, float *gfeat, void *ws, size_t wsb,
-                                     void *stream) {
-  (void)ws;
-  (void)wsb;
-  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
-  KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
-  return raster_backward_gather<float>(B, H, W, F, D, grad, fidx, weights, fvi, feat, valid, M,
-                                       eps, gfvi, gfeat, (hipStream_t)stream);
-}
-int kd_rasterize_backward_gather_f64(int B, int H, int W, int64_t F, int D, const double *grad,
-                                     const int64_t *fidx, const double *weights,
-                                     const double *fvi, const double *feat, const uint8_t *valid,
-                                     double M, float eps, double *gfvi, double *gfeat, void *ws,
-                                     size_t wsb, void *stream) {
-  (void)ws;
-  (void)wsb;
-  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
-  KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
-  return raster_backward_gather<double>(B, H, W, F, D, grad, fidx, weights, fvi, feat, valid, M,
-                                        eps, gfvi, gfeat, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -4,10 +4,10 @@ The reference's ``DibrSoftMaskCuda`` (dibr.py:27-73) scales the coordinates, bui
 boxes, runs the per-pixel all-faces scan and saves the (B, H, W, K) close-face lists
 (prob / int64 idx / uint8 type, 13*K bytes per pixel) for its backward.  Here the scaling and
 boxes are computed in the kernel, the scan runs over ordered tile bins, and by default the lists
-are NOT materialised: the backward (face-gather, deterministic) re-derives each face's membership
-in a pixel's first-K list from one int32 per pixel (``close_last``) and recomputes the
-distance type / probability bit-identically.  Set ``SAVE_CLOSE_LISTS = True`` to materialise the
-lists and use the reference-structured atomic backward instead (same results to float-sum order).
+are NOT materialised: the backward re-derives every uncovered pixel's first-K close faces over the
+same bins (kept from the forward) and recomputes the distance types / probabilities
+bit-identically.  Set ``SAVE_CLOSE_LISTS = True`` to materialise the lists and use the
+reference-structured atomic backward instead (same results up to float-sum order).
 """
 import torch
 from torch.autograd import Function
@@ -30,18 +30,20 @@ class DibrSoftMaskCuda(Function):
         face_vertices_image = face_vertices_image.contiguous()
         selected_face_idx = selected_face_idx.contiguous()
         lists = SAVE_CLOSE_LISTS
-        soft_mask, close_last, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
+        soft_mask, workspace, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
             face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier,
             with_lists=lists)
         ctx.multiplier = multiplier
         ctx.sigmainv = sigmainv
         ctx.boxlen = boxlen
+        ctx.knum = knum
         ctx.lists = lists
+        ctx.workspace = None if lists else workspace
         if lists:
             ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, prob, cidx,
                                   ctype)
         else:
-            ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, close_last)
+            ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx)
         return soft_mask
 
     @staticmethod
@@ -55,10 +57,11 @@ class DibrSoftMaskCuda(Function):
                 grad_soft_mask, soft_mask, face_idx, prob, cidx, ctype,
                 (fvi * ctx.multiplier).contiguous(), ctx.sigmainv, ctx.multiplier)
         else:
-            soft_mask, fvi, face_idx, close_last = ctx.saved_tensors
-            grad = _C.render.mesh.dibr_soft_mask_backward_gather(
-                grad_soft_mask, soft_mask, face_idx, close_last, fvi, ctx.multiplier,
-                ctx.boxlen, ctx.sigmainv)
+            soft_mask, fvi, face_idx = ctx.saved_tensors
+            grad = _C.render.mesh.dibr_soft_mask_backward_binned(
+                grad_soft_mask, soft_mask, face_idx, fvi, ctx.multiplier, ctx.boxlen,
+                ctx.sigmainv, ctx.knum, ctx.workspace)
+            ctx.workspace = None
         return grad, None, None, None, None, None
 
 

@@ -4,8 +4,8 @@ The reference's ``RasterizeCuda`` (rasterization.py:243-388) packs the valid fac
 ``torch.where`` (a device->host sync), scales, builds boxes, calls the packed kernel and remaps
 the packed index.  Here all of that happens inside one HIP launch sequence (binning + tile
 raster, kaolin_amd/csrc/kd_raster.hip) with no host sync; the outputs are bit-identical.
-The backward is the face-gather kernel (deterministic, no atomics), same math as
-rasterization_cuda.cu:238-402.
+The backward is the tile kernel (per-tile LDS sums, one atomic per tile and face), same math
+as rasterization_cuda.cu:238-402.
 """
 import torch
 from torch.autograd import Function
@@ -28,8 +28,7 @@ class RasterizeCuda(Function):
             _C.render.mesh.rasterize_forward_fused(
                 height, width, face_vertices_z, face_vertices_image, face_features,
                 valid_faces, multiplier, eps)
-        ctx.save_for_backward(face_idx, output_weights, face_vertices_image, face_features,
-                              valid_u8)
+        ctx.save_for_backward(face_idx, output_weights, face_vertices_image, face_features)
         ctx.mark_non_differentiable(face_idx)
         ctx.eps = eps
         ctx.multiplier = multiplier
@@ -37,15 +36,13 @@ class RasterizeCuda(Function):
 
     @staticmethod
     def backward(ctx, grad_interpolated_features, grad_face_idx):
-        face_idx, output_weights, face_vertices_image, face_features, valid_u8 = \
-            ctx.saved_tensors
+        face_idx, output_weights, face_vertices_image, face_features = ctx.saved_tensors
         need_fvi, need_feat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         if not (need_fvi or need_feat):
             return None, None, None, None, None, None, None, None
-        grad_fvi, grad_feat = _C.render.mesh.rasterize_backward_gather(
+        grad_fvi, grad_feat = _C.render.mesh.rasterize_backward_autograd(
             grad_interpolated_features.contiguous(), face_idx, output_weights,
-            face_vertices_image, face_features, valid_u8, ctx.multiplier, ctx.eps,
-            need_feat=need_feat)
+            face_vertices_image, face_features, ctx.eps, need_feat=need_feat)
         return None, None, None, grad_fvi if need_fvi else None, grad_feat, None, None, None
 
 

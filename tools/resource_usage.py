@@ -1,0 +1,28 @@
+"""Per-kernel VGPR / scratch / LDS / occupancy of the gfx950 build (hipcc -Rpass-analysis)."""
+import os
+import re
+import subprocess
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'kaolin_amd',
+                    'csrc')
+for f in ('kd_binning', 'kd_raster', 'kd_softmask'):
+    out = subprocess.run(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off',
+                          '--offload-arch=gfx950', '-c', f'{f}.hip', '-o', '/tmp/kd_ru.o',
+                          '-Rpass-analysis=kernel-resource-usage'], cwd=CSRC,
+                         capture_output=True, text=True).stderr
+    cur = None
+    for line in out.splitlines():
+        m = re.search(r'Function Name: (\S+)', line)
+        if m:
+            cur = {'name': m.group(1)}
+            continue
+        for key, pat in (('vgpr', r'VGPRs: (\d+)'), ('scratch', r'ScratchSize \[bytes/lane\]: (\d+)'),
+                         ('lds', r'LDS Size \[bytes/block\]: (\d+)'),
+                         ('occ', r'Occupancy \[waves/SIMD\]: (\d+)')):
+            m = re.search(pat, line)
+            if m and cur is not None:
+                cur[key] = m.group(1)
+        if cur and 'occ' in cur:
+            print(f"{cur['name'][:64]:64s} vgpr={cur.get('vgpr')} scratch={cur.get('scratch')} "
+                  f"lds={cur.get('lds')} occ={cur.get('occ')}")
+            cur = None
