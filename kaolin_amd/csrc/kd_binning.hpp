@@ -1,4 +1,4 @@
-// kd_binning.hpp -- ordered coarse binning of faces into 64x64-pixel (or larger) tiles.
+// kd_binning.hpp -- ordered coarse binning of faces into 32x32-pixel (or larger) tiles.
 //
 // The reference scans every face for every pixel (rasterization_cuda.cu:88-171,
 // dibr_soft_mask_cuda.cu:80-172).  Its results depend on face ORDER: the raster keeps the first

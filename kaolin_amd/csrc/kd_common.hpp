@@ -251,7 +251,7 @@ struct BinGeom {
 
 __host__ __device__ inline BinGeom bin_geom(int H, int W) {
   int m = H > W ? H : W;
-  int ct = 64;
+  int ct = 32;
   while (((m + ct - 1) / ct) > 32) ct *= 2;
   BinGeom g;
   g.ct = ct;

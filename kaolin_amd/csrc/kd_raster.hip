@@ -1,13 +1,14 @@
 // kd_raster.hip -- rasterize forward / backward for gfx950.
 //
 // Forward (replaces packed_rasterize_forward_cuda_kernel, rasterization_cuda.cu:43-192):
-//   one 256-thread workgroup per 16x16 pixel tile, one wave per 8x8 sub-tile.
+//   one 256-thread workgroup per 16x16 pixel tile, one wave per 8x8 sub-tile (kd_tile.hpp).
 //   The workgroup walks its coarse bin (ascending face order), keeps the faces whose exact pixel
-//   span touches the tile (ballot compaction, order preserved) and stages their corners, depths
-//   and boxes in LDS (SoA).  Each wave then compacts the faces touching its 8x8 sub-tile and every
-//   lane (pixel) runs the reference's exact per-face test over that short list with LDS broadcast
-//   reads: the same sequence of faces the reference visits, minus faces whose box provably
-//   misses the pixel, so face_idx / weights / features are bit-identical.
+//   span touches the tile and stages their corners and depths in LDS (SoA).  Each wave keeps the
+//   spans of the faces touching its 8x8 sub-tile in registers; every lane (pixel) walks them in
+//   order (readlane broadcast), and for the faces whose box holds its centre runs the
+//   reference's exact test with LDS broadcast reads: the same sequence of faces the reference
+//   visits, minus faces whose box misses the pixel, so face_idx / weights / features are
+//   bit-identical.
 // Backward (replaces rasterize_backward_cuda_kernel, rasterization_cuda.cu:238-402):
 //   kd_raster_bwd_tile    -- one workgroup per 16x16 tile; a pixel's terms (6 corner terms summed
 //                            over the features, 3*D feature terms) are summed per face in an LDS
@@ -17,6 +18,7 @@
 #include "../../include/kaolin_dibr.h"
 #include "kd_binning.hpp"
 #include "kd_capi.hpp"
+#include "kd_tile.hpp"
 
 namespace kd {
 
@@ -33,16 +35,9 @@ struct RasterFwdArgs {
   T *weights;
 };
 
-template <typename T>
-struct RasterCap {
-  static constexpr int value = 512;
-};
-template <>
-struct RasterCap<double> {
-  static constexpr int value = 256;
-};
-
-// The reference per-face test (rasterization_cuda.cu:115-169) for one pixel.
+// The reference per-face test (rasterization_cuda.cu:131-159) for one pixel whose centre passed
+// the box test: edge functions, eps-normalised barycentrics (division before the sign test,
+// exactly as the reference), depth.
 template <typename T>
 __device__ __forceinline__ bool raster_face_test(T x0, T y0, T ax, T ay, T bx, T by, T cx, T cy,
                                                  T az, T bz, T cz, float eps, T &w0, T &w1,
@@ -65,110 +60,63 @@ __device__ __forceinline__ bool raster_face_test(T x0, T y0, T ax, T ay, T bx, T
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
-  constexpr int CAP = RasterCap<T>::value;
-  __shared__ int s_f[CAP];
-  __shared__ Span s_span[CAP];
-  __shared__ T s_geo[13][CAP];  // ax ay bx by cx cy az bz cz xmin ymin xmax ymax
-  __shared__ unsigned short s_sub[4][CAP];
-  __shared__ int s_cnt[4];
+  __shared__ TileLists L;
+  __shared__ T s_geo[9][kCap];  // ax ay bx by cx cy (scaled), az bz cz
 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const int b = blockIdx.y;
-  const int ntx = (W + kTile - 1) / kTile;
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-
-  const int X0 = tx * kTile, Y0 = ty * kTile;
-  const int X1 = min(X0 + kTile - 1, W - 1), Y1 = min(Y0 + kTile - 1, H - 1);
-  const int WX0 = X0 + (w & 1) * 8, WY0 = Y0 + (w >> 1) * 8;
-  const int WX1 = min(WX0 + 7, W - 1), WY1 = min(WY0 + 7, H - 1);
-  const int px = WX0 + (lane & 7), py = WY0 + (lane >> 3);
-  const bool inimg = px < W && py < H;
-  const T x0 = (T)px_cx(fs.M, W, px);
-  const T y0 = (T)px_cy(fs.M, H, py);
+  const TileGeom t = tile_geom(H, W);
+  const T x0 = (T)px_cx(fs.M, W, t.px);
+  const T y0 = (T)px_cy(fs.M, H, t.py);
 
   T max_z0 = (T)-INFINITY;
   int best = -1;
   T bw0 = 0., bw1 = 0., bw2 = 0.;
 
-  const BinGeom &g = a.bb.g;
-  const int ct = (Y0 / g.ct) * g.nctx + (X0 / g.ct);
-  const int n = a.bb.totals[(int64_t)b * g.nct() + ct];
-  const int *bin = a.bb.bins + (int64_t)ct * fs.N + lo;
-  const bool wave_live = WX0 < W && WY0 < H;
-
-  int cnt = 0;
-  for (int base = 0; base < n; base += kBlock) {
-    const int e = base + tid;
-    int f = 0;
-    bool ov = false;
-    Span sp;
-    if (e < n) {
-      f = bin[e];
-      sp = a.bb.spans[lo + f];
-      ov = span_overlaps(sp, X0, X1, Y0, Y1);
-    }
-    int tot;
-    const int pos = wg_compact(ov, s_cnt, tot);
-    if (ov) {
-      s_f[cnt + pos] = f;
-      s_span[cnt + pos] = sp;
-    }
-    cnt += tot;
-    if (cnt > CAP - kBlock || base + kBlock >= n) {
-      __syncthreads();
-      for (int k = tid; k < cnt; k += kBlock) {
-        const int64_t fi = lo + s_f[k];
-        T v[6], box[4];
-        load_corners(fs, fi, v);
-        face_box(fs, fi, v, box);
+  auto stage = [&](int k, int64_t fi) {
+    T v[6];
+    load_corners(fs, fi, v);
 #pragma unroll
-        for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
-        const T *zz = a.fvz + fi * 3;
-        s_geo[6][k] = zz[0];
-        s_geo[7][k] = zz[1];
-        s_geo[8][k] = zz[2];
+    for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
+    const T *zz = a.fvz + fi * 3;
+    s_geo[6][k] = zz[0];
+    s_geo[7][k] = zz[1];
+    s_geo[8][k] = zz[2];
+  };
+  auto round = [&](int nsub, int) {
+    if (nsub == 0) return;
+    const SubSpans ss = load_subspans(L, nsub);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) s_geo[9 + q][k] = box[q];
+    for (int c = 0; c < 4; ++c) {
+      if (c * kWave >= nsub) break;
+      const int nj = min(kWave, nsub - c * kWave);
+      for (int l = 0; l < nj; ++l) {  // the sub-list in ascending face order
+        PSpan sp;
+        sp.lo = (uint32_t)__builtin_amdgcn_readlane((int)ss.s[c].lo, l);
+        sp.hi = (uint32_t)__builtin_amdgcn_readlane((int)ss.s[c].hi, l);
+        if (!t.inimg || !pspan_has(sp, t.px, t.py)) continue;  // :115, exact on spans
+        const int k = __builtin_amdgcn_readlane(ss.k[c], l);
+        T w0, w1, w2, z0;
+        if (!raster_face_test<T>(x0, y0, s_geo[0][k], s_geo[1][k], s_geo[2][k], s_geo[3][k],
+                                 s_geo[4][k], s_geo[5][k], s_geo[6][k], s_geo[7][k],
+                                 s_geo[8][k], a.eps, w0, w1, w2, z0))
+          continue;
+        if (z0 <= max_z0) continue;  // :162, strict: ties keep the lower index
+        max_z0 = z0;
+        best = L.f[k];
+        bw0 = w0;
+        bw1 = w1;
+        bw2 = w2;
       }
-      int nsub = 0;
-      for (int k0 = 0; k0 < cnt; k0 += kWave) {
-        const int k = k0 + lane;
-        const bool ok = wave_live && k < cnt && span_overlaps(s_span[k], WX0, WX1, WY0, WY1);
-        const uint64_t m = __ballot(ok);
-        if (ok) s_sub[w][nsub + mbcnt(m)] = (unsigned short)k;
-        nsub += __popcll(m);
-      }
-      __syncthreads();
-      if (inimg) {
-        for (int j = 0; j < nsub; ++j) {
-          const int k = s_sub[w][j];
-          const T xmin = s_geo[9][k], ymin = s_geo[10][k], xmax = s_geo[11][k],
-                  ymax = s_geo[12][k];
-          if (x0 < xmin || x0 >= xmax || y0 < ymin || y0 >= ymax) continue;
-          T w0, w1, w2, z0;
-          if (!raster_face_test<T>(x0, y0, s_geo[0][k], s_geo[1][k], s_geo[2][k], s_geo[3][k],
-                                   s_geo[4][k], s_geo[5][k], s_geo[6][k], s_geo[7][k],
-                                   s_geo[8][k], a.eps, w0, w1, w2, z0))
-            continue;
-          if (z0 <= max_z0) continue;
-          max_z0 = z0;
-          best = s_f[k];
-          bw0 = w0;
-          bw1 = w1;
-          bw2 = w2;
-        }
-      }
-      __syncthreads();
-      cnt = 0;
     }
-  }
+  };
+  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round);
 
-  if (!inimg) return;
-  const int64_t p = ((int64_t)b * H + py) * W + px;
+  if (!t.inimg) return;
+  const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   a.face_idx[p] = best;
   T *wo = a.weights + p * 3;
   T *io = a.interp + p * a.D;
@@ -292,9 +240,13 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_atomic(
   }
 }
 
-// One workgroup per 16x16 tile: pixels of the same face are summed in an LDS hash table
-// (ds_add), then one float atomic per (tile, face, term) with the lanes of a face's terms
-// adjacent (its 6 corner terms and its 3*D feature terms are contiguous in memory).
+// One workgroup per 16x16 tile.  Every pixel writes its terms to LDS; pixels are grouped by face
+// without any contended atomics: an LDS hash table gives each face a slot, a 256-bit pixel mask
+// per slot gives each pixel its rank among the slot's pixels (popcount), a prefix sum over the
+// slots turns (slot, rank) into a position, and the tile sum of each (face, term) is then
+// added in ascending pixel order by one lane -- deterministic within the tile -- and flushed with
+// one float atomic per (tile, face, term), a face's terms on adjacent lanes (its 6 corner terms
+// and its 3*D feature terms are contiguous in memory).
 template <typename T, int DMAX>
 __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
     int B, int H, int W, int64_t F, int D, const T *__restrict__ grad,
@@ -302,9 +254,12 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
     const T *__restrict__ fvi, const T *__restrict__ feat, float eps, T *grad_fvi,
     T *grad_feat) {
   constexpr int SMAX = 6 + 3 * DMAX;
-  constexpr int HT = kBlock;  // table entries >= distinct faces of a tile
+  constexpr int HT = kBlock;  // slots >= distinct faces of a tile
   __shared__ int s_key[HT];
-  __shared__ T s_acc[SMAX][HT];
+  __shared__ uint32_t s_mask[HT][8];
+  __shared__ T s_con[kBlock][SMAX + 1];
+  __shared__ short s_off[HT];
+  __shared__ unsigned char s_ord[kBlock];
   __shared__ int s_list[HT];
   __shared__ int s_cnt[4];
   const int S = 6 + 3 * D;
@@ -315,45 +270,63 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   const int py = (blockIdx.x / ntx) * kTile + (tid >> 4);
   s_key[tid] = -1;
 #pragma unroll
-  for (int j = 0; j < SMAX; ++j) s_acc[j][tid] = (T)0;
+  for (int k = 0; k < 8; ++k) s_mask[tid][k] = 0u;
   __syncthreads();
+  int h = -1;
   if (px < W && py < H) {
     const int64_t p = ((int64_t)b * H + py) * W + px;
     const int64_t f = face_idx[p];
     if (f >= 0 && f < F) {
-      unsigned h = ((unsigned)f * 2654435761u) >> 24;
+      unsigned u = ((unsigned)f * 2654435761u) >> 24;
       for (;;) {  // <= 256 keys in 256 slots: terminates
-        const int old = atomicCAS(&s_key[h], -1, (int)f);
+        const int old = atomicCAS(&s_key[u], -1, (int)f);
         if (old == -1 || old == (int)f) break;
-        h = (h + 1) & (HT - 1);
+        u = (u + 1) & (HT - 1);
       }
+      h = (int)u;
+      atomicOr(&s_mask[h][tid >> 5], 1u << (tid & 31));
       const int64_t tf = (int64_t)b * F + f;
       const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
       T c[SMAX];
-#pragma unroll
-      for (int j = 0; j < SMAX; ++j) c[j] = (T)0;
       raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, grad + p * D, feat + tf * 3 * D, D, eps, c);
 #pragma unroll
-      for (int j = 0; j < 6; ++j)
-        if (c[j] != (T)0) atomicAdd(&s_acc[j][h], c[j]);
+      for (int j = 0; j < 6; ++j) s_con[tid][j] = c[j];
 #pragma unroll
       for (int ii = 0; ii < 3; ++ii)
 #pragma unroll
         for (int d = 0; d < DMAX; ++d)
-          if (d < D && c[6 + ii * DMAX + d] != (T)0)
-            atomicAdd(&s_acc[6 + ii * D + d][h], c[6 + ii * DMAX + d]);
+          if (d < D) s_con[tid][6 + ii * D + d] = c[6 + ii * DMAX + d];
     }
   }
   __syncthreads();
+  // slot sizes -> positions (prefix sum over slots), and the list of occupied slots
+  int sz = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) sz += __popc(s_mask[tid][k]);
+  int total;
+  const int off = wg_exclusive_scan(sz, s_cnt, total);
+  s_off[tid] = (short)off;
   int nocc;
-  const bool occ = s_key[tid] >= 0;
+  const bool occ = sz > 0;
   const int pos = wg_compact(occ, s_cnt, nocc);
   if (occ) s_list[pos] = tid;
+  int rank = 0;
+  if (h >= 0) {
+    rank = __popc(s_mask[h][tid >> 5] & ((1u << (tid & 31)) - 1u));
+    for (int k = 0; k < (tid >> 5); ++k) rank += __popc(s_mask[h][k]);
+  }
+  __syncthreads();
+  if (h >= 0) s_ord[s_off[h] + rank] = (unsigned char)tid;
   __syncthreads();
   for (int idx = tid; idx < nocc * S; idx += kBlock) {
     const int i = idx / S, j = idx - i * S;
     const int slot = s_list[i];
-    const T v = s_acc[j][slot];
+    int n = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) n += __popc(s_mask[slot][k]);
+    const int o = s_off[slot];
+    T v = (T)0;
+    for (int r = 0; r < n; ++r) v += s_con[s_ord[o + r]][j];
     if (v == (T)0) continue;
     const int64_t row = (int64_t)b * F + s_key[slot];
     if (j < 6)

@@ -109,14 +109,6 @@ __device__ __forceinline__ void soft_bwd_terms(T x0, T y0, const T v[6], int edg
   }
 }
 
-template <typename T>
-struct SoftCap {
-  static constexpr int value = 512;
-};
-template <>
-struct SoftCap<double> {
-  static constexpr int value = 256;
-};
 constexpr int kPairCap = 512;  // (pixel, face) pairs per wave batch
 
 template <typename T>
@@ -138,21 +130,19 @@ struct SoftArgs {
   T *grad_fvi;
 };
 
-// Per-wave pair list and the per-pixel bookkeeping of the current batch.
-template <typename T>
-struct PairLds {
-  unsigned short pair[4][kPairCap];  // (q << 9) | k, q = pixel lane, k = tile-list entry
-  T val[4][kPairCap];                // forward: probability of the pair
+// Per-wave pair list of the current batch and its per-pixel bookkeeping.
+struct PairBook {
+  unsigned short pair[4][kPairCap];  // (q << 8) | k, q = pixel lane, k = tile-list entry
   short start[4][64], n[4][64], base[4][64];
-  T px_a[4][64], px_b[4][64];        // backward: grad_soft, soft of pixel q
 };
 
-// Pass A over the uncovered pixels of this wave for one batch of tile faces.  Calls
-// flush(npairs) whenever the pair list is full and at the end.
-template <typename T, int CAP, typename Flush>
-__device__ __forceinline__ void soft_pass_a(const TileLists<CAP> &L, const T (*geo)[CAP],
-                                            PairLds<T> &P, int nsub, uint64_t umask, int K,
-                                            T x0, T y0, int &my_kid, Flush flush) {
+// Pass A over the uncovered pixels of this wave for one batch of tile faces: per pixel, the
+// first K - kid hits (ascending face order = ascending ballot rank) are appended to the pair
+// list.  flush(npairs) runs passes B / C whenever the list is full and at the end.
+template <typename Flush>
+__device__ __forceinline__ void soft_pass_a(const SubSpans &ss, int nsub, PairBook &P,
+                                            uint64_t umask, int K, const TileGeom &t,
+                                            int &my_kid, Flush flush) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int npairs = 0;
   P.n[w][lane] = 0;
@@ -160,17 +150,12 @@ __device__ __forceinline__ void soft_pass_a(const TileLists<CAP> &L, const T (*g
     const int q = __builtin_ctzll(mm);
     int kid = rdlane_i(my_kid, q);
     if (kid >= K) continue;
-    const T qx = rdlane(x0, q), qy = rdlane(y0, q);
+    const int qx = t.WX0 + (q & 7), qy = t.WY0 + (q >> 3);
     int start = npairs, base = kid;
-    for (int j0 = 0; j0 < nsub && kid < K; j0 += kWave) {
-      const int j = j0 + lane;
-      bool hit = false;
-      int k = 0;
-      if (j < nsub) {
-        k = L.sub[w][j];
-        hit = !(qx < geo[6][k] || qx >= geo[8][k] || qy < geo[7][k] ||
-                qy >= geo[9][k]);  // dibr_soft_mask_cuda.cu:95
-      }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c * kWave >= nsub || kid >= K) break;
+      const bool hit = pspan_has(ss.s[c], qx, qy);  // dibr_soft_mask_cuda.cu:95, exact
       const uint64_t hm = __ballot(hit);
       if (!hm) continue;
       const int need = K - kid;
@@ -188,7 +173,7 @@ __device__ __forceinline__ void soft_pass_a(const TileLists<CAP> &L, const T (*g
         base = kid;
       }
       const int rank = mbcnt(hm);
-      if (hit && rank < need) P.pair[w][npairs + rank] = (unsigned short)((q << 9) | k);
+      if (hit && rank < need) P.pair[w][npairs + rank] = (unsigned short)((q << 8) | ss.k[c]);
       npairs += ntake;
       kid += ntake;
     }
@@ -202,12 +187,21 @@ __device__ __forceinline__ void soft_pass_a(const TileLists<CAP> &L, const T (*g
   flush(npairs);
 }
 
+template <typename T>
+__device__ __forceinline__ void soft_stage(const FaceSet<T> &fs, T (*geo)[kCap], int k,
+                                           int64_t fi) {
+  T v[6];
+  load_corners(fs, fi, v);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) geo[q][k] = v[q];
+}
+
 template <typename T, bool LISTS>
 __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
-  constexpr int CAP = SoftCap<T>::value;
-  __shared__ TileLists<CAP> L;
-  __shared__ T s_geo[10][CAP];  // x0 y0 x1 y1 x2 y2 (scaled corners), xmin ymin xmax ymax
-  __shared__ PairLds<T> P;
+  __shared__ TileLists L;
+  __shared__ T s_geo[6][kCap];  // scaled corners
+  __shared__ PairBook P;
+  __shared__ T s_val[4][kPairCap];  // probability of each pair
 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
@@ -217,8 +211,6 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   const TileGeom t = tile_geom(H, W);
-  const T x0 = (T)px_cx(M, W, t.px);
-  const T y0 = (T)px_cy(M, H, t.py);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const bool covered = t.inimg && a.face_idx[p] >= 0;
   const bool unc = t.inimg && !covered;
@@ -228,20 +220,12 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
   bool any_sub = false;
 
   if (__syncthreads_or(unc)) {
-    auto stage = [&](int k, int64_t fi) {
-      T v[6], box[4];
-      load_corners(fs, fi, v);
-      face_box(fs, fi, v, box);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) s_geo[6 + q][k] = box[q];
-    };
+    auto stage = [&](int k, int64_t fi) { soft_stage(fs, s_geo, k, fi); };
     auto flush = [&](int npairs) {  // passes B and C
       wave_lds_sync();
       for (int e = lane; e < npairs; e += kWave) {
         const int pr = P.pair[w][e];
-        const int q = pr >> 9, k = pr & 511;
+        const int q = pr >> 8, k = pr & 255;
         const int qx = t.WX0 + (q & 7), qy = t.WY0 + (q >> 3);
         T v[6];
 #pragma unroll
@@ -249,7 +233,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
         int et;
         T pb;
         soft_face_dist<T>((T)px_cx(M, W, qx), (T)px_cy(M, H, qy), v, M, a.sigmainv, et, pb);
-        P.val[w][e] = pb;
+        s_val[w][e] = pb;
         const int slot = P.base[w][q] + (e - P.start[w][q]);
         const int64_t qp = ((int64_t)b * H + qy) * W + qx;
         if (LISTS) {
@@ -264,7 +248,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
       const int nq = P.n[w][lane];
       const int sq = P.start[w][lane];
       for (int i = 0; i < nq; ++i)  // dibr_soft_mask_cuda.cu:174-178, slot order
-        my_prod = (T)((double)my_prod * (1.0 - (double)P.val[w][sq + i]));
+        my_prod = (T)((double)my_prod * (1.0 - (double)s_val[w][sq + i]));
       wave_lds_sync();
       P.n[w][lane] = 0;
       wave_lds_sync();
@@ -272,9 +256,10 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
     auto round = [&](int nsub, int) {
       if (!umask || nsub == 0) return;
       any_sub = true;
-      soft_pass_a<T, CAP>(L, s_geo, P, nsub, umask, K, x0, y0, my_kid, flush);
+      const SubSpans ss = load_subspans(L, nsub);
+      soft_pass_a(ss, nsub, P, umask, K, t, my_kid, flush);
     };
-    tile_rounds<CAP>(L, a.bb, fs.N, b, lo, t, stage, round);
+    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round);
   }
 
   if (!t.wave_live) return;
@@ -312,11 +297,11 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_bwd_tile(SoftArgs<T> a) {
-  constexpr int CAP = SoftCap<T>::value;
-  __shared__ TileLists<CAP> L;
-  __shared__ T s_geo[10][CAP];
-  __shared__ T s_acc[6][CAP];
-  __shared__ PairLds<T> P;
+  __shared__ TileLists L;
+  __shared__ T s_geo[6][kCap];
+  __shared__ T s_acc[6][kCap];
+  __shared__ PairBook P;
+  __shared__ T s_pg[4][64], s_ps[4][64];  // grad_soft, soft of each pixel
 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
@@ -326,32 +311,24 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_tile(SoftArgs<T> a) {
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   const TileGeom t = tile_geom(H, W);
-  const T x0 = (T)px_cx(M, W, t.px);
-  const T y0 = (T)px_cy(M, H, t.py);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const bool unc = t.inimg && a.face_idx[p] < 0;
   const uint64_t umask = __ballot(unc);
   int my_kid = 0;
   if (!__syncthreads_or(unc)) return;
-  P.px_a[w][lane] = unc ? a.grad_soft[p] : (T)0;
-  P.px_b[w][lane] = unc ? a.soft_in[p] : (T)0;
+  s_pg[w][lane] = unc ? a.grad_soft[p] : (T)0;
+  s_ps[w][lane] = unc ? a.soft_in[p] : (T)0;
 
   auto stage = [&](int k, int64_t fi) {
-    T v[6], box[4];
-    load_corners(fs, fi, v);
-    face_box(fs, fi, v, box);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) s_geo[6 + q][k] = box[q];
+    soft_stage(fs, s_geo, k, fi);
 #pragma unroll
     for (int q = 0; q < 6; ++q) s_acc[q][k] = (T)0;
   };
-  auto flush = [&](int npairs) {  // pass B: gradient terms, accumulated per face in LDS
+  auto flush = [&](int npairs) {  // pass B: gradient terms, summed per face in LDS
     wave_lds_sync();
     for (int e = lane; e < npairs; e += kWave) {
       const int pr = P.pair[w][e];
-      const int q = pr >> 9, k = pr & 511;
+      const int q = pr >> 8, k = pr & 255;
       const int qx = t.WX0 + (q & 7), qy = t.WY0 + (q >> 3);
       const T xq = (T)px_cx(M, W, qx), yq = (T)px_cy(M, H, qy);
       T v[6];
@@ -361,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_tile(SoftArgs<T> a) {
       T pb;
       soft_face_dist<T>(xq, yq, v, M, a.sigmainv, et, pb);
       T g[6] = {0, 0, 0, 0, 0, 0};
-      soft_bwd_terms<T>(xq, yq, v, et, pb, P.px_a[w][q], P.px_b[w][q], a.sigmainv, M, g);
+      soft_bwd_terms<T>(xq, yq, v, et, pb, s_pg[w][q], s_ps[w][q], a.sigmainv, M, g);
 #pragma unroll
       for (int c = 0; c < 6; ++c)
         if (g[c] != (T)0) atomicAdd(&s_acc[c][k], g[c]);
@@ -371,8 +348,10 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_tile(SoftArgs<T> a) {
     wave_lds_sync();
   };
   auto round = [&](int nsub, int cnt) {
-    if (umask && nsub > 0)
-      soft_pass_a<T, CAP>(L, s_geo, P, nsub, umask, K, x0, y0, my_kid, flush);
+    if (umask && nsub > 0) {
+      const SubSpans ss = load_subspans(L, nsub);
+      soft_pass_a(ss, nsub, P, umask, K, t, my_kid, flush);
+    }
     __syncthreads();
     // one atomic per (face, coordinate) with a nonzero tile sum; lanes walk a face's 6
     // coordinates contiguously (24 contiguous bytes per face).
@@ -382,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_tile(SoftArgs<T> a) {
       if (v != (T)0) atomicAdd(a.grad_fvi + (lo + L.f[k]) * 6 + c, v);
     }
   };
-  tile_rounds<CAP>(L, a.bb, fs.N, b, lo, t, stage, round);
+  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round);
 }
 
 template <typename T>

@@ -4,14 +4,21 @@
 // (w & 1, w >> 1).  tile_rounds() walks the tile's ordered coarse bin, keeps the faces whose exact
 // pixel span touches the tile (ballot compaction keeps ascending face order), lets the caller
 // stage their data in LDS (stage(k, row)), builds per-wave sub-lists of the faces touching each
-// 8x8 sub-tile, and calls round(nsub) once per batch of at most CAP faces.  Across batches the
-// faces keep ascending order, so a caller that processes batches in sequence sees the faces in
-// exactly the order the reference loop does (minus faces whose box misses the pixel).
+// 8x8 sub-tile, and calls round(nsub, cnt) once per batch of at most kCap faces.  Across batches
+// the faces keep ascending order, so a caller that processes batches in sequence sees the faces
+// in exactly the order the reference loop does (minus faces whose box misses the pixel).
+//
+// The box test itself is done on the exact integer pixel spans (kd_common.hpp make_span): pixel
+// (x, y) passes the reference's half-open float box test iff x0 <= x <= x1 and y0 <= y <= y1.
+// SubSpans keeps a wave's sub-list (<= kCap = 4 x 64 entries) in registers: lane l holds entry
+// c*64 + l of chunk c, so per-pixel hit masks are 4 compares and a ballot, no LDS traffic.
 #pragma once
 
 #include "kd_binning.hpp"
 
 namespace kd {
+
+constexpr int kCap = 256;  // faces per batch (LDS list)
 
 struct TileGeom {
   int X0, X1, Y0, Y1;      // tile pixel rect (inclusive)
@@ -40,20 +47,55 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W) {
   return t;
 }
 
-template <int CAP>
 struct TileLists {
-  int f[CAP];                   // local face index (ascending)
-  Span span[CAP];
-  unsigned short sub[4][CAP];   // per-wave sub-list: indices into f[]
+  int f[kCap];                   // local face index (ascending)
+  Span span[kCap];
+  unsigned char sub[4][kCap];    // per-wave sub-list: indices into f[]
   int cnt[4];
 };
 
-// Stage(k, face_row) fills the caller's LDS arrays for list entry k;
-// Round(nsub, cnt) processes one batch of cnt tile faces (called by every thread; nsub, the
-// length of this wave's sub-list, is wave-uniform).
-template <int CAP, typename Stage, typename Round>
-__device__ __forceinline__ void tile_rounds(TileLists<CAP> &L, const BinBuffers &bb, int64_t N,
-                                            int b, int64_t lo, const TileGeom &t, Stage stage,
+// Packed span: lo = x0 | x1 << 16, hi = y0 | y1 << 16 (int16 fields, sign-extended on unpack).
+struct PSpan {
+  uint32_t lo, hi;
+};
+__device__ __forceinline__ PSpan pack_span(Span s) {
+  PSpan p;
+  p.lo = (uint32_t)(uint16_t)s.x0 | ((uint32_t)(uint16_t)s.x1 << 16);
+  p.hi = (uint32_t)(uint16_t)s.y0 | ((uint32_t)(uint16_t)s.y1 << 16);
+  return p;
+}
+__device__ __forceinline__ bool pspan_has(PSpan p, int x, int y) {
+  const int x0 = (int)(int16_t)(p.lo & 0xffff), x1 = (int)(int16_t)(p.lo >> 16);
+  const int y0 = (int)(int16_t)(p.hi & 0xffff), y1 = (int)(int16_t)(p.hi >> 16);
+  return x >= x0 && x <= x1 && y >= y0 && y <= y1;
+}
+
+struct SubSpans {
+  PSpan s[4];        // chunk c, lane l -> sub-list entry c*64 + l
+  int k[4];          // its index into the tile list
+};
+
+__device__ __forceinline__ SubSpans load_subspans(const TileLists &L, int nsub) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  SubSpans r;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const int j = c * kWave + lane;
+    if (j < nsub) {
+      r.k[c] = L.sub[w][j];
+      r.s[c] = pack_span(L.span[r.k[c]]);
+    } else {
+      r.k[c] = 0;
+      r.s[c].lo = 0xffff0001u;  // empty: x0 = 1 > x1 = -1
+      r.s[c].hi = 0xffff0001u;
+    }
+  }
+  return r;
+}
+
+template <typename Stage, typename Round>
+__device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, int64_t N, int b,
+                                            int64_t lo, const TileGeom &t, Stage stage,
                                             Round round) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const BinGeom &g = bb.g;
@@ -73,12 +115,8 @@ __device__ __forceinline__ void tile_rounds(TileLists<CAP> &L, const BinBuffers 
     }
     int tot;
     const int pos = wg_compact(ov, L.cnt, tot);
-    if (ov) {
-      L.f[cnt + pos] = f;
-      L.span[cnt + pos] = sp;
-    }
-    cnt += tot;
-    if (cnt > CAP - kBlock || base + kBlock >= n) {
+    // a batch holds at most kCap faces: flush first if this chunk would overflow it
+    if (cnt + tot > kCap) {
       __syncthreads();
       for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
       int nsub = 0;
@@ -87,7 +125,7 @@ __device__ __forceinline__ void tile_rounds(TileLists<CAP> &L, const BinBuffers 
         const bool ok =
             t.wave_live && k < cnt && span_overlaps(L.span[k], t.WX0, t.WX1, t.WY0, t.WY1);
         const uint64_t m = __ballot(ok);
-        if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned short)k;
+        if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
         nsub += __popcll(m);
       }
       __syncthreads();
@@ -95,6 +133,27 @@ __device__ __forceinline__ void tile_rounds(TileLists<CAP> &L, const BinBuffers 
       __syncthreads();
       cnt = 0;
     }
+    if (ov) {
+      L.f[cnt + pos] = f;
+      L.span[cnt + pos] = sp;
+    }
+    cnt += tot;
+  }
+  if (cnt > 0) {
+    __syncthreads();
+    for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
+    int nsub = 0;
+    for (int k0 = 0; k0 < cnt; k0 += kWave) {
+      const int k = k0 + lane;
+      const bool ok =
+          t.wave_live && k < cnt && span_overlaps(L.span[k], t.WX0, t.WX1, t.WY0, t.WY1);
+      const uint64_t m = __ballot(ok);
+      if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
+      nsub += __popcll(m);
+    }
+    __syncthreads();
+    round(nsub, cnt);
+    __syncthreads();
   }
 }
 
@@ -104,6 +163,30 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Exclusive prefix sum over the 256 threads of the workgroup; total returned in `total`.
+// scratch: 4 ints of LDS.
+__device__ __forceinline__ int wg_exclusive_scan(int v, int *scratch, int &total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == kWave - 1) scratch[w] = x;
+  __syncthreads();
+  int off = 0, tot = 0;
+#pragma unroll
+  for (int k = 0; k < kBlock / kWave; ++k) {
+    const int c = scratch[k];
+    off += (k < w) ? c : 0;
+    tot += c;
+  }
+  __syncthreads();
+  total = tot;
+  return off + x - v;
 }
 
 }  // namespace kd

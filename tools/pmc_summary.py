@@ -1,0 +1,34 @@
+"""Summarise rocprofv3 --pmc CSVs (tools/pmc_run.sh) per kernel: mean counter value per dispatch.
+HBM bytes per launch follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE are in KiB; on
+gfx950 FETCH_SIZE reads 1/2 of a wide (16 B/lane) streaming read -- both the raw and the x2
+corrected read side are reported (our kernels mix access widths)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+out = sys.argv[1] if len(sys.argv) > 1 else 'gpurun_out/pmc'
+vals = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(os.path.join(out, 'p*', '**', '*counter_collection.csv'), recursive=True):
+    for r in csv.DictReader(open(f)):
+        name = r.get('Kernel_Name') or r.get('Kernel-Name') or ''
+        short = name.split('(')[0].replace('void ', '').strip()
+        cn = r.get('Counter_Name') or r.get('Counter-Name')
+        v = float(r.get('Counter_Value') or r.get('Counter-Value') or 0)
+        vals[short][cn].append(v)
+res = {}
+for k, d in vals.items():
+    if not k.startswith('kd::'):
+        continue
+    res[k] = {cn: sum(v) / len(v) for cn, v in d.items()}
+    m = res[k]
+    if 'FETCH_SIZE' in m and 'WRITE_SIZE' in m:
+        m['hbm_bytes_raw'] = (m['FETCH_SIZE'] + m['WRITE_SIZE']) * 1024
+        m['hbm_bytes_fetch_x2'] = (2 * m['FETCH_SIZE'] + m['WRITE_SIZE']) * 1024
+for k, m in sorted(res.items()):
+    print(k)
+    for cn, v in sorted(m.items()):
+        print(f'   {cn:24s} {v:16.1f}')
+json.dump(res, open(os.path.join(out, 'summary.json'), 'w'), indent=1)
