@@ -55,6 +55,9 @@ void kd_profile_enable(int on);
 int kd_profile_collect(double *total_ms, int64_t *launches, int n);
 const char *kd_profile_kernel_name(int id);
 
+/* Diagnostics only: ablation switches read by the kernels (0 = production). */
+int kd_debug_set(int flags);
+
 /* ---------------------------------------------------------------------------------------------
  * Packed rasterize forward.  Replaces _C.render.mesh.packed_rasterize_forward_cuda
  * (reference kaolin/csrc/bindings.cpp:77 -> kaolin/csrc/render/mesh/rasterization.cpp:49-104,

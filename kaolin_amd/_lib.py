@@ -67,6 +67,8 @@ def load():
             lib.kd_profile_collect.restype = c_int
             lib.kd_profile_kernel_name.argtypes = [c_int]
             lib.kd_profile_kernel_name.restype = ctypes.c_char_p
+            lib.kd_debug_set.argtypes = [c_int]
+            lib.kd_debug_set.restype = c_int
             for base, sig in _SIGS.items():
                 for sfx in ('f32', 'f64'):
                     fn = getattr(lib, f'{base}_{sfx}')

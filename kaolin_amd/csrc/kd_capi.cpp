@@ -13,6 +13,9 @@ char *error_buffer() {
   return buf;
 }
 
+std::atomic<int> g_debug{0};
+int debug_flags() { return g_debug.load(); }
+
 namespace {
 std::atomic<bool> g_prof{false};
 std::mutex g_prof_mu;
@@ -61,6 +64,11 @@ const char *kd_last_error(void) { return kd::error_buffer(); }
 int kd_version(void) { return 1; }
 
 void kd_profile_enable(int on) { kd::g_prof.store(on != 0); }
+
+int kd_debug_set(int flags) {
+  kd::g_debug.store(flags);
+  return KD_OK;
+}
 
 int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
   std::vector<kd::Rec> recs;

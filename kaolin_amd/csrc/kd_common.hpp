@@ -14,6 +14,12 @@
 
 namespace kd {
 
+// Diagnostic ablation switches (kd_debug_set, copied into FaceSet::dbg); 0 in production.
+// Bits: 1 skip the per-pixel face tests of the forward kernels, 2 skip staging face data,
+//       4 skip the per-batch work entirely (bin walk only), 8 fp32 raster: lane-per-pixel
+//       kernel instead of the pair pipeline.
+int debug_flags();
+
 constexpr int kWave = 64;
 constexpr int kBlock = 256;      // 4 waves
 constexpr int kTile = 16;        // fine tile: 16x16 pixels per workgroup, 8x8 per wave
@@ -158,6 +164,7 @@ struct FaceSet {
   int has_margin;
   const uint8_t *valid;      // (N) uint8 or nullptr
   float M;                   // float multiplier of the pixel centres
+  int dbg;                   // diagnostic ablation flags (0 in production)
 };
 
 template <typename T>

@@ -20,6 +20,8 @@
 #include "kd_capi.hpp"
 #include "kd_tile.hpp"
 
+#include <type_traits>
+
 namespace kd {
 
 template <typename T>
@@ -33,6 +35,15 @@ struct RasterFwdArgs {
   T *interp;
   int64_t *face_idx;
   T *weights;
+};
+
+template <typename T>
+struct ScaleUp {  // 2^(-min normal exponent): |w| * value >= |norm| => |w / norm| >= min normal
+  static constexpr T value = 0x1p126f;
+};
+template <>
+struct ScaleUp<double> {
+  static constexpr double value = 0x1p1022;
 };
 
 // The reference per-face test (rasterization_cuda.cu:131-159) for one pixel whose centre passed
@@ -50,6 +61,18 @@ __device__ __forceinline__ bool raster_face_test(T x0, T y0, T ax, T ay, T bx, T
   w2 = a_edge_x * b_edge_y - a_edge_y * b_edge_x;
   T norm = w0 + w1 + w2;
   norm = (T)((double)norm + copysign((double)eps, (double)norm));
+  // Exact early rejection: with a finite nonzero norm, a nonzero non-NaN w of the opposite sign
+  // whose quotient cannot round to -0 (|w| >= |norm| * 2^-(min normal exponent)) makes the
+  // reference's `w / norm < 0` true.  Anything else takes the reference path below.
+  if (isfinite(norm) && norm != (T)0) {
+    const bool nneg = norm < (T)0;
+    const T big = ScaleUp<T>::value;
+    const T an = fabs(norm);
+    if (((w0 < (T)0) != nneg && w0 != (T)0 && !isnan(w0) && fabs(w0) * big >= an) ||
+        ((w1 < (T)0) != nneg && w1 != (T)0 && !isnan(w1) && fabs(w1) * big >= an) ||
+        ((w2 < (T)0) != nneg && w2 != (T)0 && !isnan(w2) && fabs(w2) * big >= an))
+      return false;
+  }
   w0 /= norm;
   w1 /= norm;
   w2 /= norm;
@@ -87,7 +110,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
     s_geo[8][k] = zz[2];
   };
   auto round = [&](int nsub, int) {
-    if (nsub == 0) return;
+    if (nsub == 0 || (fs.dbg & 1)) return;
     const SubSpans ss = load_subspans(L, nsub);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -113,7 +136,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
       }
     }
   };
-  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round);
+  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
 
   if (!t.inimg) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
@@ -132,6 +155,229 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
     wo[1] = 0.;
     wo[2] = 0.;
     for (int d = 0; d < a.D; ++d) io[d] = 0.;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// fp32 forward as a (pixel, face) pair pipeline.  The lane-per-pixel loop above runs every face
+// of the wave's sub-list on every lane although a pixel's centre is in only ~1/3 of those boxes;
+// here the heavy test runs once per (pixel, face-whose-box-holds-it) pair with every lane busy:
+//   A  lane = face: its box's pixels inside the 8x8 sub-tile as a 64-bit mask (exact spans);
+//      one ballot per pixel appends that pixel's candidate faces to a per-wave pair list;
+//   B1 lane = pair: edge functions + eps-norm + the exact early sign rejection; survivors are
+//      compacted (on this workload ~10-20 % of the pairs);
+//   B2 lane = survivor: the reference's divisions, inside test and depth; an inside face posts
+//      key = (order-preserving bits of z, ~face index) with a 64-bit LDS atomicMax per pixel.
+//   The winner is the face with the largest z and, among equal z, the lowest index -- exactly
+//   what the reference's ascending scan with strict `z > best` keeps (rasterization_cuda.cu:162),
+//   provided no depth is NaN (-0 is folded to +0 first; -inf never wins there); a pixel that
+//   meets a NaN depth replays the reference's sequential loop over its coarse bin instead.
+//   The winner's weights are recomputed with the identical expression for the outputs.
+// ------------------------------------------------------------------------------------------
+constexpr int kRasterPairCap = 512;
+
+__device__ __forceinline__ uint32_t ordered_f32(float z) {
+  const uint32_t u = __float_as_uint(z + 0.0f);  // -0 -> +0
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// 64-bit mask of the 8x8 sub-tile pixels (bit = row*8 + col) inside an exact span.
+__device__ __forceinline__ uint64_t span_tile_mask(PSpan p, int WX0, int WY0) {
+  int x0 = (int)(int16_t)(p.lo & 0xffff) - WX0, x1 = (int)(int16_t)(p.lo >> 16) - WX0;
+  int y0 = (int)(int16_t)(p.hi & 0xffff) - WY0, y1 = (int)(int16_t)(p.hi >> 16) - WY0;
+  x0 = max(x0, 0);
+  y0 = max(y0, 0);
+  x1 = min(x1, 7);
+  y1 = min(y1, 7);
+  if (x0 > x1 || y0 > y1) return 0ull;
+  const uint32_t cols = ((2u << x1) - 1u) & ~((1u << x0) - 1u);  // bits x0..x1
+  const uint64_t rows = ((y1 == 7) ? ~0ull : ((1ull << (8 * (y1 + 1))) - 1ull)) &
+                        ~((1ull << (8 * y0)) - 1ull);
+  return ((uint64_t)cols * 0x0101010101010101ull) & rows;
+}
+
+struct RasterTestF {
+  float w0, w1, w2, norm;
+};
+
+__global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<float> a) {
+  __shared__ TileLists L;
+  __shared__ float s_geo[9][kCap];  // ax ay bx by cx cy (scaled), az bz cz
+  __shared__ unsigned short s_pair[4][kRasterPairCap];  // (q << 8) | k
+  __shared__ unsigned short s_surv[4][kRasterPairCap];
+  __shared__ unsigned long long s_key[4][64];
+  __shared__ unsigned long long s_nan[4];
+
+  const FaceSet<float> &fs = a.fs;
+  const int H = fs.H, W = fs.W;
+  const float M = fs.M;
+  const int b = blockIdx.y;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int64_t lo, hi;
+  view_range(fs, b, lo, hi);
+  const TileGeom t = tile_geom(H, W);
+  const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
+  s_key[w][lane] = 0ull;
+  if (lane == 0) s_nan[w] = 0ull;
+
+  auto stage = [&](int k, int64_t fi) {
+    float v[6];
+    load_corners(fs, fi, v);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
+    const float *zz = a.fvz + fi * 3;
+    s_geo[6][k] = zz[0];
+    s_geo[7][k] = zz[1];
+    s_geo[8][k] = zz[2];
+  };
+  // edge functions + eps-normalisation (rasterization_cuda.cu:131-142) of pair (q, k)
+  auto edges = [&](int q, int k, RasterTestF &r) {
+    const float x0 = sx * (float)(2 * (t.WX0 + (q & 7)) + 1 - W);
+    const float y0 = sy * (float)(H - 2 * (t.WY0 + (q >> 3)) - 1);
+    const float a_edge_x = s_geo[0][k] - x0, a_edge_y = s_geo[1][k] - y0;
+    const float b_edge_x = s_geo[2][k] - x0, b_edge_y = s_geo[3][k] - y0;
+    const float c_edge_x = s_geo[4][k] - x0, c_edge_y = s_geo[5][k] - y0;
+    r.w0 = b_edge_x * c_edge_y - b_edge_y * c_edge_x;
+    r.w1 = c_edge_x * a_edge_y - c_edge_y * a_edge_x;
+    r.w2 = a_edge_x * b_edge_y - a_edge_y * b_edge_x;
+    const float norm = r.w0 + r.w1 + r.w2;
+    r.norm = (float)((double)norm + copysign((double)a.eps, (double)norm));
+  };
+  // B1 + B2 over the current pair batch
+  auto test_batch = [&](int total) {
+    wave_lds_sync();
+    int nsurv = 0;
+    for (int e0 = 0; e0 < total; e0 += kWave) {
+      const int e = e0 + lane;
+      bool keep = false;
+      if (e < total) {
+        const int pr = s_pair[w][e];
+        RasterTestF r;
+        edges(pr >> 8, pr & 255, r);
+        keep = true;
+        if (isfinite(r.norm) && r.norm != 0.f) {
+          const bool nneg = r.norm < 0.f;
+          const float an = fabsf(r.norm);
+          if (((r.w0 < 0.f) != nneg && r.w0 != 0.f && !isnan(r.w0) &&
+               fabsf(r.w0) * 0x1p126f >= an) ||
+              ((r.w1 < 0.f) != nneg && r.w1 != 0.f && !isnan(r.w1) &&
+               fabsf(r.w1) * 0x1p126f >= an) ||
+              ((r.w2 < 0.f) != nneg && r.w2 != 0.f && !isnan(r.w2) &&
+               fabsf(r.w2) * 0x1p126f >= an))
+            keep = false;
+        }
+      }
+      const uint64_t km = __ballot(keep);
+      if (keep) s_surv[w][nsurv + mbcnt(km)] = (unsigned short)e;
+      nsurv += __popcll(km);
+    }
+    wave_lds_sync();
+    for (int e0 = 0; e0 < nsurv; e0 += kWave) {
+      const int e = e0 + lane;
+      if (e < nsurv) {
+        const int pr = s_pair[w][s_surv[w][e]];
+        const int q = pr >> 8, k = pr & 255;
+        RasterTestF r;
+        edges(q, k, r);
+        const float w0 = r.w0 / r.norm, w1 = r.w1 / r.norm, w2 = r.w2 / r.norm;
+        if (!(w0 < 0.f || w1 < 0.f || w2 < 0.f)) {
+          const float z0 = w0 * s_geo[6][k] + w1 * s_geo[7][k] + w2 * s_geo[8][k];
+          if (isnan(z0)) {
+            atomicOr(&s_nan[w], 1ull << q);
+          } else if (z0 != -INFINITY) {
+            const unsigned long long key =
+                ((unsigned long long)ordered_f32(z0) << 32) |
+                (unsigned long long)(0xffffffffu - (uint32_t)L.f[k]);
+            atomicMax(&s_key[w][q], key);
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+  };
+  auto round = [&](int nsub, int) {
+    if (nsub == 0 || (fs.dbg & 1)) return;
+    const SubSpans ss = load_subspans(L, nsub);
+    int total = 0;
+#pragma unroll 1
+    for (int c = 0; c < 4; ++c) {
+      if (c * kWave >= nsub) break;
+      const PSpan sp = c == 0 ? ss.s[0] : c == 1 ? ss.s[1] : c == 2 ? ss.s[2] : ss.s[3];
+      const int kc = c == 0 ? ss.k[0] : c == 1 ? ss.k[1] : c == 2 ? ss.k[2] : ss.k[3];
+      const uint64_t fm = span_tile_mask(sp, t.WX0, t.WY0);
+      // A: pixel-major emission, lane = face: one ballot per pixel of the sub-tile
+      for (uint64_t any = __ballot(fm != 0ull) ? ~0ull : 0ull; any; any = 0ull) {
+        for (int q = 0; q < 64; ++q) {
+          const bool hit = (fm >> q) & 1ull;
+          const uint64_t hm = __ballot(hit);
+          if (!hm) continue;
+          const int nh = __popcll(hm);
+          if (total + nh > kRasterPairCap) {
+            test_batch(total);
+            total = 0;
+          }
+          if (hit) s_pair[w][total + mbcnt(hm)] = (unsigned short)((q << 8) | kc);
+          total += nh;
+        }
+      }
+    }
+    if (total) test_batch(total);
+  };
+  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
+
+  if (!t.inimg) return;
+  const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
+  const float x0 = px_cx(M, W, t.px), y0 = px_cy(M, H, t.py);
+  int best = -1;
+  float bw0 = 0.f, bw1 = 0.f, bw2 = 0.f;
+  if ((s_nan[w] >> lane) & 1ull) {
+    // the reference's sequential loop over this pixel's coarse bin (ascending faces)
+    const BinGeom &g = a.bb.g;
+    const int ct = (t.py / g.ct) * g.nctx + (t.px / g.ct);
+    const int n = a.bb.totals[(int64_t)b * g.nct() + ct];
+    const int *bin = a.bb.bins + (int64_t)ct * fs.N + lo;
+    float max_z0 = -INFINITY;
+    for (int e = 0; e < n; ++e) {
+      const int f = bin[e];
+      if (!pspan_has(pack_span(a.bb.spans[lo + f]), t.px, t.py)) continue;
+      float v[6];
+      load_corners(fs, lo + f, v);
+      const float *zz = a.fvz + (lo + f) * 3;
+      float w0, w1, w2, z0;
+      if (!raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[1],
+                                   zz[2], a.eps, w0, w1, w2, z0))
+        continue;
+      if (z0 <= max_z0) continue;
+      max_z0 = z0;
+      best = f;
+      bw0 = w0;
+      bw1 = w1;
+      bw2 = w2;
+    }
+  } else if (s_key[w][lane] != 0ull) {
+    best = (int)(0xffffffffu - (uint32_t)(s_key[w][lane] & 0xffffffffull));
+    float v[6];
+    load_corners(fs, lo + best, v);
+    const float *zz = a.fvz + (lo + best) * 3;
+    float z0;
+    raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[1], zz[2],
+                            a.eps, bw0, bw1, bw2, z0);
+  }
+  a.face_idx[p] = best;
+  float *wo = a.weights + p * 3;
+  float *io = a.interp + p * a.D;
+  if (best >= 0) {
+    wo[0] = bw0;
+    wo[1] = bw1;
+    wo[2] = bw2;
+    const float *r = a.feat + (lo + best) * 3 * a.D;
+    for (int d = 0; d < a.D; ++d)
+      io[d] = bw0 * r[d] + bw1 * r[a.D + d] + bw2 * r[2 * a.D + d];
+  } else {
+    wo[0] = 0.f;
+    wo[1] = 0.f;
+    wo[2] = 0.f;
+    for (int d = 0; d < a.D; ++d) io[d] = 0.f;
   }
 }
 
@@ -352,10 +598,18 @@ int raster_forward(const FaceSet<T> &fs, int64_t max_per_view, const T *fvz, con
   hipError_t e = bin_faces<T>(fs, bb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> a{fs, bb, fvz, feat, D, eps, interp, face_idx, weights};
+  a.fs.dbg = debug_flags();
   const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
   {
     ProfScope prof(K_RASTER_FWD, stream);
-    hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+    if constexpr (std::is_same<T, float>::value) {
+      if (!(a.fs.dbg & 8))
+        hipLaunchKernelGGL(kd_raster_fwd_pairs, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+      else
+        hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+    } else {
+      hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+    }
   }
   e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster fwd: %s", hipGetErrorString(e));

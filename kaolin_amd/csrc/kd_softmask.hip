@@ -254,12 +254,12 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
       wave_lds_sync();
     };
     auto round = [&](int nsub, int) {
-      if (!umask || nsub == 0) return;
+      if (!umask || nsub == 0 || (fs.dbg & 1)) return;
       any_sub = true;
       const SubSpans ss = load_subspans(L, nsub);
       soft_pass_a(ss, nsub, P, umask, K, t, my_kid, flush);
     };
-    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round);
+    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
   }
 
   if (!t.wave_live) return;
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_tile(SoftArgs<T> a) {
       if (v != (T)0) atomicAdd(a.grad_fvi + (lo + L.f[k]) * 6 + c, v);
     }
   };
-  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round);
+  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
 }
 
 template <typename T>
@@ -410,6 +410,7 @@ int soft_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool build_bins,
   if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
   size_t off = 0;
   a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
+  a.fs.dbg = debug_flags();
   if (build_bins) {
     hipError_t e = bin_faces<T>(fs, a.bb, stream);
     if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));

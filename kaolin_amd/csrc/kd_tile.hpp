@@ -96,7 +96,7 @@ __device__ __forceinline__ SubSpans load_subspans(const TileLists &L, int nsub) 
 template <typename Stage, typename Round>
 __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, int64_t N, int b,
                                             int64_t lo, const TileGeom &t, Stage stage,
-                                            Round round) {
+                                            Round round, int dbg = 0) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 / g.ct) * g.nctx + (t.X0 / g.ct);
@@ -118,7 +118,8 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
     // a batch holds at most kCap faces: flush first if this chunk would overflow it
     if (cnt + tot > kCap) {
       __syncthreads();
-      for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
+      if (!(dbg & 2))
+        for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
       int nsub = 0;
       for (int k0 = 0; k0 < cnt; k0 += kWave) {
         const int k = k0 + lane;
@@ -129,7 +130,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
         nsub += __popcll(m);
       }
       __syncthreads();
-      round(nsub, cnt);
+      if (!(dbg & 4)) round(nsub, cnt);
       __syncthreads();
       cnt = 0;
     }
@@ -141,7 +142,8 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
   }
   if (cnt > 0) {
     __syncthreads();
-    for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
+    if (!(dbg & 2))
+      for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
     int nsub = 0;
     for (int k0 = 0; k0 < cnt; k0 += kWave) {
       const int k = k0 + lane;
@@ -152,7 +154,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
       nsub += __popcll(m);
     }
     __syncthreads();
-    round(nsub, cnt);
+    if (!(dbg & 4)) round(nsub, cnt);
     __syncthreads();
   }
 }
