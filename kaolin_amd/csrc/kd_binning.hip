@@ -3,6 +3,8 @@
 
 #include "kd_capi.hpp"
 
+#include <type_traits>
+
 namespace kd {
 
 size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view) {
@@ -13,6 +15,7 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view)
   s += align_up(sizeof(int) * (size_t)B * (size_t)(nchunk > 0 ? nchunk : 1) * g.nct());
   s += align_up(sizeof(int) * (size_t)B * g.nct());
   s += align_up(sizeof(int) * (size_t)g.nct() * (size_t)(N > 0 ? N : 1));
+  s += align_up(sizeof(float4) * 2 * (size_t)N);
   return s;
 }
 
@@ -30,7 +33,77 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   off += align_up(sizeof(int) * (size_t)B * bb.g.nct());
   bb.bins = (int *)(base + off);
   off += align_up(sizeof(int) * (size_t)bb.g.nct() * (size_t)(N > 0 ? N : 1));
+  bb.cull = (float4 *)(base + off);
+  off += align_up(sizeof(float4) * 2 * (size_t)N);
+  bb.cull_eps = 0.f;
   return bb;
+}
+
+// Edge-culling coefficients of one face for the fp32 pair raster (kd_raster.hip).
+//
+// With the reference's fp32 centres x0, y0 and the scaled corners, w0 is computed as
+// fl(fl(bex*cey) - fl(bey*cex)) over rounded edges; its exact counterpart is affine,
+//   W0 = A0 + B0 x0 + C0 y0,  A0 = bx cy - by cx,  B0 = by - cy,  C0 = cx - bx  (cyclic for 1, 2),
+// and |w_i - W_i| <= tau = 2^-20 E^2 with E = max|corner| + |M| (4.02u(|P1|+|P2|) <= 8.04u E^2,
+// u = 2^-24).  The three W_i sum to N = A0 + A1 + A2 (twice the signed area) at every pixel;
+// when |N| > 6 tau the computed eps-normalised norm has the sign s of N, so a pixel with
+// s W_i < -2 tau for some i has w_i / norm < 0 and is rejected by the reference
+// (rasterization_cuda.cu:145; |w_i| > tau and |eps| <= E^2 keep the quotient finite and away
+// from -0) -- culling it cannot change the result.  Keep iff s W_i >= -2 tau
+// is, for s B_i > 0 (< 0), x0 >= (<=) X*(y0); in tile-local pixel units
+// in pixel units relative to the face's own span (column span.x0, row span.y0),
+//   p*(y0) = P0 + P1 (y0 - y0ref),  y0ref = centre of row span.y0,
+// and the raster keeps columns >= ceil(max_lo - 1/64) and <= floor(min_hi + 1/64).  The 1/64 px
+// slack covers the fp32 evaluation there (|P0| <= 2^14, |P1 d| <= 2^13 over the span's rows,
+// a handful of roundings of at most 2^-10 each), the centre rounding (u W / 2 <= 2^-10 for
+// W <= 2^15) and the double-precision coefficients (terms bounded by 2^40 px: < 2^-12).  Edges outside these bounds, degenerate
+// or non-finite faces and non-positive pixel steps cull nothing (slots stay -inf / +inf).
+// out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}
+__device__ void raster_cull_coefs(const float v[6], float M, int H, int W, Span sp, float eps,
+                                  float out[8]) {
+  out[0] = out[2] = -INFINITY;
+  out[4] = out[6] = INFINITY;
+  out[1] = out[3] = out[5] = out[7] = 0.f;
+  const double ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
+  const double vm = fmax(fmax(fmax(fabs(ax), fabs(ay)), fmax(fabs(bx), fabs(by))),
+                         fmax(fabs(cx), fabs(cy)));
+  const float sxf = M / (float)W, syf = M / (float)H;
+  if (!(vm < 0x1p59) || !(sxf > 0.f) || !(syf > 0.f) || W > 32768 || H > 32768) return;
+  const double E = vm + 1.001 * fabs((double)M);
+  const double tau = 0x1p-20 * E * E;
+  const double A[3] = {bx * cy - by * cx, cx * ay - cy * ax, ax * by - ay * bx};
+  const double Bc[3] = {by - cy, cy - ay, ay - by};
+  const double Cc[3] = {cx - bx, ax - cx, bx - ax};
+  const double N = A[0] + A[1] + A[2];
+  if (!(fabs(N) > 6.0 * tau) || !(fabs((double)eps) <= E * E)) return;
+  const double s = N > 0.0 ? 1.0 : -1.0;
+  const double sx = sxf, sy = syf;
+  const double y0ref = (double)px_cy(M, H, sp.y0);
+  const double drows = 2.0 * sy * (double)(sp.y1 - sp.y0 + 1);  // >= |y0 - y0ref| on the span
+  bool has_lo = false, has_hi = false;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double sB = s * Bc[i];
+    if (sB == 0.0) continue;
+    const double inv = 1.0 / (2.0 * sB * sx);
+    const double P1 = -s * Cc[i] * inv;
+    const double t = -2.0 * tau - s * (A[i] + Cc[i] * y0ref);
+    if (!(fabs(P1) * drows <= 0x1p13) ||
+        !((fabs(A[i]) + fabs(Cc[i] * y0ref) + 2.0 * tau) * fabs(inv) <= 0x1p40))
+      continue;
+    double P0 = t * inv + 0.5 * (double)(W - 1) - (double)sp.x0;
+    P0 = fmin(fmax(P0, -0x1p14), 0x1p14);
+    // the exact signs of the B_i cannot all agree (B0 + B1 + B2 = 0): at most two per side
+    if (sB > 0.0) {
+      out[has_lo ? 2 : 0] = (float)P0;
+      out[has_lo ? 3 : 1] = (float)P1;
+      has_lo = true;
+    } else {
+      out[has_hi ? 6 : 4] = (float)P0;
+      out[has_hi ? 7 : 5] = (float)P1;
+      has_hi = true;
+    }
+  }
 }
 
 template <typename T>
@@ -51,6 +124,14 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(FaceSet<T> fs, BinBuffers
       load_corners(fs, i, v);
       face_box(fs, i, v, box);
       s = make_span<T>(box[0], box[1], box[2], box[3], fs.M, fs.H, fs.W);
+      if constexpr (std::is_same<T, float>::value) {
+        if (bb.cull && !span_empty(s)) {
+          float cc[8];
+          raster_cull_coefs(v, fs.M, fs.H, fs.W, s, bb.cull_eps, cc);
+          bb.cull[2 * i] = make_float4(cc[0], cc[1], cc[2], cc[3]);
+          bb.cull[2 * i + 1] = make_float4(cc[4], cc[5], cc[6], cc[7]);
+        }
+      }
     } else {
       s.x0 = 1;
       s.x1 = 0;

@@ -17,6 +17,8 @@
 //   totals [B][nct]      int32
 //   bins   [nct][N]      int32 local face index; the (b, c) bin starts at c*N + first[b] and has
 //                        room for the view's whole face count.
+//   cull   [N][2]        float4: fp32 raster edge-culling coefficients (raster_cull_coefs), only
+//                        written when BinBuffers::cull is set (fp32 rasterization).
 #pragma once
 
 #include "kd_common.hpp"
@@ -28,9 +30,16 @@ struct BinBuffers {
   int *counts;
   int *totals;
   int *bins;
+  float4 *cull;    // nullptr: not computed
+  float cull_eps;  // the raster eps (cull coefficients only)
   int nchunk;
   BinGeom g;
 };
+
+// Edge-culling coefficients of one face in its own frame (column span.x0, row span.y0); see
+// kd_binning.hip.  out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}.
+__device__ void raster_cull_coefs(const float v[6], float M, int H, int W, Span sp, float eps,
+                                  float out[8]);
 
 size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view);
 // Carves the buffers from `ws` starting at *offset (advanced past them).

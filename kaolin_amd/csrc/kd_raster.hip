@@ -48,8 +48,8 @@ struct ScaleUp<double> {
 
 // The reference per-face test (rasterization_cuda.cu:131-159) for one pixel whose centre passed
 // the box test: edge functions, eps-normalised barycentrics (division before the sign test,
-// exactly as the reference), depth.
-template <typename T>
+// exactly as the reference), depth.  EarlyReject adds an exact shortcut for pixels outside.
+template <typename T, bool EarlyReject = true>
 __device__ __forceinline__ bool raster_face_test(T x0, T y0, T ax, T ay, T bx, T by, T cx, T cy,
                                                  T az, T bz, T cz, float eps, T &w0, T &w1,
                                                  T &w2, T &z0) {
@@ -64,7 +64,7 @@ __device__ __forceinline__ bool raster_face_test(T x0, T y0, T ax, T ay, T bx, T
   // Exact early rejection: with a finite nonzero norm, a nonzero non-NaN w of the opposite sign
   // whose quotient cannot round to -0 (|w| >= |norm| * 2^-(min normal exponent)) makes the
   // reference's `w / norm < 0` true.  Anything else takes the reference path below.
-  if (isfinite(norm) && norm != (T)0) {
+  if (EarlyReject && isfinite(norm) && norm != (T)0) {
     const bool nneg = norm < (T)0;
     const T big = ScaleUp<T>::value;
     const T an = fabs(norm);
@@ -160,14 +160,18 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
 
 // ------------------------------------------------------------------------------------------
 // fp32 forward as a (pixel, face) pair pipeline.  The lane-per-pixel loop above runs every face
-// of the wave's sub-list on every lane although a pixel's centre is in only ~1/3 of those boxes;
-// here the heavy test runs once per (pixel, face-whose-box-holds-it) pair with every lane busy:
-//   A  lane = face: its box's pixels inside the 8x8 sub-tile as a 64-bit mask (exact spans);
-//      one ballot per pixel appends that pixel's candidate faces to a per-wave pair list;
-//   B1 lane = pair: edge functions + eps-norm + the exact early sign rejection; survivors are
-//      compacted (on this workload ~10-20 % of the pairs);
-//   B2 lane = survivor: the reference's divisions, inside test and depth; an inside face posts
-//      key = (order-preserving bits of z, ~face index) with a 64-bit LDS atomicMax per pixel.
+// of the wave's sub-list on every lane, although a pixel centre is inside only ~1/5 of the boxes
+// that hold it on this workload; here the full test runs once per (pixel, candidate face) pair
+// with every lane busy, and the candidates are culled per pixel row by the triangle's edges:
+//   stage  lane = face (once per tile): the keep-interval of every edge as an affine function of
+//          the row, in tile-local pixel units, with a rigorous error margin (raster_cull_coefs);
+//   A  lane = face: per row of the 8x8 sub-tile, [ceil(max lo - d), floor(min hi + d)] clipped
+//      to the exact box span -> a 64-bit pixel mask; a 64x64 bit transpose across the wave gives
+//      each pixel lane its candidate mask over the chunk; a DPP scan places the (pixel, face)
+//      pairs in a per-wave list;
+//   B  lane = pair: the reference's edge functions, eps-norm, divisions, inside test and depth;
+//      an inside face posts key = (order-preserving bits of z, ~face index) with a 64-bit LDS
+//      atomicMax per pixel.
 //   The winner is the face with the largest z and, among equal z, the lowest index -- exactly
 //   what the reference's ascending scan with strict `z > best` keeps (rasterization_cuda.cu:162),
 //   provided no depth is NaN (-0 is folded to +0 first; -inf never wins there); a pixel that
@@ -181,30 +185,29 @@ __device__ __forceinline__ uint32_t ordered_f32(float z) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// 64-bit mask of the 8x8 sub-tile pixels (bit = row*8 + col) inside an exact span.
-__device__ __forceinline__ uint64_t span_tile_mask(PSpan p, int WX0, int WY0) {
-  int x0 = (int)(int16_t)(p.lo & 0xffff) - WX0, x1 = (int)(int16_t)(p.lo >> 16) - WX0;
-  int y0 = (int)(int16_t)(p.hi & 0xffff) - WY0, y1 = (int)(int16_t)(p.hi >> 16) - WY0;
-  x0 = max(x0, 0);
-  y0 = max(y0, 0);
-  x1 = min(x1, 7);
-  y1 = min(y1, 7);
-  if (x0 > x1 || y0 > y1) return 0ull;
-  const uint32_t cols = ((2u << x1) - 1u) & ~((1u << x0) - 1u);  // bits x0..x1
-  const uint64_t rows = ((y1 == 7) ? ~0ull : ((1ull << (8 * (y1 + 1))) - 1ull)) &
-                        ~((1ull << (8 * y0)) - 1ull);
-  return ((uint64_t)cols * 0x0101010101010101ull) & rows;
+// 64x64 bit-matrix transpose across a wave: lane l bit j -> lane j bit l (block swaps).
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t masks[6] = {0x00000000ffffffffull, 0x0000ffff0000ffffull,
+                             0x00ff00ff00ff00ffull, 0x0f0f0f0f0f0f0f0full,
+                             0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const int sh = 32 >> st;
+    const uint64_t mlo = masks[st];
+    const uint32_t ylo = (uint32_t)__shfl_xor((int)(uint32_t)x, sh);
+    const uint32_t yhi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), sh);
+    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+    x = (lane & sh) ? ((x & ~mlo) | ((y & ~mlo) >> sh)) : ((x & mlo) | ((y & mlo) << sh));
+  }
+  return x;
 }
-
-struct RasterTestF {
-  float w0, w1, w2, norm;
-};
 
 __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<float> a) {
   __shared__ TileLists L;
-  __shared__ float s_geo[9][kCap];  // ax ay bx by cx cy (scaled), az bz cz
-  __shared__ unsigned short s_pair[4][kRasterPairCap];  // (q << 8) | k
-  __shared__ unsigned short s_surv[4][kRasterPairCap];
+  __shared__ float s_geo[9][kCap];   // ax ay bx by cx cy (scaled), az bz cz
+  __shared__ float4 s_cull[2][kCap];  // raster_cull_coefs (kd_binning), face frame
+  __shared__ unsigned short s_pair[4][kRasterPairCap];  // (q << 8) | sub-list entry
   __shared__ unsigned long long s_key[4][64];
   __shared__ unsigned long long s_nan[4];
 
@@ -219,6 +222,12 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
   s_key[w][lane] = 0ull;
   if (lane == 0) s_nan[w] = 0ull;
+  // this wave's row centres relative to its first row
+  const float ysub = px_cy(M, H, t.WY0);
+  float drow[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) drow[r] = px_cy(M, H, t.WY0 + r) - ysub;
+  constexpr float kSlack = 1.f / 64.f;
 
   auto stage = [&](int k, int64_t fi) {
     float v[6];
@@ -229,59 +238,24 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
     s_geo[6][k] = zz[0];
     s_geo[7][k] = zz[1];
     s_geo[8][k] = zz[2];
+    s_cull[0][k] = a.bb.cull[2 * fi];
+    s_cull[1][k] = a.bb.cull[2 * fi + 1];
   };
-  // edge functions + eps-normalisation (rasterization_cuda.cu:131-142) of pair (q, k)
-  auto edges = [&](int q, int k, RasterTestF &r) {
-    const float x0 = sx * (float)(2 * (t.WX0 + (q & 7)) + 1 - W);
-    const float y0 = sy * (float)(H - 2 * (t.WY0 + (q >> 3)) - 1);
-    const float a_edge_x = s_geo[0][k] - x0, a_edge_y = s_geo[1][k] - y0;
-    const float b_edge_x = s_geo[2][k] - x0, b_edge_y = s_geo[3][k] - y0;
-    const float c_edge_x = s_geo[4][k] - x0, c_edge_y = s_geo[5][k] - y0;
-    r.w0 = b_edge_x * c_edge_y - b_edge_y * c_edge_x;
-    r.w1 = c_edge_x * a_edge_y - c_edge_y * a_edge_x;
-    r.w2 = a_edge_x * b_edge_y - a_edge_y * b_edge_x;
-    const float norm = r.w0 + r.w1 + r.w2;
-    r.norm = (float)((double)norm + copysign((double)a.eps, (double)norm));
-  };
-  // B1 + B2 over the current pair batch
+  // B: the reference's per-pixel test (rasterization_cuda.cu:131-162) over the current batch
   auto test_batch = [&](int total) {
+    if (fs.dbg & 16) return;
     wave_lds_sync();
-    int nsurv = 0;
     for (int e0 = 0; e0 < total; e0 += kWave) {
       const int e = e0 + lane;
-      bool keep = false;
       if (e < total) {
         const int pr = s_pair[w][e];
-        RasterTestF r;
-        edges(pr >> 8, pr & 255, r);
-        keep = true;
-        if (isfinite(r.norm) && r.norm != 0.f) {
-          const bool nneg = r.norm < 0.f;
-          const float an = fabsf(r.norm);
-          if (((r.w0 < 0.f) != nneg && r.w0 != 0.f && !isnan(r.w0) &&
-               fabsf(r.w0) * 0x1p126f >= an) ||
-              ((r.w1 < 0.f) != nneg && r.w1 != 0.f && !isnan(r.w1) &&
-               fabsf(r.w1) * 0x1p126f >= an) ||
-              ((r.w2 < 0.f) != nneg && r.w2 != 0.f && !isnan(r.w2) &&
-               fabsf(r.w2) * 0x1p126f >= an))
-            keep = false;
-        }
-      }
-      const uint64_t km = __ballot(keep);
-      if (keep) s_surv[w][nsurv + mbcnt(km)] = (unsigned short)e;
-      nsurv += __popcll(km);
-    }
-    wave_lds_sync();
-    for (int e0 = 0; e0 < nsurv; e0 += kWave) {
-      const int e = e0 + lane;
-      if (e < nsurv) {
-        const int pr = s_pair[w][s_surv[w][e]];
-        const int q = pr >> 8, k = pr & 255;
-        RasterTestF r;
-        edges(q, k, r);
-        const float w0 = r.w0 / r.norm, w1 = r.w1 / r.norm, w2 = r.w2 / r.norm;
-        if (!(w0 < 0.f || w1 < 0.f || w2 < 0.f)) {
-          const float z0 = w0 * s_geo[6][k] + w1 * s_geo[7][k] + w2 * s_geo[8][k];
+        const int q = pr >> 8, k = L.sub[w][pr & 255];
+        const float x0 = sx * (float)(2 * (t.WX0 + (q & 7)) + 1 - W);
+        const float y0 = sy * (float)(H - 2 * (t.WY0 + (q >> 3)) - 1);
+        float w0, w1, w2, z0;
+        if (raster_face_test<float, false>(x0, y0, s_geo[0][k], s_geo[1][k], s_geo[2][k],
+                                           s_geo[3][k], s_geo[4][k], s_geo[5][k], s_geo[6][k],
+                                           s_geo[7][k], s_geo[8][k], a.eps, w0, w1, w2, z0)) {
           if (isnan(z0)) {
             atomicOr(&s_nan[w], 1ull << q);
           } else if (z0 != -INFINITY) {
@@ -297,29 +271,53 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
   };
   auto round = [&](int nsub, int) {
     if (nsub == 0 || (fs.dbg & 1)) return;
-    const SubSpans ss = load_subspans(L, nsub);
     int total = 0;
 #pragma unroll 1
     for (int c = 0; c < 4; ++c) {
       if (c * kWave >= nsub) break;
-      const PSpan sp = c == 0 ? ss.s[0] : c == 1 ? ss.s[1] : c == 2 ? ss.s[2] : ss.s[3];
-      const int kc = c == 0 ? ss.k[0] : c == 1 ? ss.k[1] : c == 2 ? ss.k[2] : ss.k[3];
-      const uint64_t fm = span_tile_mask(sp, t.WX0, t.WY0);
-      // A: pixel-major emission, lane = face: one ballot per pixel of the sub-tile
-      for (uint64_t any = __ballot(fm != 0ull) ? ~0ull : 0ull; any; any = 0ull) {
-        for (int q = 0; q < 64; ++q) {
-          const bool hit = (fm >> q) & 1ull;
-          const uint64_t hm = __ballot(hit);
-          if (!hm) continue;
-          const int nh = __popcll(hm);
-          if (total + nh > kRasterPairCap) {
-            test_batch(total);
-            total = 0;
-          }
-          if (hit) s_pair[w][total + mbcnt(hm)] = (unsigned short)((q << 8) | kc);
-          total += nh;
+      // A: lane = face (chunk entry c*64 + lane): culled row intervals -> 64-bit pixel mask
+      const int j = c * kWave + lane;
+      uint64_t fm = 0ull;
+      if (j < nsub) {
+        const int k = L.sub[w][j];
+        const Span sp = L.span[k];
+        const int rx0 = max(sp.x0 - t.WX0, 0), rx1 = min(sp.x1 - t.WX0, 7);
+        const int ry0 = max(sp.y0 - t.WY0, 0), ry1 = min(sp.y1 - t.WY0, 7);
+        // face frame -> this sub-tile: columns shift by WX0 - span.x0, rows by the centre offset
+        const float xo = (float)(t.WX0 - sp.x0);
+        const float dref = ysub - px_cy(M, H, sp.y0);
+        const float4 cl = s_cull[0][k], ch = s_cull[1][k];
+        const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float d = drow[r] + dref;
+          const float plo = fmaxf(fmaf(cl.y, d, l0), fmaf(cl.w, d, l2)) - kSlack;
+          const float phi = fminf(fmaf(ch.y, d, h0), fmaf(ch.w, d, h2)) + kSlack;
+          const int xs = max((int)ceilf(__builtin_amdgcn_fmed3f(plo, -1.f, 9.f)), rx0);
+          const int xe = min((int)floorf(__builtin_amdgcn_fmed3f(phi, -1.f, 9.f)), rx1);
+          const bool row = r >= ry0 && r <= ry1 && xs <= xe;
+          const uint32_t bits = row ? ((2u << xe) - (1u << xs)) : 0u;
+          fm |= (uint64_t)bits << (8 * r);
         }
       }
+      // lane = pixel: candidate mask over the chunk, pairs placed by a DPP scan
+      uint64_t m = wave_transpose64(fm);
+      const int cnt = __popcll(m);
+      const int incl = wave_incl_scan(cnt);
+      int end_tot = total + __builtin_amdgcn_readlane(incl, 63);
+      int pos = total + incl - cnt;
+      const int qbits = (lane << 8) | (c << 6);
+      while (true) {
+        while (m && pos < kRasterPairCap) {
+          s_pair[w][pos++] = (unsigned short)(qbits | (int)__builtin_ctzll(m));
+          m &= m - 1ull;
+        }
+        if (end_tot <= kRasterPairCap) break;
+        test_batch(kRasterPairCap);  // the batch is exactly full
+        pos -= kRasterPairCap;
+        end_tot -= kRasterPairCap;
+      }
+      total = end_tot;
     }
     if (total) test_batch(total);
   };
@@ -595,15 +593,19 @@ int raster_forward(const FaceSet<T> &fs, int64_t max_per_view, const T *fvz, con
   if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
   size_t off = 0;
   BinBuffers bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, max_per_view);
+  const int dbg = debug_flags();
+  const bool pairs = std::is_same<T, float>::value && !(dbg & 8);
+  if (!pairs) bb.cull = nullptr;
+  bb.cull_eps = eps;
   hipError_t e = bin_faces<T>(fs, bb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> a{fs, bb, fvz, feat, D, eps, interp, face_idx, weights};
-  a.fs.dbg = debug_flags();
+  a.fs.dbg = dbg;
   const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
   {
     ProfScope prof(K_RASTER_FWD, stream);
     if constexpr (std::is_same<T, float>::value) {
-      if (!(a.fs.dbg & 8))
+      if (pairs)
         hipLaunchKernelGGL(kd_raster_fwd_pairs, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
       else
         hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);

@@ -410,6 +410,7 @@ int soft_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool build_bins,
   if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
   size_t off = 0;
   a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
+  a.bb.cull = nullptr;
   a.fs.dbg = debug_flags();
   if (build_bins) {
     hipError_t e = bin_faces<T>(fs, a.bb, stream);

@@ -167,16 +167,23 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Inclusive prefix sum over the 64 lanes of a wave with DPP: row_shr 1/2/4/8 inside each
+// 16-lane row, then row_bcast 15 / 31 carry the row totals across rows.  No LDS traffic.
+__device__ __forceinline__ int wave_incl_scan(int x) {
+  x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+  x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
 // Exclusive prefix sum over the 256 threads of the workgroup; total returned in `total`.
 // scratch: 4 ints of LDS.
 __device__ __forceinline__ int wg_exclusive_scan(int v, int *scratch, int &total) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int x = v;
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const int y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
+  const int x = wave_incl_scan(v);
   if (lane == kWave - 1) scratch[w] = x;
   __syncthreads();
   int off = 0, tot = 0;
