@@ -53,21 +53,51 @@ __device__ __forceinline__ T nmax3(T a, T b, T c) {
 // ------------------------------------------------------------------------------------------
 // Exact pixel span of a half-open box test.  The reference rejects a pixel when
 //   x0 < xmin || x0 >= xmax || y0 < ymin || y0 >= ymax
-// with x0 / y0 the fp32 centres widened to T.  Centres are monotone in the pixel index, so the
-// accepted pixels form [a, b] x [c, d]; a NaN bound rejects nothing on its side (every
-// comparison with NaN is false), exactly like the reference.  Estimate in double, then settle
-// the boundary with the exact centre formula.
+// with x0 / y0 the fp32 centres widened to T.  Centres are monotone in the pixel index (for any
+// finite multiplier; a zero multiplier makes them all 0), so the accepted pixels form
+// [a, b] x [c, d]; a NaN bound rejects nothing on its side (every comparison with NaN is false),
+// exactly like the reference.  Positive multiplier: estimate in double, then settle the boundary
+// with the exact centre formula; otherwise binary search on the exact test.
 // ------------------------------------------------------------------------------------------
 struct Span {
   short x0, x1, y0, y1;  // inclusive; empty when x0 > x1 or y0 > y1
 };
 
+// First index in [0, n) where a monotone predicate (false...false true...true) holds, n if none.
+template <typename Pred>
+__device__ inline int first_true(int n, Pred p) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (p(mid))
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  return lo;
+}
+
+// General span of `!(c(i) < lo) && !(c(i) >= hi)` for centres c(i) monotone in i (either
+// direction, ties allowed: a negative or zero multiplier), by binary search on the exact test.
+template <typename T, typename Centre>
+__device__ inline void span_monotone(T lo, T hi, int n, bool increasing, Centre c, int &a,
+                                     int &b) {
+  auto ge_lo = [&](int i) { return !((T)c(i) < lo); };
+  auto lt_hi = [&](int i) { return !((T)c(i) >= hi); };
+  if (increasing) {  // ge_lo: F..T, lt_hi: T..F
+    a = first_true(n, ge_lo);
+    b = first_true(n, [&](int i) { return !lt_hi(i); }) - 1;
+  } else {           // ge_lo: T..F, lt_hi: F..T
+    a = first_true(n, lt_hi);
+    b = first_true(n, [&](int i) { return !ge_lo(i); }) - 1;
+  }
+}
+
 template <typename T>
 __device__ inline void span_x(T lo, T hi, float M, int W, int &a, int &b) {
   const float s = M / (float)W;
-  if (!(s > 0.f) || !isfinite(s)) {  // degenerate multiplier: be conservative
-    a = 0;
-    b = W - 1;
+  if (!(s > 0.f)) {  // negative or zero multiplier (finite: checked by the C ABI)
+    span_monotone<T>(lo, hi, W, false, [&](int i) { return px_cx(M, W, i); }, a, b);
     return;
   }
   if (isnan(lo)) {
@@ -95,9 +125,8 @@ __device__ inline void span_x(T lo, T hi, float M, int W, int &a, int &b) {
 template <typename T>
 __device__ inline void span_y(T lo, T hi, float M, int H, int &c, int &d) {
   const float s = M / (float)H;
-  if (!(s > 0.f) || !isfinite(s)) {
-    c = 0;
-    d = H - 1;
+  if (!(s > 0.f)) {  // centres increase with h for a negative multiplier
+    span_monotone<T>(lo, hi, H, true, [&](int i) { return px_cy(M, H, i); }, c, d);
     return;
   }
   // rows accepted: !(cy < lo) && !(cy >= hi); cy decreases with h.

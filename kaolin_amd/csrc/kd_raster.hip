@@ -666,6 +666,7 @@ static int packed_fwd(int B, int H, int W, int64_t Fp, int D, const T *fvz, cons
                       void *stream) {
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && Fp >= 0 && D >= 0, "negative size");
   KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
   KD_CHECK_ARG(Fp < (1ll << 31), "too many faces");
   KD_CHECK_ARG(first_idx || B == 0, "first_idx is NULL");
   FaceSet<T> fs{};
@@ -689,6 +690,7 @@ static int batched_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, cons
                        int64_t *face_idx, T *weights, void *ws, size_t ws_bytes, void *stream) {
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
   KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
   KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
   FaceSet<T> fs{};
   fs.B = B;

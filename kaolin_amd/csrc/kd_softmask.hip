@@ -482,6 +482,7 @@ static int soft_fwd_raw(int B, int H, int W, int64_t F, int K, const T *fvi, con
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0, "negative size");
   KD_CHECK_ARG(K >= 1, "knum must be >= 1");
   KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
   KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
   KD_CHECK_ARG(prob && cidx && ctype, "close lists are required");
   SoftArgs<T> a{};
@@ -512,6 +513,7 @@ static int soft_fwd_fused(int B, int H, int W, int64_t F, int K, const T *fvi, d
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0, "negative size");
   KD_CHECK_ARG(K >= 1, "knum must be >= 1");
   KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
   KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
   KD_CHECK_ARG((prob && cidx && ctype) || (!prob && !cidx && !ctype),
                "close lists must be all set or all NULL");
@@ -536,6 +538,7 @@ static int soft_bwd_binned(int B, int H, int W, int64_t F, int K, const T *gs, c
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0, "negative size");
   KD_CHECK_ARG(K >= 1, "knum must be >= 1");
   KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
   const int64_t nf = (int64_t)B * F;
   if (nf > 0) {
     hipError_t e = hipMemsetAsync(gfvi, 0, sizeof(T) * nf * 6, (hipStream_t)stream);

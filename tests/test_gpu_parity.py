@@ -8,6 +8,8 @@ transcendental is involved (close_face_prob, soft mask: device expf vs glibc exp
 (summed in a different order than the oracle) to rtol 1e-4 / atol 1e-5 in fp32 and 1e-10 in fp64.
 The reference's own test tolerances are used against its goldens.
 """
+import zlib
+
 import numpy as np
 import pytest
 import torch
@@ -356,3 +358,85 @@ def test_edge_cases():
         np.testing.assert_array_equal(N(ti), ri)
     nz = T(np.array([[1., 1., 1., -1.]], np.float32))
     dibr_rasterization(19, 23, T(fvz), T(fvi), T(feat), nz)
+
+
+# --------------------------------------------------------------------------------------------
+# fp32 edge culling (kd_binning.hip raster_cull_coefs): cases aimed at its error margins --
+# vertices on pixel centres (edge functions exactly 0 at many centres), slivers, huge and tiny
+# coordinates, odd multipliers and eps.  Every output must stay bit-identical to the oracle.
+# --------------------------------------------------------------------------------------------
+def _cull_soup(kind, rng, h, w, Fn=400):
+    if kind == 'grid':
+        px = rng.integers(0, w, (1, Fn, 3))
+        py = rng.integers(0, h, (1, Fn, 3))
+        x = (2 * px + 1 - w) / w
+        y = (h - 2 * py - 1) / h
+        return np.stack([x, y], -1).astype(np.float32)
+    if kind == 'grid_half':  # corners on pixel borders / half-way points
+        px = rng.integers(0, 2 * w + 1, (1, Fn, 3))
+        py = rng.integers(0, 2 * h + 1, (1, Fn, 3))
+        return np.stack([(px - w) / w, (h - py) / h], -1).astype(np.float32)
+    if kind == 'sliver':
+        a = rng.uniform(-1, 1, (1, Fn, 1, 2))
+        d = rng.normal(0, 0.6, (1, Fn, 1, 2))
+        t = rng.uniform(0, 1, (1, Fn, 1, 1))
+        n = rng.normal(0, 1, (1, Fn, 1, 2)) * 10.0 ** rng.uniform(-9, -2, (1, Fn, 1, 1))
+        return np.concatenate([a, a + d, a + t * d + n], 2).astype(np.float32)
+    if kind == 'tiny':
+        c = rng.uniform(-1, 1, (1, Fn, 1, 2))
+        return (c + rng.normal(0, 1, (1, Fn, 3, 2)) * 10.0 **
+                rng.uniform(-7, -2, (1, Fn, 1, 1))).astype(np.float32)
+    if kind == 'huge':
+        c = rng.uniform(-1, 1, (1, Fn, 1, 2))
+        s = 10.0 ** rng.uniform(0, 12, (1, Fn, 1, 1))
+        return (c + rng.normal(0, 1, (1, Fn, 3, 2)) * s).astype(np.float32)
+    raise ValueError(kind)
+
+
+@pytest.mark.parametrize('kind', ['grid', 'grid_half', 'sliver', 'tiny', 'huge'])
+@pytest.mark.parametrize('mult_eps', [(1000, 1e-8), (1, 1e-8), (1e-3, 1e-8), (1000, 1e3),
+                                      (-1000, 1e-8), (1e6, 0.0), (7.5, 1e30)])
+def test_raster_cull_margins(kind, mult_eps):
+    from kaolin_amd.render.mesh import rasterize
+    multiplier, eps = mult_eps
+    rng = np.random.default_rng(zlib.crc32(f'{kind}/{multiplier}/{eps}'.encode()))
+    h, w = 45, 53
+    fvi = _cull_soup(kind, rng, h, w)
+    Fn = fvi.shape[1]
+    fvz = (-1 - rng.uniform(0, 1, (1, Fn, 3))).astype(np.float32)
+    if kind == 'grid':  # many exact depth ties too
+        fvz = np.round(fvz, 1).astype(np.float32)
+    feat = rng.random((1, Fn, 3, 2)).astype(np.float32)
+    interp, face_idx = rasterize(h, w, T(fvz), T(fvi), T(feat), multiplier=multiplier, eps=eps)
+    ri, rf, rw = oracle.rasterize(h, w, fvz, fvi, feat, None, multiplier=multiplier, eps=eps)
+    np.testing.assert_array_equal(N(face_idx), rf)
+    np.testing.assert_array_equal(N(interp), ri)
+
+
+@pytest.mark.parametrize('multiplier', [-1000., -1., 0.])
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_nonpositive_multiplier(multiplier, dname):
+    """Pixel centres run right-to-left / bottom-to-top (or collapse to 0): spans by exact search."""
+    from kaolin_amd.render.mesh import dibr_soft_mask, rasterize
+    dt = DTYPES[dname]
+    rng = np.random.default_rng(11)
+    h, w, Fn = 29, 37, 300
+    c = rng.uniform(-1, 1, (1, Fn, 1, 2))
+    fvi = (c + rng.normal(0, 0.15, (1, Fn, 3, 2))).astype(dt)
+    fvz = (-1 - rng.uniform(0, 1, (1, Fn, 3))).astype(dt)
+    feat = rng.random((1, Fn, 3, 2)).astype(dt)
+    interp, face_idx = rasterize(h, w, T(fvz), T(fvi), T(feat), multiplier=multiplier)
+    ri, rf, _ = oracle.rasterize(h, w, fvz, fvi, feat, None, multiplier=multiplier)
+    np.testing.assert_array_equal(N(face_idx), rf)
+    np.testing.assert_array_equal(N(interp), ri)
+    soft = dibr_soft_mask(T(fvi), face_idx, 7000, 0.05, 30, multiplier)
+    osoft, _, _, _, _ = oracle.soft_mask_forward(fvi, rf, 7000, 0.05, 30, multiplier)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+
+
+def test_nonfinite_multiplier_rejected():
+    from kaolin_amd.render.mesh import rasterize
+    z = torch.zeros((1, 2, 3), device=DEV)
+    with pytest.raises((RuntimeError, ValueError)):
+        rasterize(8, 8, z, torch.zeros((1, 2, 3, 2), device=DEV),
+                  torch.zeros((1, 2, 3, 1), device=DEV), multiplier=float('inf'))
