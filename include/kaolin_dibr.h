@@ -35,7 +35,7 @@ extern "C" {
 /* Workspace kinds for kd_workspace_size(). */
 #define KD_WS_RASTER_PACKED 1 /* kd_packed_rasterize_forward_*      */
 #define KD_WS_RASTER 2        /* kd_rasterize_forward_*             */
-#define KD_WS_SOFT_MASK 3     /* kd_dibr_soft_mask_forward*_* / _backward_binned_* */
+#define KD_WS_SOFT_MASK 3     /* kd_dibr_soft_mask_forward_* (op form)                    */
 
 /* Bytes of device workspace the call of `kind` needs.  num_faces_total = rows of the face arrays
  * (Fp for the packed layout, B*F otherwise); max_faces_per_view = the largest per-view count
@@ -55,8 +55,11 @@ void kd_profile_enable(int on);
 int kd_profile_collect(double *total_ms, int64_t *launches, int n);
 const char *kd_profile_kernel_name(int id);
 
-/* Diagnostics only: ablation switches read by the kernels (0 = production). */
+/* Diagnostics only: ablation switches read by the kernels (0 = production), and (flag 64) a
+ * device int64 array of 3 * views * tiles entries receiving per-tile durations (100 MHz ticks)
+ * of the raster forward / soft forward / soft backward tile kernels. */
 int kd_debug_set(int flags);
+int kd_debug_buffer(void *device_ptr);
 
 /* ---------------------------------------------------------------------------------------------
  * Packed rasterize forward.  Replaces _C.render.mesh.packed_rasterize_forward_cuda
@@ -134,24 +137,28 @@ int kd_dibr_soft_mask_forward_f64(int batch, int height, int width, int64_t num_
 
 /* ---------------------------------------------------------------------------------------------
  * DIB-R soft mask forward from UNSCALED fvi (DibrSoftMaskCuda.forward dibr.py:29-55 fused: the
- * x multiplier and the +-boxlen*multiplier bounding boxes are computed in the kernel).
+ * x multiplier and the +-boxlen*multiplier bounding boxes are computed in the kernels).
  * close_last (B, H, W) int32, if not NULL, receives per pixel the K-th close face when the list
  * is full, else -1.  The three close_face_* lists may all be NULL (then they are not
- * materialised).  Keep `workspace` for kd_dibr_soft_mask_backward_binned_* (bins_ready = 1).
+ * materialised).  Workspace: kd_soft_mask_workspace_size().  With want_grad != 0 the workspace
+ * also receives every (pixel, close face) pair's backward coefficients; keep it for
+ * kd_dibr_soft_mask_backward_binned_* (bins_ready = 1).
  * ------------------------------------------------------------------------------------------- */
+size_t kd_soft_mask_workspace_size(int batch, int height, int width, int64_t num_faces, int knum,
+                                   int double_precision);
 int kd_dibr_soft_mask_forward_fused_f32(int batch, int height, int width, int64_t num_faces,
                                         int knum, const float *fvi, double multiplier,
                                         double boxlen, const int64_t *face_idx, float sigmainv,
                                         float *soft_mask, float *close_face_prob,
                                         int64_t *close_face_idx, uint8_t *close_face_dist_type,
-                                        int32_t *close_last, void *workspace,
+                                        int32_t *close_last, int want_grad, void *workspace,
                                         size_t workspace_bytes, void *stream);
 int kd_dibr_soft_mask_forward_fused_f64(int batch, int height, int width, int64_t num_faces,
                                         int knum, const double *fvi, double multiplier,
                                         double boxlen, const int64_t *face_idx, float sigmainv,
                                         double *soft_mask, double *close_face_prob,
                                         int64_t *close_face_idx, uint8_t *close_face_dist_type,
-                                        int32_t *close_last, void *workspace,
+                                        int32_t *close_last, int want_grad, void *workspace,
                                         size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
@@ -175,13 +182,13 @@ int kd_dibr_soft_mask_backward_f64(int batch, int height, int width, int64_t num
                                    void *stream);
 
 /* ---------------------------------------------------------------------------------------------
- * DIB-R soft mask backward, recompute form (the autograd path of dibr_soft_mask): no close
- * lists.  For every uncovered pixel the first K close faces and their distance types /
- * probabilities are re-derived bit-identically from the same tile bins as the forward, the
- * reference's gradient terms (dibr_soft_mask_cuda.cu:281-348) are summed per face and tile in
- * LDS and added with float atomics.  `workspace` is the fused forward's workspace: with
- * bins_ready != 0 its bins (same fvi / multiplier / boxlen) are reused, else they are rebuilt.
- * fvi is NOT scaled; grad_fvi is the gradient w.r.t. fvi.
+ * DIB-R soft mask backward, autograd form (DibrSoftMaskCuda.backward dibr.py:57-73 without close
+ * lists).  `workspace` is the fused forward's (want_grad = 1, same fvi / multiplier / boxlen /
+ * knum, bins_ready != 0): every pair's stored coefficients times the pixel's
+ * -sigmainv * grad * (1 - soft) are summed per face and tile in LDS and added with float atomics
+ * (the reference's terms dibr_soft_mask_cuda.cu:281-348, up to rounding order).  With
+ * bins_ready == 0 the pairs and coefficients are rebuilt first.  fvi is NOT scaled; grad_fvi is
+ * the gradient w.r.t. fvi.
  * ------------------------------------------------------------------------------------------- */
 int kd_dibr_soft_mask_backward_binned_f32(int batch, int height, int width, int64_t num_faces,
                                           int knum, const float *grad_soft_mask,

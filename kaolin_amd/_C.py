@@ -273,10 +273,11 @@ def rasterize_backward_autograd(grad_interp, face_idx, weights, face_vertices_im
 
 
 def dibr_soft_mask_forward_fused(face_vertices_image, selected_face_idx, sigmainv, boxlen, knum,
-                                 multiplier, with_lists=False):
+                                 multiplier, with_lists=False, want_grad=True):
     """DibrSoftMaskCuda.forward (dibr.py:29-55) with the x multiplier and the enlarged boxes in
-    the kernel.  Returns (soft, workspace, prob, cidx, ctype) (lists None unless with_lists); the
-    workspace holds the tile bins the backward reuses."""
+    the kernel.  Returns (soft, workspace, prob, cidx, ctype) (lists None unless with_lists); with
+    want_grad the workspace holds the (pixel, face) records and backward coefficients that
+    dibr_soft_mask_backward_binned consumes."""
     fn = 'dibr_soft_mask'
     dev = _check_same_gpu(fn, face_vertices_image=face_vertices_image,
                           selected_face_idx=selected_face_idx)
@@ -295,17 +296,19 @@ def dibr_soft_mask_forward_fused(face_vertices_image, selected_face_idx, sigmain
         prob = torch.empty((B, H, W, knum), **opts)
         cidx = torch.empty((B, H, W, knum), device=dev, dtype=torch.long)
         ctype = torch.empty((B, H, W, knum), device=dev, dtype=torch.uint8)
-    ws, nb = _workspace(_lib.KD_WS_SOFT_MASK, dev, B, H, W, B * F, F)
+    nb = _lib.soft_mask_workspace_size(B, H, W, F, knum, face_vertices_image.dtype == torch.float64)
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
     _lib.call(f'kd_dibr_soft_mask_forward_fused_{sfx}', B, H, W, F, knum,
               _ptr(face_vertices_image), float(multiplier), float(boxlen),
               _ptr(selected_face_idx), float(sigmainv), _ptr(soft), _ptr(prob), _ptr(cidx),
-              _ptr(ctype), None, _ptr(ws), nb, _stream(dev))
+              _ptr(ctype), None, 1 if want_grad else 0, _ptr(ws), nb, _stream(dev))
     return soft, ws, prob, cidx, ctype
 
 
 def dibr_soft_mask_backward_binned(grad_soft, soft, selected_face_idx, face_vertices_image,
                                    multiplier, boxlen, sigmainv, knum, workspace):
-    """DibrSoftMaskCuda.backward without close lists (recompute over the forward's bins)."""
+    """DibrSoftMaskCuda.backward without close lists, from the forward's workspace (records and
+    backward coefficients, kd_softpair.hip)."""
     dev = grad_soft.device
     B, F = face_vertices_image.shape[:2]
     H, W = selected_face_idx.shape[1:3]

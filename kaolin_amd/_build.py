@@ -16,7 +16,7 @@ LIBDIR = os.path.join(PKG, 'lib')
 LIB = os.path.join(LIBDIR, 'libkaolin_dibr.so')
 OBJDIR = os.path.join(PKG, 'build')
 
-SOURCES = ['kd_capi.cpp', 'kd_binning.hip', 'kd_raster.hip', 'kd_softmask.hip']
+SOURCES = ['kd_capi.cpp', 'kd_binning.hip', 'kd_raster.hip', 'kd_softmask.hip', 'kd_softpair.hip']
 HEADERS = ['kd_common.hpp', 'kd_binning.hpp', 'kd_capi.hpp']
 ARCH = os.environ.get('KAOLIN_AMD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
@@ -56,7 +56,8 @@ def build(force=False, verbose=True):
         objs = list(ex.map(_compile, SOURCES))
     if force or _stale(LIB, objs):
         tmp = LIB + f'.{os.getpid()}.tmp'
-        subprocess.check_call([HIPCC, '-shared', f'--offload-arch={ARCH}', *objs, '-o', tmp])
+        subprocess.check_call([HIPCC, '-shared', f'--offload-arch={ARCH}', *objs, '-Wl,--no-undefined',
+                               '-o', tmp])
         os.replace(tmp, LIB)
         if verbose:
             print(f'[kaolin_amd] built {LIB}', file=sys.stderr)

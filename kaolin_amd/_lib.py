@@ -34,8 +34,8 @@ _SIGS = {
     'kd_dibr_soft_mask_forward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_float,
                                   c_float, c_p, c_p, c_p, c_p, c_p, c_size, c_p],
     'kd_dibr_soft_mask_forward_fused': [c_int, c_int, c_int, c_i64, c_int, c_p, c_double,
-                                        c_double, c_p, c_float, c_p, c_p, c_p, c_p, c_p, c_p,
-                                        c_size, c_p],
+                                        c_double, c_p, c_float, c_p, c_p, c_p, c_p, c_p, c_int,
+                                        c_p, c_size, c_p],
     'kd_dibr_soft_mask_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
                                    c_p, c_p, c_float, c_float, c_p, c_p],
     'kd_dibr_soft_mask_backward_binned': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,
@@ -58,6 +58,8 @@ def load():
             lib = ctypes.CDLL(LIB_PATH)
             lib.kd_workspace_size.argtypes = [c_int, c_int, c_int, c_int, c_i64, c_i64]
             lib.kd_workspace_size.restype = c_size
+            lib.kd_soft_mask_workspace_size.argtypes = [c_int, c_int, c_int, c_i64, c_int, c_int]
+            lib.kd_soft_mask_workspace_size.restype = c_size
             lib.kd_last_error.argtypes = []
             lib.kd_last_error.restype = ctypes.c_char_p
             lib.kd_version.restype = c_int
@@ -69,6 +71,8 @@ def load():
             lib.kd_profile_kernel_name.restype = ctypes.c_char_p
             lib.kd_debug_set.argtypes = [c_int]
             lib.kd_debug_set.restype = c_int
+            lib.kd_debug_buffer.argtypes = [c_p]
+            lib.kd_debug_buffer.restype = c_int
             for base, sig in _SIGS.items():
                 for sfx in ('f32', 'f64'):
                     fn = getattr(lib, f'{base}_{sfx}')
@@ -87,6 +91,10 @@ def call(name, *args):
 
 def workspace_size(kind, B, H, W, n_total, max_per_view):
     return int(load().kd_workspace_size(kind, B, H, W, n_total, max_per_view))
+
+
+def soft_mask_workspace_size(B, H, W, F, knum, double_precision):
+    return int(load().kd_soft_mask_workspace_size(B, H, W, F, knum, 1 if double_precision else 0))
 
 
 def profile_enable(on=True):

@@ -36,6 +36,8 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   bb.cull = (float4 *)(base + off);
   off += align_up(sizeof(float4) * 2 * (size_t)N);
   bb.cull_eps = 0.f;
+  bb.clear = nullptr;
+  bb.n_clear = 0;
   return bb;
 }
 
@@ -112,6 +114,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(FaceSet<T> fs, BinBuffers
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
   for (int c = tid; c < nct; c += kBlock) s_cnt[c] = 0;
+  if (bb.clear && b == 0 && chunk == 0 && tid < bb.n_clear) bb.clear[tid] = 0;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   const int64_t i = lo + (int64_t)chunk * kChunk + tid;
@@ -231,7 +234,11 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(FaceSet<T> fs, BinBuffe
 template <typename T>
 hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t stream) {
   if (bb.nchunk <= 0 || fs.B <= 0) {
-    // no faces: totals must still read zero
+    // no faces: totals (and the counters kd_bin_count would clear) must still read zero
+    if (bb.clear && bb.n_clear > 0) {
+      const hipError_t e = hipMemsetAsync(bb.clear, 0, sizeof(int) * bb.n_clear, stream);
+      if (e != hipSuccess) return e;
+    }
     return hipMemsetAsync(bb.totals, 0, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * bb.g.nct(),
                           stream);
   }

@@ -32,6 +32,8 @@ struct BinBuffers {
   int *bins;
   float4 *cull;    // nullptr: not computed
   float cull_eps;  // the raster eps (cull coefficients only)
+  int *clear;      // nullable: n_clear ints zeroed by kd_bin_count (counters of later passes)
+  int n_clear;
   int nchunk;
   BinGeom g;
 };

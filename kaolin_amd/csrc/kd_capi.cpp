@@ -15,6 +15,8 @@ char *error_buffer() {
 
 std::atomic<int> g_debug{0};
 int debug_flags() { return g_debug.load(); }
+std::atomic<long long *> g_tbuf{nullptr};
+long long *debug_tile_buffer() { return (g_debug.load() & 64) ? g_tbuf.load() : nullptr; }
 
 namespace {
 std::atomic<bool> g_prof{false};
@@ -27,7 +29,7 @@ std::vector<Rec> g_recs;
 const char *kNames[K_NUM_KERNELS] = {
     "kd_bin_count", "kd_bin_scan", "kd_bin_scatter", "kd_raster_fwd", "kd_soft_fwd",
     "kd_raster_bwd_tile", "kd_soft_bwd_tile", "kd_raster_bwd_atomic", "kd_soft_bwd_atomic",
-    "kd_zero"};
+    "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs"};
 }  // namespace
 
 ProfScope::ProfScope(int id_, hipStream_t s) : id(id_), stream(s), on(g_prof.load()) {
@@ -67,6 +69,11 @@ void kd_profile_enable(int on) { kd::g_prof.store(on != 0); }
 
 int kd_debug_set(int flags) {
   kd::g_debug.store(flags);
+  return KD_OK;
+}
+
+int kd_debug_buffer(void *device_ptr) {
+  kd::g_tbuf.store((long long *)device_ptr);
   return KD_OK;
 }
 

@@ -23,6 +23,10 @@ enum KernelId {
   K_RASTER_BWD_ATOMIC,
   K_SOFT_BWD_ATOMIC,
   K_ZERO,
+  K_SOFT_PAIRS,
+  K_SOFT_MATH,
+  K_SOFT_REDUCE,
+  K_SOFT_BWD_PAIRS,
   K_NUM_KERNELS
 };
 

@@ -17,8 +17,25 @@ namespace kd {
 // Diagnostic ablation switches (kd_debug_set, copied into FaceSet::dbg); 0 in production.
 // Bits: 1 skip the per-pixel face tests of the forward kernels, 2 skip staging face data,
 //       4 skip the per-batch work entirely (bin walk only), 8 fp32 raster: lane-per-pixel
-//       kernel instead of the pair pipeline.
+//       kernel instead of the pair pipeline, 16 / 32 skip the per-pair pass of the fp32
+//       raster / soft mask, 64 record per-tile durations into the kd_debug_buffer array.
 int debug_flags();
+long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
+
+// Per-workgroup duration (wall clock, 100 MHz ticks) for diagnostics: written by thread 0 when
+// the workgroup's kernel body returns.
+struct TileClock {
+  long long *buf;
+  long long t0;
+  int64_t idx;
+  __device__ TileClock(long long *b, int slot)
+      : buf(b), t0(b ? wall_clock64() : 0),
+        idx((int64_t)slot * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x +
+            blockIdx.x) {}
+  __device__ ~TileClock() {
+    if (buf && threadIdx.x == 0) buf[idx] = wall_clock64() - t0;
+  }
+};
 
 constexpr int kWave = 64;
 constexpr int kBlock = 256;      // 4 waves
@@ -194,6 +211,7 @@ struct FaceSet {
   const uint8_t *valid;      // (N) uint8 or nullptr
   float M;                   // float multiplier of the pixel centres
   int dbg;                   // diagnostic ablation flags (0 in production)
+  long long *tbuf;           // diagnostic per-tile clock buffer (nullptr in production)
 };
 
 template <typename T>

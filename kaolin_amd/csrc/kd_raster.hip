@@ -185,25 +185,8 @@ __device__ __forceinline__ uint32_t ordered_f32(float z) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// 64x64 bit-matrix transpose across a wave: lane l bit j -> lane j bit l (block swaps).
-__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t masks[6] = {0x00000000ffffffffull, 0x0000ffff0000ffffull,
-                             0x00ff00ff00ff00ffull, 0x0f0f0f0f0f0f0f0full,
-                             0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    const int sh = 32 >> st;
-    const uint64_t mlo = masks[st];
-    const uint32_t ylo = (uint32_t)__shfl_xor((int)(uint32_t)x, sh);
-    const uint32_t yhi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), sh);
-    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
-    x = (lane & sh) ? ((x & ~mlo) | ((y & ~mlo) >> sh)) : ((x & mlo) | ((y & mlo) << sh));
-  }
-  return x;
-}
-
 __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<float> a) {
+  TileClock clk(a.fs.tbuf, 0);
   __shared__ TileLists L;
   __shared__ float s_geo[9][kCap];   // ax ay bx by cx cy (scaled), az bz cz
   __shared__ float4 s_cull[2][kCap];  // raster_cull_coefs (kd_binning), face frame
@@ -601,6 +584,7 @@ int raster_forward(const FaceSet<T> &fs, int64_t max_per_view, const T *fvz, con
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> a{fs, bb, fvz, feat, D, eps, interp, face_idx, weights};
   a.fs.dbg = dbg;
+  a.fs.tbuf = debug_tile_buffer();
   const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
   {
     ProfScope prof(K_RASTER_FWD, stream);

@@ -1,0 +1,218 @@
+// kd_soft.hpp -- shared pieces of the DIB-R soft-mask kernels (kd_softmask.hip, kd_softpair.hip):
+// the reference's per-pair arithmetic (distance type / probability, backward terms), the per-wave
+// (pixel, face) pair book and pass A (first K close faces per pixel over the tile lists).
+#pragma once
+
+#include "kd_binning.hpp"
+#include "kd_capi.hpp"
+#include "kd_tile.hpp"
+
+namespace kd {
+
+#define KD_SOFT_EPS 1e-7  // dibr_soft_mask_cuda.cu:23 (a double literal)
+
+__device__ __forceinline__ float kexp(float x) { return expf(x); }
+__device__ __forceinline__ double kexp(double x) { return exp(x); }
+
+// dibr_soft_mask_cuda.cu:100-163: squared distance type (0..5) and probability of one face.
+template <typename T>
+__device__ __forceinline__ void soft_face_dist(T x0, T y0, const T v[6], float M, float sigmainv,
+                                               int &edgeid, T &prob) {
+  T pdis[6];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int j = (i + 1) % 3;
+    const T x1 = v[i * 2], y1 = v[i * 2 + 1], x2 = v[j * 2], y2 = v[j * 2 + 1];
+    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+    const T up = A * x0 + Bc * y0 + C;
+    const T down = A * A + Bc * Bc;
+    T x3 = Bc * Bc * x0 - A * Bc * y0 - A * C;
+    T y3 = A * A * y0 - A * Bc * x0 - Bc * C;
+    x3 = (T)((double)x3 / ((double)down + KD_SOFT_EPS));
+    y3 = (T)((double)y3 / ((double)down + KD_SOFT_EPS));
+    const T direct = (x3 - x1) * (x3 - x2) + (y3 - y1) * (y3 - y2);
+    if (direct > (T)0)
+      pdis[i] = (T)(4.0f * M * M);
+    else
+      pdis[i] = (T)((double)(up * up) / ((double)down + KD_SOFT_EPS));
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const T x1 = v[i * 2], y1 = v[i * 2 + 1];
+    pdis[i + 3] = (x0 - x1) * (x0 - x1) + (y0 - y1) * (y0 - y1);
+  }
+  edgeid = 0;
+  T d = pdis[0];
+#pragma unroll
+  for (int i = 1; i < 6; ++i)
+    if (d > pdis[i]) {
+      d = pdis[i];
+      edgeid = i;
+    }
+  const T z = (T)sigmainv * d / (T)M / (T)M;
+  prob = kexp(-z);
+}
+
+// backward terms of one (pixel, close face) pair, dibr_soft_mask_cuda.cu:281-348; adds to the
+// face's 6 corner gradients (already divided by M per term, like the reference).
+template <typename T>
+__device__ __forceinline__ void soft_bwd_terms(T x0, T y0, const T v[6], int edgeid, T prob,
+                                               T dLdp, T allprob, float sigmainv, float M,
+                                               T g[6]) {
+  const T dLdz = (T)(-1.0 * (double)sigmainv * (double)dLdp * (1.0 - (double)allprob) /
+                     (1.0 - (double)prob + KD_SOFT_EPS) * (double)prob);
+  if (edgeid >= 3) {
+    const int ps = (edgeid - 3) * 2;
+    const T x1 = v[ps], y1 = v[ps + 1];
+    const T dLdx1 = dLdz * (T)2 * (x1 - x0);
+    const T dLdy1 = dLdz * (T)2 * (y1 - y0);
+    g[ps] += dLdx1 / (T)M;
+    g[ps + 1] += dLdy1 / (T)M;
+  } else {
+    const int ps = edgeid * 2, ps2 = ((edgeid + 1) % 3) * 2;
+    const T x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
+    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+    const T up = A * x0 + Bc * y0 + C;
+    const T down = A * A + Bc * Bc;
+    const T dissquare = (T)((double)(up * up) / ((double)down + KD_SOFT_EPS));
+    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) / ((double)down + KD_SOFT_EPS));
+    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) / ((double)down + KD_SOFT_EPS));
+    const T dzdC = (T)((double)((T)2 * up) / ((double)down + KD_SOFT_EPS));
+    const T dLdx1 = dLdz * (dzdB - y2 * dzdC);
+    const T dLdy1 = dLdz * (x2 * dzdC - dzdA);
+    const T dLdx2 = dLdz * (y1 * dzdC - dzdB);
+    const T dLdy2 = dLdz * (dzdA - x1 * dzdC);
+    g[ps] += dLdx1 / (T)M;
+    g[ps + 1] += dLdy1 / (T)M;
+    g[ps2] += dLdx2 / (T)M;
+    g[ps2 + 1] += dLdy2 / (T)M;
+  }
+}
+
+constexpr int kPairCap = 512;  // (pixel, face) pairs per wave batch
+
+template <typename T>
+struct SoftArgs {
+  FaceSet<T> fs;
+  BinBuffers bb;
+  const int64_t *face_idx;
+  int K;
+  float sigmainv;
+  // forward outputs
+  T *soft;
+  T *prob;
+  int64_t *cidx;
+  uint8_t *ctype;
+  int32_t *last;
+  // backward
+  const T *grad_soft;
+  const T *soft_in;
+  T *grad_fvi;
+};
+
+// Per-wave pair list of the current batch and its per-pixel bookkeeping.
+struct PairBook {
+  unsigned short pair[4][kPairCap];  // (q << 8) | k, q = pixel lane, k = tile-list entry
+  short start[4][64], n[4][64], base[4][64];
+};
+
+// Pass A over the uncovered pixels of this wave for one batch of tile faces: per pixel, the
+// first K - kid hits (ascending face order = ascending ballot rank) are appended to the pair
+// list.  flush(npairs) runs passes B / C whenever the list is full and at the end.
+template <typename Flush>
+__device__ __forceinline__ void soft_pass_a(const SubSpans &ss, int nsub, PairBook &P,
+                                            uint64_t umask, int K, const TileGeom &t,
+                                            int &my_kid, Flush flush) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int npairs = 0;
+  P.n[w][lane] = 0;
+  for (uint64_t mm = umask; mm; mm &= mm - 1) {
+    const int q = __builtin_ctzll(mm);
+    int kid = rdlane_i(my_kid, q);
+    if (kid >= K) continue;
+    const int qx = t.WX0 + (q & 7), qy = t.WY0 + (q >> 3);
+    int start = npairs, base = kid;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (c * kWave >= nsub || kid >= K) break;
+      const bool hit = pspan_has(ss.s[c], qx, qy);  // dibr_soft_mask_cuda.cu:95, exact
+      const uint64_t hm = __ballot(hit);
+      if (!hm) continue;
+      const int need = K - kid;
+      const int nh = __popcll(hm);
+      const int ntake = nh < need ? nh : need;
+      if (npairs + ntake > kPairCap) {
+        if (lane == 0) {
+          P.start[w][q] = (short)start;
+          P.n[w][q] = (short)(npairs - start);
+          P.base[w][q] = (short)base;
+        }
+        flush(npairs);
+        npairs = 0;
+        start = 0;
+        base = kid;
+      }
+      const int rank = mbcnt(hm);
+      if (hit && rank < need) P.pair[w][npairs + rank] = (unsigned short)((q << 8) | ss.k[c]);
+      npairs += ntake;
+      kid += ntake;
+    }
+    if (lane == 0) {
+      P.start[w][q] = (short)start;
+      P.n[w][q] = (short)(npairs - start);
+      P.base[w][q] = (short)base;
+    }
+    if (lane == q) my_kid = kid;
+  }
+  flush(npairs);
+}
+
+template <typename T>
+__device__ __forceinline__ void soft_stage(const FaceSet<T> &fs, T (*geo)[kCap], int k,
+                                           int64_t fi) {
+  T v[6];
+  load_corners(fs, fi, v);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) geo[q][k] = v[q];
+}
+
+// ------------------------------------------------------------------------------------------
+// pair pipeline of the autograd path (kd_softpair.hip)
+// ------------------------------------------------------------------------------------------
+struct SoftPairRec {
+  int32_t row;    // face row (view offset + face index)
+  uint32_t lid;   // position of the face in the tile's face list (all batches)
+  uint16_t slot;  // close-face slot of the pixel, 0..K-1
+  uint8_t q;      // pixel of the tile (tile_geom thread index)
+  uint8_t type;   // distance type 0..5 (set by the math pass)
+};
+
+template <typename T>
+struct SoftCoef {
+  T h[4];
+};
+
+template <typename T>
+struct SoftPairBuf {
+  SoftPairRec *rec;   // [B * ntiles][cap]
+  SoftCoef<T> *coef;  // [B * ntiles][cap] backward coefficients
+  T *sprob;           // [B * H * W][K] probability by (pixel, slot)
+  int32_t *npix;      // [B * H * W] close faces of each uncovered pixel
+  int32_t *ntile;     // [B * ntiles][2]: records, faces in the tile list
+  int2 *items;        // [B * ntiles * ceil(cap / 256)] (tile, 256-record chunk) work items
+  int32_t *tiles;     // [B * ntiles] tiles with records
+  int32_t *counters;  // [2]: items, tiles (zeroed by the binning's count kernel)
+  int64_t ntiles, cap;
+  int ntx;
+};
+
+// bins + pair buffers for B views of F faces, K close faces, element size esize
+size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize);
+// bins + pass A + pair math (+ backward coefficients when grad) + (when reduce) the soft mask
+template <typename T>
+int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, bool reduce,
+                       hipStream_t stream);
+template <typename T>
+int soft_pairs_backward(SoftArgs<T> &a, void *ws, size_t ws_bytes, hipStream_t stream);
+
+}  // namespace kd

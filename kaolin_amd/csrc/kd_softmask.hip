@@ -14,190 +14,20 @@
 //   The expensive distance math (9 double divisions) thus runs with every lane busy, once per
 //   (pixel, close face) pair.  With the close lists not requested nothing but soft (and
 //   optionally close_last) is written.
+// This file serves the reference's op forms (_C.render.mesh.dibr_soft_mask_forward_cuda /
+// _backward_cuda: explicit boxes, close lists in and out); the autograd path is the pair
+// pipeline of kd_softpair.hip.
 // Backward.
-//   kd_soft_bwd_tile   -- autograd form: the same tiles, bins reused from the forward's workspace,
-//                         pass A re-derives each uncovered pixel's first-K close faces, pass B
-//                         computes the reference's gradient terms per pair and accumulates them
-//                         per face in LDS (ds_add); one global float atomic per (tile, face,
-//                         coordinate) flushes them.  No close lists are read or stored.
 //   kd_soft_bwd_atomic -- general form of the reference op (any given close lists), one thread
 //                         per pixel, float atomics (dibr_soft_mask_cuda.cu:230-353).
 #include "../../include/kaolin_dibr.h"
-#include "kd_binning.hpp"
-#include "kd_capi.hpp"
-#include "kd_tile.hpp"
+#include "kd_soft.hpp"
 
 namespace kd {
 
-#define KD_SOFT_EPS 1e-7  // dibr_soft_mask_cuda.cu:23 (a double literal)
-
-__device__ __forceinline__ float kexp(float x) { return expf(x); }
-__device__ __forceinline__ double kexp(double x) { return exp(x); }
-
-// dibr_soft_mask_cuda.cu:100-163: squared distance type (0..5) and probability of one face.
-template <typename T>
-__device__ __forceinline__ void soft_face_dist(T x0, T y0, const T v[6], float M, float sigmainv,
-                                               int &edgeid, T &prob) {
-  T pdis[6];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int j = (i + 1) % 3;
-    const T x1 = v[i * 2], y1 = v[i * 2 + 1], x2 = v[j * 2], y2 = v[j * 2 + 1];
-    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-    const T up = A * x0 + Bc * y0 + C;
-    const T down = A * A + Bc * Bc;
-    T x3 = Bc * Bc * x0 - A * Bc * y0 - A * C;
-    T y3 = A * A * y0 - A * Bc * x0 - Bc * C;
-    x3 = (T)((double)x3 / ((double)down + KD_SOFT_EPS));
-    y3 = (T)((double)y3 / ((double)down + KD_SOFT_EPS));
-    const T direct = (x3 - x1) * (x3 - x2) + (y3 - y1) * (y3 - y2);
-    if (direct > (T)0)
-      pdis[i] = (T)(4.0f * M * M);
-    else
-      pdis[i] = (T)((double)(up * up) / ((double)down + KD_SOFT_EPS));
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const T x1 = v[i * 2], y1 = v[i * 2 + 1];
-    pdis[i + 3] = (x0 - x1) * (x0 - x1) + (y0 - y1) * (y0 - y1);
-  }
-  edgeid = 0;
-  T d = pdis[0];
-#pragma unroll
-  for (int i = 1; i < 6; ++i)
-    if (d > pdis[i]) {
-      d = pdis[i];
-      edgeid = i;
-    }
-  const T z = (T)sigmainv * d / (T)M / (T)M;
-  prob = kexp(-z);
-}
-
-// backward terms of one (pixel, close face) pair, dibr_soft_mask_cuda.cu:281-348; adds to the
-// face's 6 corner gradients (already divided by M per term, like the reference).
-template <typename T>
-__device__ __forceinline__ void soft_bwd_terms(T x0, T y0, const T v[6], int edgeid, T prob,
-                                               T dLdp, T allprob, float sigmainv, float M,
-                                               T g[6]) {
-  const T dLdz = (T)(-1.0 * (double)sigmainv * (double)dLdp * (1.0 - (double)allprob) /
-                     (1.0 - (double)prob + KD_SOFT_EPS) * (double)prob);
-  if (edgeid >= 3) {
-    const int ps = (edgeid - 3) * 2;
-    const T x1 = v[ps], y1 = v[ps + 1];
-    const T dLdx1 = dLdz * (T)2 * (x1 - x0);
-    const T dLdy1 = dLdz * (T)2 * (y1 - y0);
-    g[ps] += dLdx1 / (T)M;
-    g[ps + 1] += dLdy1 / (T)M;
-  } else {
-    const int ps = edgeid * 2, ps2 = ((edgeid + 1) % 3) * 2;
-    const T x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
-    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-    const T up = A * x0 + Bc * y0 + C;
-    const T down = A * A + Bc * Bc;
-    const T dissquare = (T)((double)(up * up) / ((double)down + KD_SOFT_EPS));
-    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) / ((double)down + KD_SOFT_EPS));
-    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) / ((double)down + KD_SOFT_EPS));
-    const T dzdC = (T)((double)((T)2 * up) / ((double)down + KD_SOFT_EPS));
-    const T dLdx1 = dLdz * (dzdB - y2 * dzdC);
-    const T dLdy1 = dLdz * (x2 * dzdC - dzdA);
-    const T dLdx2 = dLdz * (y1 * dzdC - dzdB);
-    const T dLdy2 = dLdz * (dzdA - x1 * dzdC);
-    g[ps] += dLdx1 / (T)M;
-    g[ps + 1] += dLdy1 / (T)M;
-    g[ps2] += dLdx2 / (T)M;
-    g[ps2 + 1] += dLdy2 / (T)M;
-  }
-}
-
-constexpr int kPairCap = 512;  // (pixel, face) pairs per wave batch
-
-template <typename T>
-struct SoftArgs {
-  FaceSet<T> fs;
-  BinBuffers bb;
-  const int64_t *face_idx;
-  int K;
-  float sigmainv;
-  // forward outputs
-  T *soft;
-  T *prob;
-  int64_t *cidx;
-  uint8_t *ctype;
-  int32_t *last;
-  // backward
-  const T *grad_soft;
-  const T *soft_in;
-  T *grad_fvi;
-};
-
-// Per-wave pair list of the current batch and its per-pixel bookkeeping.
-struct PairBook {
-  unsigned short pair[4][kPairCap];  // (q << 8) | k, q = pixel lane, k = tile-list entry
-  short start[4][64], n[4][64], base[4][64];
-};
-
-// Pass A over the uncovered pixels of this wave for one batch of tile faces: per pixel, the
-// first K - kid hits (ascending face order = ascending ballot rank) are appended to the pair
-// list.  flush(npairs) runs passes B / C whenever the list is full and at the end.
-template <typename Flush>
-__device__ __forceinline__ void soft_pass_a(const SubSpans &ss, int nsub, PairBook &P,
-                                            uint64_t umask, int K, const TileGeom &t,
-                                            int &my_kid, Flush flush) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int npairs = 0;
-  P.n[w][lane] = 0;
-  for (uint64_t mm = umask; mm; mm &= mm - 1) {
-    const int q = __builtin_ctzll(mm);
-    int kid = rdlane_i(my_kid, q);
-    if (kid >= K) continue;
-    const int qx = t.WX0 + (q & 7), qy = t.WY0 + (q >> 3);
-    int start = npairs, base = kid;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c * kWave >= nsub || kid >= K) break;
-      const bool hit = pspan_has(ss.s[c], qx, qy);  // dibr_soft_mask_cuda.cu:95, exact
-      const uint64_t hm = __ballot(hit);
-      if (!hm) continue;
-      const int need = K - kid;
-      const int nh = __popcll(hm);
-      const int ntake = nh < need ? nh : need;
-      if (npairs + ntake > kPairCap) {
-        if (lane == 0) {
-          P.start[w][q] = (short)start;
-          P.n[w][q] = (short)(npairs - start);
-          P.base[w][q] = (short)base;
-        }
-        flush(npairs);
-        npairs = 0;
-        start = 0;
-        base = kid;
-      }
-      const int rank = mbcnt(hm);
-      if (hit && rank < need) P.pair[w][npairs + rank] = (unsigned short)((q << 8) | ss.k[c]);
-      npairs += ntake;
-      kid += ntake;
-    }
-    if (lane == 0) {
-      P.start[w][q] = (short)start;
-      P.n[w][q] = (short)(npairs - start);
-      P.base[w][q] = (short)base;
-    }
-    if (lane == q) my_kid = kid;
-  }
-  flush(npairs);
-}
-
-template <typename T>
-__device__ __forceinline__ void soft_stage(const FaceSet<T> &fs, T (*geo)[kCap], int k,
-                                           int64_t fi) {
-  T v[6];
-  load_corners(fs, fi, v);
-#pragma unroll
-  for (int q = 0; q < 6; ++q) geo[q][k] = v[q];
-}
-
 template <typename T, bool LISTS>
 __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
+  TileClock clk(a.fs.tbuf, 1);
   __shared__ TileLists L;
   __shared__ T s_geo[6][kCap];  // scaled corners
   __shared__ PairBook P;
@@ -222,6 +52,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
   if (__syncthreads_or(unc)) {
     auto stage = [&](int k, int64_t fi) { soft_stage(fs, s_geo, k, fi); };
     auto flush = [&](int npairs) {  // passes B and C
+      if (fs.dbg & 32) npairs = 0;
       wave_lds_sync();
       for (int e = lane; e < npairs; e += kWave) {
         const int pr = P.pair[w][e];
@@ -259,7 +90,9 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
       const SubSpans ss = load_subspans(L, nsub);
       soft_pass_a(ss, nsub, P, umask, K, t, my_kid, flush);
     };
-    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
+    // once every uncovered pixel of the tile holds K close faces, later faces cannot enter
+    auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
+    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg, done);
   }
 
   if (!t.wave_live) return;
@@ -293,75 +126,6 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
       }
     }
   }
-}
-
-template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_soft_bwd_tile(SoftArgs<T> a) {
-  __shared__ TileLists L;
-  __shared__ T s_geo[6][kCap];
-  __shared__ T s_acc[6][kCap];
-  __shared__ PairBook P;
-  __shared__ T s_pg[4][64], s_ps[4][64];  // grad_soft, soft of each pixel
-
-  const FaceSet<T> &fs = a.fs;
-  const int H = fs.H, W = fs.W, K = a.K;
-  const float M = fs.M;
-  const int b = blockIdx.y;
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  int64_t lo, hi;
-  view_range(fs, b, lo, hi);
-  const TileGeom t = tile_geom(H, W);
-  const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-  const bool unc = t.inimg && a.face_idx[p] < 0;
-  const uint64_t umask = __ballot(unc);
-  int my_kid = 0;
-  if (!__syncthreads_or(unc)) return;
-  s_pg[w][lane] = unc ? a.grad_soft[p] : (T)0;
-  s_ps[w][lane] = unc ? a.soft_in[p] : (T)0;
-
-  auto stage = [&](int k, int64_t fi) {
-    soft_stage(fs, s_geo, k, fi);
-#pragma unroll
-    for (int q = 0; q < 6; ++q) s_acc[q][k] = (T)0;
-  };
-  auto flush = [&](int npairs) {  // pass B: gradient terms, summed per face in LDS
-    wave_lds_sync();
-    for (int e = lane; e < npairs; e += kWave) {
-      const int pr = P.pair[w][e];
-      const int q = pr >> 8, k = pr & 255;
-      const int qx = t.WX0 + (q & 7), qy = t.WY0 + (q >> 3);
-      const T xq = (T)px_cx(M, W, qx), yq = (T)px_cy(M, H, qy);
-      T v[6];
-#pragma unroll
-      for (int c = 0; c < 6; ++c) v[c] = s_geo[c][k];
-      int et;
-      T pb;
-      soft_face_dist<T>(xq, yq, v, M, a.sigmainv, et, pb);
-      T g[6] = {0, 0, 0, 0, 0, 0};
-      soft_bwd_terms<T>(xq, yq, v, et, pb, s_pg[w][q], s_ps[w][q], a.sigmainv, M, g);
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-        if (g[c] != (T)0) atomicAdd(&s_acc[c][k], g[c]);
-    }
-    wave_lds_sync();
-    P.n[w][lane] = 0;
-    wave_lds_sync();
-  };
-  auto round = [&](int nsub, int cnt) {
-    if (umask && nsub > 0) {
-      const SubSpans ss = load_subspans(L, nsub);
-      soft_pass_a(ss, nsub, P, umask, K, t, my_kid, flush);
-    }
-    __syncthreads();
-    // one atomic per (face, coordinate) with a nonzero tile sum; lanes walk a face's 6
-    // coordinates contiguously (24 contiguous bytes per face).
-    for (int idx = tid; idx < cnt * 6; idx += kBlock) {
-      const int k = idx / 6, c = idx - k * 6;
-      const T v = s_acc[c][k];
-      if (v != (T)0) atomicAdd(a.grad_fvi + (lo + L.f[k]) * 6 + c, v);
-    }
-  };
-  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
 }
 
 template <typename T>
@@ -412,15 +176,13 @@ int soft_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool build_bins,
   a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
   a.bb.cull = nullptr;
   a.fs.dbg = debug_flags();
+  a.fs.tbuf = debug_tile_buffer();
   if (build_bins) {
     hipError_t e = bin_faces<T>(fs, a.bb, stream);
     if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   }
   const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
-  if (a.grad_fvi) {
-    ProfScope prof(K_SOFT_BWD_TILE, stream);
-    hipLaunchKernelGGL(kd_soft_bwd_tile<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-  } else {
+  {
     ProfScope prof(K_SOFT_FWD, stream);
     if (a.prob)
       hipLaunchKernelGGL((kd_soft_fwd<T, true>), dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
@@ -508,15 +270,16 @@ static int soft_fwd_raw(int B, int H, int W, int64_t F, int K, const T *fvi, con
 template <typename T>
 static int soft_fwd_fused(int B, int H, int W, int64_t F, int K, const T *fvi, double M,
                           double boxlen, const int64_t *fidx, float sigmainv, T *soft, T *prob,
-                          int64_t *cidx, uint8_t *ctype, int32_t *last, void *ws, size_t wsb,
-                          void *stream) {
+                          int64_t *cidx, uint8_t *ctype, int32_t *last, int want_grad, void *ws,
+                          size_t wsb, void *stream) {
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0, "negative size");
-  KD_CHECK_ARG(K >= 1, "knum must be >= 1");
+  KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
   KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
   KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
   KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
   KD_CHECK_ARG((prob && cidx && ctype) || (!prob && !cidx && !ctype),
                "close lists must be all set or all NULL");
+  KD_CHECK_ARG(soft, "soft_mask is NULL");
   SoftArgs<T> a{};
   a.fs = fused_faceset<T>(B, H, W, F, fvi, M, boxlen);
   a.face_idx = fidx;
@@ -527,7 +290,7 @@ static int soft_fwd_fused(int B, int H, int W, int64_t F, int K, const T *fvi, d
   a.cidx = cidx;
   a.ctype = ctype;
   a.last = last;
-  return soft_forward<T>(a, ws, wsb, true, (hipStream_t)stream);
+  return soft_pairs_forward<T>(a, ws, wsb, want_grad != 0, true, (hipStream_t)stream);
 }
 
 template <typename T>
@@ -536,9 +299,10 @@ static int soft_bwd_binned(int B, int H, int W, int64_t F, int K, const T *gs, c
                            float sigmainv, T *gfvi, void *ws, size_t wsb, int bins_ready,
                            void *stream) {
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0, "negative size");
-  KD_CHECK_ARG(K >= 1, "knum must be >= 1");
+  KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
   KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
   KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
+  KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
   const int64_t nf = (int64_t)B * F;
   if (nf > 0) {
     hipError_t e = hipMemsetAsync(gfvi, 0, sizeof(T) * nf * 6, (hipStream_t)stream);
@@ -552,7 +316,11 @@ static int soft_bwd_binned(int B, int H, int W, int64_t F, int K, const T *gs, c
   a.grad_soft = gs;
   a.soft_in = soft;
   a.grad_fvi = gfvi;
-  return soft_forward<T>(a, ws, wsb, bins_ready == 0, (hipStream_t)stream);
+  if (!bins_ready) {  // no forward workspace: rebuild the records and their coefficients
+    const int rc = soft_pairs_forward<T>(a, ws, wsb, true, false, (hipStream_t)stream);
+    if (rc != KD_OK) return rc;
+  }
+  return soft_pairs_backward<T>(a, ws, wsb, (hipStream_t)stream);
 }
 
 extern "C" {
@@ -572,21 +340,27 @@ int kd_dibr_soft_mask_forward_f64(int B, int H, int W, int64_t F, int K, const d
                               ctype, ws, wsb, stream);
 }
 
+size_t kd_soft_mask_workspace_size(int B, int H, int W, int64_t F, int knum,
+                                   int double_precision) {
+  if (B < 0 || H < 0 || W < 0 || F < 0 || knum < 1) return 0;
+  return soft_pair_workspace_bytes(B, H, W, (int64_t)B * F, F, knum, double_precision ? 8 : 4);
+}
+
 int kd_dibr_soft_mask_forward_fused_f32(int B, int H, int W, int64_t F, int K, const float *fvi,
                                         double M, double boxlen, const int64_t *fidx,
                                         float sigmainv, float *soft, float *prob, int64_t *cidx,
-                                        uint8_t *ctype, int32_t *last, void *ws, size_t wsb,
-                                        void *stream) {
+                                        uint8_t *ctype, int32_t *last, int want_grad, void *ws,
+                                        size_t wsb, void *stream) {
   return soft_fwd_fused<float>(B, H, W, F, K, fvi, M, boxlen, fidx, sigmainv, soft, prob, cidx,
-                               ctype, last, ws, wsb, stream);
+                               ctype, last, want_grad, ws, wsb, stream);
 }
 int kd_dibr_soft_mask_forward_fused_f64(int B, int H, int W, int64_t F, int K, const double *fvi,
                                         double M, double boxlen, const int64_t *fidx,
                                         float sigmainv, double *soft, double *prob,
-                                        int64_t *cidx, uint8_t *ctype, int32_t *last, void *ws,
-                                        size_t wsb, void *stream) {
+                                        int64_t *cidx, uint8_t *ctype, int32_t *last,
+                                        int want_grad, void *ws, size_t wsb, void *stream) {
   return soft_fwd_fused<double>(B, H, W, F, K, fvi, M, boxlen, fidx, sigmainv, soft, prob, cidx,
-                                ctype, last, ws, wsb, stream);
+                                ctype, last, want_grad, ws, wsb, stream);
 }
 
 int kd_dibr_soft_mask_backward_f32(int B, int H, int W, int64_t F, int K, const float *gs,

@@ -1,0 +1,497 @@
+// kd_softpair.hip -- the autograd path of dibr_soft_mask (dibr.py:27-73) as a pair pipeline.
+//
+// The reference's per-pixel loop (dibr_soft_mask_cuda.cu:27-184) spends its time in two places:
+// finding each uncovered pixel's first K close faces, and the distance / probability math of
+// those (pixel, face) pairs.  Only pixels near the silhouette have pairs (~8 % of the pixels,
+// ~16 pairs each at C3), so a tile kernel that also does the math is badly unbalanced: a
+// handful of silhouette tiles carry all of it.  Here the two parts are separate launches:
+//   kd_soft_pairs      one workgroup per 16x16 tile: walks the tile's ordered bin (kd_tile.hpp),
+//                      pass A (kd_soft.hpp) picks each uncovered pixel's first K close faces by
+//                      face index, and the (pixel, slot, face) records go to the tile's region.
+//                      It stops as soon as every uncovered pixel of the tile holds K faces.
+//   kd_soft_pair_math  flat over the records (several workgroups per tile): distance type and
+//                      probability with the reference arithmetic (bit-identical), stored by
+//                      (pixel, slot); with gradients requested also the pair's backward
+//                      coefficients (below); optionally the reference's close-face lists.
+//   kd_soft_reduce     per pixel: soft = 1 - prod(1 - p) in slot order with the reference's
+//                      double promotion (dibr_soft_mask_cuda.cu:174-181); 1 on covered pixels.
+//   kd_soft_bwd_pairs  the backward: per tile, every record adds s_p * h_j to its face's corner
+//                      sums in LDS, one float atomic per (tile, face, coordinate) flushes them.
+// Backward factorisation: the reference's per-pair gradient (dibr_soft_mask_cuda.cu:281-348) is
+//   dLdz * f_j / M  with  dLdz = -sigmainv * dLdp * (1 - soft) / (1 - p + 1e-7) * p
+// and f_j the geometric factors of the distance type (2(x1 - x0) ... for a vertex, the four
+// dzdA / dzdB / dzdC combinations for an edge).  Only s_p = -sigmainv * dLdp * (1 - soft)
+// depends on the incoming gradient, so the forward stores h_j = p / (1 - p + 1e-7) * f_j / M per
+// pair and the backward is a multiply-add per coordinate (same value up to rounding order, like
+// the reference's own atomics).  Nothing is recomputed and the close lists are never needed.
+#include "kd_soft.hpp"
+
+namespace kd {
+
+constexpr unsigned kPersistentBlocks = 2048;  // 8 workgroups per CU for the item loops
+
+size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize) {
+  const int64_t ntiles = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+  const int64_t tiles = (int64_t)B * ntiles, cap = (int64_t)kBlock * K, P = (int64_t)B * H * W;
+  size_t s = bin_workspace_bytes(B, H, W, N, F);
+  s += align_up(sizeof(SoftPairRec) * (size_t)(tiles * cap));
+  s += align_up((size_t)esize * 4 * (size_t)(tiles * cap));
+  s += align_up((size_t)esize * (size_t)(P * K));
+  s += align_up(sizeof(int32_t) * (size_t)P);
+  s += align_up(sizeof(int32_t) * 2 * (size_t)tiles);
+  s += align_up(sizeof(int2) * (size_t)(tiles * ((cap + kBlock - 1) / kBlock)));
+  s += align_up(sizeof(int32_t) * (size_t)tiles);
+  s += align_up(sizeof(int32_t) * 2);
+  return s;
+}
+
+template <typename T>
+SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K) {
+  SoftPairBuf<T> pb;
+  pb.ntx = (W + kTile - 1) / kTile;
+  pb.ntiles = (int64_t)pb.ntx * ((H + kTile - 1) / kTile);
+  pb.cap = (int64_t)kBlock * K;
+  const int64_t tiles = (int64_t)B * pb.ntiles, P = (int64_t)B * H * W;
+  char *base = (char *)ws;
+  pb.rec = (SoftPairRec *)(base + off);
+  off += align_up(sizeof(SoftPairRec) * (size_t)(tiles * pb.cap));
+  pb.coef = (SoftCoef<T> *)(base + off);
+  off += align_up(sizeof(T) * 4 * (size_t)(tiles * pb.cap));
+  pb.sprob = (T *)(base + off);
+  off += align_up(sizeof(T) * (size_t)(P * K));
+  pb.npix = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * (size_t)P);
+  pb.ntile = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * 2 * (size_t)tiles);
+  pb.items = (int2 *)(base + off);
+  off += align_up(sizeof(int2) * (size_t)(tiles * ((pb.cap + kBlock - 1) / kBlock)));
+  pb.tiles = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * (size_t)tiles);
+  pb.counters = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * 2);
+  return pb;
+}
+
+// pixel of tile-local thread index q (kd_tile.hpp tile_geom layout)
+__device__ __forceinline__ void tile_pixel(int tx, int ty, int q, int &px, int &py) {
+  const int w = q >> 6, l = q & 63;
+  px = tx * kTile + (w & 1) * 8 + (l & 7);
+  py = ty * kTile + (w >> 1) * 8 + (l >> 3);
+}
+
+// ------------------------------------------------------------------------------------------
+// pass A: (pixel, slot, face) records per tile
+// ------------------------------------------------------------------------------------------
+// Lowest `need` set bits of m (need < popc(m)).
+__device__ __forceinline__ uint64_t lowest_bits(uint64_t m, int need) {
+  uint64_t sel = 0ull;
+  for (int i = 0; i < need; ++i) {
+    const uint64_t lsb = m & (~m + 1ull);
+    sel |= lsb;
+    m ^= lsb;
+  }
+  return sel;
+}
+
+// One 64-face chunk of a wave's sub-list (lane j = chunk entry j): every uncovered pixel lane
+// takes the first K - kid faces of the chunk whose exact enlarged span holds its centre
+// (ascending face index = ascending entry, dibr_soft_mask_cuda.cu:95 and :165-171), then the
+// selections are transposed so that each face lane writes its records, face-major.
+__device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
+                                                   int K, const TileGeom &t, int64_t lo,
+                                                   int lbase, int &my_kid, uint64_t *s_sel,
+                                                   unsigned short *s_kb, int *s_nrec,
+                                                   SoftPairRec *rec) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int qx = lane & 7, qy = lane >> 3;
+  const int j = c * kWave + lane;
+  const bool has = j < nsub;
+  const int k = has ? L.sub[w][j] : 0;
+  const Span sp = has ? L.span[k] : Span{1, -1, 1, -1};
+  const int x0 = sp.x0 - t.WX0, x1 = sp.x1 - t.WX0, y0 = sp.y0 - t.WY0, y1 = sp.y1 - t.WY0;
+  uint64_t mc = 0ull, mr = 0ull;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t bc = __ballot(x0 <= i && i <= x1);
+    const uint64_t br = __ballot(y0 <= i && i <= y1);
+    mc = (qx == i) ? bc : mc;
+    mr = (qy == i) ? br : mr;
+  }
+  uint64_t sel = (unc && my_kid < K) ? (mc & mr) : 0ull;
+  const int need = K - my_kid;
+  if (__popcll(sel) > need) sel = lowest_bits(sel, need);
+  s_sel[lane] = sel;
+  s_kb[lane] = (unsigned short)my_kid;
+  my_kid += __popcll(sel);
+  wave_lds_sync();
+  // face lanes: pixels that selected this face
+  uint64_t pm = wave_transpose64(sel);
+  const int cnt = __popcll(pm);
+  const int incl = wave_incl_scan(cnt);
+  const int tot = __builtin_amdgcn_readlane(incl, 63);
+  if (tot == 0) return;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(s_nrec, tot);
+  base = __builtin_amdgcn_readfirstlane(base);
+  int pos = base + incl - cnt;
+  const uint64_t below = (1ull << lane) - 1ull;
+  const int32_t row = (int32_t)(lo + L.f[k]);
+  const uint32_t lid = (uint32_t)(lbase + k);
+  while (pm) {
+    const int q = __builtin_ctzll(pm);
+    pm &= pm - 1ull;
+    SoftPairRec r;
+    r.row = row;
+    r.lid = lid;
+    r.slot = (uint16_t)(s_kb[q] + __popcll(s_sel[q] & below));
+    r.q = (uint8_t)(w * kWave + q);
+    r.type = 0;
+    rec[pos++] = r;
+  }
+  wave_lds_sync();
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  TileClock clk(a.fs.tbuf, 1);
+  __shared__ TileLists L;
+  __shared__ uint64_t s_sel[4][kWave];
+  __shared__ unsigned short s_kb[4][kWave];
+  __shared__ int s_nrec;
+
+  const FaceSet<T> &fs = a.fs;
+  const int H = fs.H, W = fs.W, K = a.K;
+  const int b = blockIdx.y;
+  const int tid = threadIdx.x, w = tid >> 6;
+  int64_t lo, hi;
+  view_range(fs, b, lo, hi);
+  const TileGeom t = tile_geom(H, W);
+  const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
+  const bool unc = t.inimg && a.face_idx[p] < 0;
+  const bool wave_unc = __ballot(unc) != 0ull;
+  const int64_t tile = (int64_t)b * pb.ntiles + blockIdx.x;
+  SoftPairRec *rec = pb.rec + tile * pb.cap;
+  int my_kid = 0, lbase = 0;
+  if (tid == 0) s_nrec = 0;
+
+  if (__syncthreads_or(unc)) {
+    auto stage = [&](int, int64_t) {};  // pass A needs the spans only
+    auto round = [&](int nsub, int cnt) {
+      if (wave_unc && !(fs.dbg & 1))
+        for (int c = 0; c * kWave < nsub; ++c)
+          soft_chunk_records(L, nsub, c, unc, K, t, lo, lbase, my_kid, s_sel[w], s_kb[w],
+                             &s_nrec, rec);
+      lbase += cnt;
+    };
+    // once every uncovered pixel holds K close faces, later faces cannot enter
+    auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
+    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg, done);
+  }
+  if (t.inimg) pb.npix[p] = unc ? my_kid : 0;
+  __syncthreads();
+  const int n = s_nrec;
+  if (tid == 0) {
+    pb.ntile[2 * tile] = n;
+    pb.ntile[2 * tile + 1] = lbase;
+  }
+  if (n > 0) {  // work items of the math and backward passes
+    const int nch = (n + kBlock - 1) / kBlock;
+    __shared__ int s_base;
+    if (tid == 0) {
+      s_base = atomicAdd(&pb.counters[0], nch);
+      pb.tiles[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
+    }
+    __syncthreads();
+    for (int c = tid; c < nch; c += kBlock) pb.items[s_base + c] = make_int2((int)tile, c);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// per-pair math
+// ------------------------------------------------------------------------------------------
+// Backward coefficients h_j of one pair (see the file comment); the geometric factors are the
+// reference's expressions (dibr_soft_mask_cuda.cu:288-343) in T.
+template <typename T>
+__device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et, T prob, float M,
+                                               T h[4]) {
+  const double s = (double)prob / (1.0 - (double)prob + KD_SOFT_EPS) / (double)M;
+  if (et >= 3) {
+    const int ps = (et - 3) * 2;
+    h[0] = (T)(s * (double)((T)2 * (v[ps] - x0)));
+    h[1] = (T)(s * (double)((T)2 * (v[ps + 1] - y0)));
+    h[2] = (T)0;
+    h[3] = (T)0;
+  } else {
+    const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
+    const T x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
+    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+    const T up = A * x0 + Bc * y0 + C;
+    const T down = A * A + Bc * Bc;
+    const double dd = (double)down + KD_SOFT_EPS;
+    const T dissquare = (T)((double)(up * up) / dd);
+    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) / dd);
+    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) / dd);
+    const T dzdC = (T)((double)((T)2 * up) / dd);
+    h[0] = (T)(s * (double)(dzdB - y2 * dzdC));
+    h[1] = (T)(s * (double)(x2 * dzdC - dzdA));
+    h[2] = (T)(s * (double)(y1 * dzdC - dzdB));
+    h[3] = (T)(s * (double)(dzdA - x1 * dzdC));
+  }
+}
+
+template <typename T, bool GRAD, bool LISTS>
+__global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  const FaceSet<T> &fs = a.fs;
+  const int H = fs.H, W = fs.W, K = a.K;
+  const float M = fs.M;
+  const int nitems = pb.counters[0];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {  // (tile, 256-record chunk) items
+    const int2 item = pb.items[it];
+    const int64_t tile = item.x;
+    const int n = pb.ntile[2 * tile];
+    const int i = item.y * kBlock + threadIdx.x;
+    if (i >= n) continue;
+    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+    const int tx = tl % pb.ntx, ty = tl / pb.ntx;
+    int64_t lo, hi;
+    view_range(fs, b, lo, hi);
+    SoftPairRec *rp = pb.rec + tile * pb.cap + i;
+    const SoftPairRec r = *rp;
+    int px, py;
+    tile_pixel(tx, ty, r.q, px, py);
+    const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
+    T v[6];
+    load_corners(fs, (int64_t)r.row, v);
+    int et = 0;
+    T prob = (T)0;
+    if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+    const int64_t gp = ((int64_t)b * H + py) * W + px;
+    const int64_t o = gp * K + r.slot;
+    pb.sprob[o] = prob;
+    rp->type = (uint8_t)et;
+    if (LISTS) {
+      a.prob[o] = prob;
+      a.cidx[o] = (int64_t)r.row - lo;
+      a.ctype[o] = (uint8_t)(et + 1);
+    }
+    if (a.last && r.slot == K - 1) a.last[gp] = (int32_t)((int64_t)r.row - lo);
+    if (GRAD) {
+      SoftCoef<T> c;
+      soft_pair_coef<T>(x0, y0, v, et, prob, M, c.h);
+      pb.coef[tile * pb.cap + i] = c;
+    }
+  }
+}
+
+template <typename T, bool LISTS>
+__global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  const int K = a.K;
+  const int64_t total = (int64_t)a.fs.B * a.fs.H * a.fs.W;
+  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total;
+       p += (int64_t)gridDim.x * kBlock) {
+    const bool covered = a.face_idx[p] >= 0;
+    const int n = covered ? 0 : pb.npix[p];
+    T prod = (T)1.0;
+    const T *sp = pb.sprob + p * K;
+    for (int s0 = 0; s0 < n; s0 += 8) {  // 8 loads in flight, then the ordered product
+      T v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = s0 + j < n ? sp[s0 + j] : (T)0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)  // dibr_soft_mask_cuda.cu:174-178, slot order
+        if (s0 + j < n) prod = (T)((double)prod * (1.0 - (double)v[j]));
+    }
+    a.soft[p] = covered ? (T)1.0 : (T)(1.0 - (double)prod);  // :69, :181
+    if (a.last && n < K) a.last[p] = -1;
+    if (LISTS)  // -1 / 0 / 0 padding (dibr_soft_mask.cpp:86-97 pre-fill)
+      for (int s = n; s < K; ++s) {
+        a.prob[p * K + s] = (T)0;
+        a.cidx[p * K + s] = -1;
+        a.ctype[p * K + s] = 0;
+      }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// backward: per tile, per face sums in LDS
+// ------------------------------------------------------------------------------------------
+// Adds one pair's contribution s_p * h_j to the register sums g[6] of its face's corners.
+template <typename T>
+__device__ __forceinline__ void soft_add_pair(T g[6], int et, double sp, const SoftCoef<T> &c) {
+  const int ps = et >= 3 ? (et - 3) * 2 : et * 2;
+  const int ps2 = et >= 3 ? -8 : ((et + 1) % 3) * 2;  // vertex types touch one corner only
+  const T v0 = (T)(sp * (double)c.h[0]), v1 = (T)(sp * (double)c.h[1]);
+  const T v2 = (T)(sp * (double)c.h[2]), v3 = (T)(sp * (double)c.h[3]);
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+    g[i] += i == ps ? v0 : i == ps + 1 ? v1 : i == ps2 ? v2 : i == ps2 + 1 ? v3 : (T)0;
+}
+
+// The records of a tile are face-major runs (kd_soft_pairs), so a thread walking U consecutive
+// records sums most of them in registers and touches LDS once per run.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_soft_bwd_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  constexpr int R = 1024 * 4 / sizeof(T);  // faces per LDS pass
+  constexpr int U = 8;                     // consecutive records per thread
+  __shared__ T s_acc[6][R];
+  __shared__ int s_row[R];
+  __shared__ double s_sp[kBlock];  // -sigmainv * grad * (1 - soft) of the tile's pixels
+  const int ntl = pb.counters[1];
+  for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) {  // tiles with records
+  const int64_t tile = pb.tiles[ti];
+  const int n = pb.ntile[2 * tile], nf = pb.ntile[2 * tile + 1];
+  const FaceSet<T> &fs = a.fs;
+  const int H = fs.H, W = fs.W;
+  const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+  const int tx = tl % pb.ntx, ty = tl / pb.ntx;
+  const int tid = threadIdx.x;
+  __syncthreads();  // the previous tile's LDS is done
+  {
+    int px, py;
+    tile_pixel(tx, ty, tid, px, py);
+    double sp = 0.0;
+    if (px < W && py < H) {
+      const int64_t gp = ((int64_t)b * H + py) * W + px;
+      sp = -(double)a.sigmainv * (double)a.grad_soft[gp] * (1.0 - (double)a.soft_in[gp]);
+    }
+    s_sp[tid] = sp;
+  }
+  const SoftPairRec *rec = pb.rec + tile * pb.cap;
+  const SoftCoef<T> *coef = pb.coef + tile * pb.cap;
+  for (int r0 = 0; r0 < nf; r0 += R) {
+    const int nr = min(R, nf - r0);
+    for (int k = tid; k < nr; k += kBlock) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) s_acc[c][k] = (T)0;
+      s_row[k] = -1;
+    }
+    __syncthreads();
+    auto flush_run = [&](int li, const T g[6]) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        if (g[c] != (T)0) atomicAdd(&s_acc[c][li], g[c]);
+    };
+    for (int s0 = tid * U; s0 < n && !(fs.dbg & 256); s0 += kBlock * U) {
+      SoftPairRec r[U];
+      SoftCoef<T> c[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)  // issue all loads first
+        if (s0 + u < n) {
+          r[u] = rec[s0 + u];
+          c[u] = coef[s0 + u];
+        }
+      T g[6] = {0, 0, 0, 0, 0, 0};
+      int cur = -1;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (s0 + u >= n) break;
+        const int li = (int)r[u].lid - r0;
+        if (li < 0 || li >= nr) continue;
+        if (li != cur) {
+          if (cur >= 0) flush_run(cur, g);
+#pragma unroll
+          for (int q = 0; q < 6; ++q) g[q] = (T)0;
+          cur = li;
+          s_row[li] = r[u].row;
+        }
+        soft_add_pair<T>(g, r[u].type, s_sp[r[u].q], c[u]);
+      }
+      if (cur >= 0) flush_run(cur, g);
+    }
+    __syncthreads();
+    // one atomic per (face, coordinate); a face's 6 coordinates on adjacent lanes (24 B)
+    for (int idx = tid; idx < nr * 6 && !(fs.dbg & 128); idx += kBlock) {
+      const int k = idx / 6, cc = idx - k * 6;
+      const T v = s_acc[cc][k];
+      if (v != (T)0 && s_row[k] >= 0) atomicAdd(a.grad_fvi + (int64_t)s_row[k] * 6 + cc, v);
+    }
+    __syncthreads();
+  }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host launchers
+// ------------------------------------------------------------------------------------------
+template <typename T>
+int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, bool reduce,
+                       hipStream_t stream) {
+  const FaceSet<T> &fs = a.fs;
+  const size_t need = soft_pair_workspace_bytes(fs.B, fs.H, fs.W, fs.N, fs.F, a.K, sizeof(T));
+  if (ws_bytes < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", ws_bytes, need);
+  if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
+  size_t off = 0;
+  a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
+  a.bb.cull = nullptr;
+  SoftPairBuf<T> pb = soft_pair_carve<T>(ws, off, fs.B, fs.H, fs.W, a.K);
+  a.bb.clear = pb.counters;
+  a.bb.n_clear = 2;
+  a.fs.dbg = debug_flags();
+  a.fs.tbuf = debug_tile_buffer();
+  hipError_t e = bin_faces<T>(fs, a.bb, stream);
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
+  {
+    ProfScope prof(K_SOFT_PAIRS, stream);
+    hipLaunchKernelGGL(kd_soft_pairs<T>, dim3((unsigned)pb.ntiles, fs.B), dim3(kBlock), 0, stream,
+                       a, pb);
+  }
+  {
+    ProfScope prof(K_SOFT_MATH, stream);
+    const dim3 grid(kPersistentBlocks);
+    const bool lists = a.prob != nullptr;
+    if (grad && lists)
+      hipLaunchKernelGGL((kd_soft_pair_math<T, true, true>), grid, dim3(kBlock), 0, stream, a, pb);
+    else if (grad)
+      hipLaunchKernelGGL((kd_soft_pair_math<T, true, false>), grid, dim3(kBlock), 0, stream, a, pb);
+    else if (lists)
+      hipLaunchKernelGGL((kd_soft_pair_math<T, false, true>), grid, dim3(kBlock), 0, stream, a, pb);
+    else
+      hipLaunchKernelGGL((kd_soft_pair_math<T, false, false>), grid, dim3(kBlock), 0, stream, a,
+                         pb);
+  }
+  if (reduce) {
+    ProfScope prof(K_SOFT_REDUCE, stream);
+    const int64_t total = (int64_t)fs.B * fs.H * fs.W;
+    const unsigned blocks = (unsigned)std::min<int64_t>((total + kBlock - 1) / kBlock, 65536);
+    if (a.prob)
+      hipLaunchKernelGGL((kd_soft_reduce<T, true>), dim3(blocks), dim3(kBlock), 0, stream, a, pb);
+    else
+      hipLaunchKernelGGL((kd_soft_reduce<T, false>), dim3(blocks), dim3(kBlock), 0, stream, a,
+                         pb);
+  }
+  e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template <typename T>
+int soft_pairs_backward(SoftArgs<T> &a, void *ws, size_t ws_bytes, hipStream_t stream) {
+  const FaceSet<T> &fs = a.fs;
+  const size_t need = soft_pair_workspace_bytes(fs.B, fs.H, fs.W, fs.N, fs.F, a.K, sizeof(T));
+  if (ws_bytes < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", ws_bytes, need);
+  if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
+  size_t off = 0;
+  a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
+  SoftPairBuf<T> pb = soft_pair_carve<T>(ws, off, fs.B, fs.H, fs.W, a.K);
+  a.fs.dbg = debug_flags();
+  a.fs.tbuf = debug_tile_buffer();
+  {
+    ProfScope prof(K_SOFT_BWD_PAIRS, stream);
+    hipLaunchKernelGGL(kd_soft_bwd_pairs<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a,
+                       pb);
+  }
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template int soft_pairs_forward<float>(SoftArgs<float> &, void *, size_t, bool, bool,
+                                       hipStream_t);
+template int soft_pairs_forward<double>(SoftArgs<double> &, void *, size_t, bool, bool,
+                                        hipStream_t);
+template int soft_pairs_backward<float>(SoftArgs<float> &, void *, size_t, hipStream_t);
+template int soft_pairs_backward<double>(SoftArgs<double> &, void *, size_t, hipStream_t);
+
+}  // namespace kd

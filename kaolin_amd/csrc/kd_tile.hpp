@@ -7,6 +7,8 @@
 // 8x8 sub-tile, and calls round(nsub, cnt) once per batch of at most kCap faces.  Across batches
 // the faces keep ascending order, so a caller that processes batches in sequence sees the faces
 // in exactly the order the reference loop does (minus faces whose box misses the pixel).
+// A caller whose result depends only on a prefix of the faces (the soft mask's first K) stops
+// the walk early through `done`.
 //
 // The box test itself is done on the exact integer pixel spans (kd_common.hpp make_span): pixel
 // (x, y) passes the reference's half-open float box test iff x0 <= x <= x1 and y0 <= y <= y1.
@@ -18,7 +20,8 @@
 
 namespace kd {
 
-constexpr int kCap = 256;  // faces per batch (LDS list)
+constexpr int kCap = 256;     // faces per batch (LDS list)
+constexpr int kPrefetch = 4;  // bin chunks loaded ahead by tile_rounds
 
 struct TileGeom {
   int X0, X1, Y0, Y1;      // tile pixel rect (inclusive)
@@ -93,52 +96,72 @@ __device__ __forceinline__ SubSpans load_subspans(const TileLists &L, int nsub) 
   return r;
 }
 
-template <typename Stage, typename Round>
+struct NeverDone {
+  __device__ bool operator()() const { return false; }
+};
+
+// `done()` (evaluated by every thread; must return a workgroup-uniform value, e.g. through
+// __syncthreads_and) lets a caller stop the walk once later faces cannot matter any more.
+template <typename Stage, typename Round, typename Done = NeverDone>
 __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, int64_t N, int b,
                                             int64_t lo, const TileGeom &t, Stage stage,
-                                            Round round, int dbg = 0) {
+                                            Round round, int dbg = 0, Done done = Done()) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 / g.ct) * g.nctx + (t.X0 / g.ct);
   const int n = bb.totals[(int64_t)b * g.nct() + ct];
   const int *bin = bb.bins + (int64_t)ct * N + lo;
   int cnt = 0;
-  for (int base = 0; base < n; base += kBlock) {
-    const int e = base + tid;
-    int f = 0;
-    bool ov = false;
-    Span sp;
-    if (e < n) {
-      f = bin[e];
-      sp = bb.spans[lo + f];
-      ov = span_overlaps(sp, t.X0, t.X1, t.Y0, t.Y1);
+  // kPrefetch chunks of bin entries and their spans are loaded up front (two dependent
+  // round trips per kPrefetch * 256 entries instead of per 256)
+  for (int base0 = 0; base0 < n; base0 += kBlock * kPrefetch) {
+    int fr[kPrefetch];
+    Span spr[kPrefetch];
+#pragma unroll
+    for (int u = 0; u < kPrefetch; ++u) {
+      const int e = base0 + u * kBlock + tid;
+      fr[u] = e < n ? bin[e] : 0;
     }
-    int tot;
-    const int pos = wg_compact(ov, L.cnt, tot);
-    // a batch holds at most kCap faces: flush first if this chunk would overflow it
-    if (cnt + tot > kCap) {
-      __syncthreads();
-      if (!(dbg & 2))
-        for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
-      int nsub = 0;
-      for (int k0 = 0; k0 < cnt; k0 += kWave) {
-        const int k = k0 + lane;
-        const bool ok =
-            t.wave_live && k < cnt && span_overlaps(L.span[k], t.WX0, t.WX1, t.WY0, t.WY1);
-        const uint64_t m = __ballot(ok);
-        if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
-        nsub += __popcll(m);
+#pragma unroll
+    for (int u = 0; u < kPrefetch; ++u) {
+      const int e = base0 + u * kBlock + tid;
+      if (e < n) spr[u] = bb.spans[lo + fr[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < kPrefetch; ++u) {
+      if (base0 + u * kBlock >= n) break;
+      const int e = base0 + u * kBlock + tid;
+      const int f = fr[u];
+      const Span sp = spr[u];
+      const bool ov = e < n && span_overlaps(sp, t.X0, t.X1, t.Y0, t.Y1);
+      int tot;
+      const int pos = wg_compact(ov, L.cnt, tot);
+      // a batch holds at most kCap faces: flush first if this chunk would overflow it
+      if (cnt + tot > kCap) {
+        __syncthreads();
+        if (!(dbg & 2))
+          for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
+        int nsub = 0;
+        for (int k0 = 0; k0 < cnt; k0 += kWave) {
+          const int k = k0 + lane;
+          const bool ok =
+              t.wave_live && k < cnt && span_overlaps(L.span[k], t.WX0, t.WX1, t.WY0, t.WY1);
+          const uint64_t m = __ballot(ok);
+          if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
+          nsub += __popcll(m);
+        }
+        __syncthreads();
+        if (!(dbg & 4)) round(nsub, cnt);
+        __syncthreads();
+        cnt = 0;
+        if (done()) return;
       }
-      __syncthreads();
-      if (!(dbg & 4)) round(nsub, cnt);
-      __syncthreads();
-      cnt = 0;
+      if (ov) {
+        L.f[cnt + pos] = f;
+        L.span[cnt + pos] = sp;
+      }
+      cnt += tot;
     }
-    if (ov) {
-      L.f[cnt + pos] = f;
-      L.span[cnt + pos] = sp;
-    }
-    cnt += tot;
   }
   if (cnt > 0) {
     __syncthreads();
@@ -176,6 +199,24 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
   x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, false);  // row_shr:8
   x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
   x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+  return x;
+}
+
+// 64x64 bit-matrix transpose across a wave: lane l bit j -> lane j bit l (block swaps).
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t masks[6] = {0x00000000ffffffffull, 0x0000ffff0000ffffull,
+                             0x00ff00ff00ff00ffull, 0x0f0f0f0f0f0f0f0full,
+                             0x3333333333333333ull, 0x5555555555555555ull};
+#pragma unroll
+  for (int st = 0; st < 6; ++st) {
+    const int sh = 32 >> st;
+    const uint64_t mlo = masks[st];
+    const uint32_t ylo = (uint32_t)__shfl_xor((int)(uint32_t)x, sh);
+    const uint32_t yhi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), sh);
+    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+    x = (lane & sh) ? ((x & ~mlo) | ((y & ~mlo) >> sh)) : ((x & mlo) | ((y & mlo) << sh));
+  }
   return x;
 }
 

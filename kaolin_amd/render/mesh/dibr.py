@@ -4,10 +4,11 @@ The reference's ``DibrSoftMaskCuda`` (dibr.py:27-73) scales the coordinates, bui
 boxes, runs the per-pixel all-faces scan and saves the (B, H, W, K) close-face lists
 (prob / int64 idx / uint8 type, 13*K bytes per pixel) for its backward.  Here the scaling and
 boxes are computed in the kernel, the scan runs over ordered tile bins, and by default the lists
-are NOT materialised: the backward re-derives every uncovered pixel's first-K close faces over the
-same bins (kept from the forward) and recomputes the distance types / probabilities
-bit-identically.  Set ``SAVE_CLOSE_LISTS = True`` to materialise the lists and use the
-reference-structured atomic backward instead (same results up to float-sum order).
+are NOT materialised: the forward keeps, per (pixel, close face) pair, the face and the pair's
+backward coefficients in its workspace (kd_softpair.hip), and the backward multiplies them by the
+incoming gradient and sums them per face and tile.  Set ``SAVE_CLOSE_LISTS = True`` to
+materialise the lists and use the reference-structured atomic backward instead (same results up
+to float-sum order).
 """
 import torch
 from torch.autograd import Function
@@ -30,9 +31,10 @@ class DibrSoftMaskCuda(Function):
         face_vertices_image = face_vertices_image.contiguous()
         selected_face_idx = selected_face_idx.contiguous()
         lists = SAVE_CLOSE_LISTS
+        want_grad = face_vertices_image.requires_grad and not lists
         soft_mask, workspace, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
             face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier,
-            with_lists=lists)
+            with_lists=lists, want_grad=want_grad)
         ctx.multiplier = multiplier
         ctx.sigmainv = sigmainv
         ctx.boxlen = boxlen

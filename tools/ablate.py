@@ -11,6 +11,8 @@ from kaolin_amd.render.mesh import dibr_rasterization  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else 'c3'
 n_lon, n_lat, H, W, B, elev = bench.CONFIGS[cfg]
+if len(sys.argv) > 3:
+    B = int(sys.argv[3])
 dev = torch.device('cuda')
 v = workloads.sphere_views(n_lon, n_lat, H, W, B, dev, elevation=elev)
 fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['normals_z']

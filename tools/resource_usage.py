@@ -5,7 +5,7 @@ import subprocess
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'kaolin_amd',
                     'csrc')
-for f in ('kd_binning', 'kd_raster', 'kd_softmask'):
+for f in ('kd_binning', 'kd_raster', 'kd_softmask', 'kd_softpair'):
     out = subprocess.run(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off',
                           '--offload-arch=gfx950', '-c', f'{f}.hip', '-o', '/tmp/kd_ru.o',
                           '-Rpass-analysis=kernel-resource-usage'], cwd=CSRC,
