@@ -196,13 +196,13 @@ template <typename T>
 struct SoftPairBuf {
   SoftPairRec *rec;   // [B * ntiles][cap]
   SoftCoef<T> *coef;  // [B * ntiles][cap] backward coefficients
-  T *sprob;           // [B * H * W][K] probability by (pixel, slot)
+  T *sprob;           // [K][B * H * W] probability by (slot, pixel)
   int32_t *npix;      // [B * H * W] close faces of each uncovered pixel
   int32_t *ntile;     // [B * ntiles][2]: records, faces in the tile list
   int2 *items;        // [B * ntiles * ceil(cap / 256)] (tile, 256-record chunk) work items
   int32_t *tiles;     // [B * ntiles] tiles with records
   int32_t *counters;  // [2]: items, tiles (zeroed by the binning's count kernel)
-  int64_t ntiles, cap;
+  int64_t ntiles, cap, npixels;
   int ntx;
 };
 

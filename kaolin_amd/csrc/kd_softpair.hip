@@ -52,6 +52,7 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   pb.ntiles = (int64_t)pb.ntx * ((H + kTile - 1) / kTile);
   pb.cap = (int64_t)kBlock * K;
   const int64_t tiles = (int64_t)B * pb.ntiles, P = (int64_t)B * H * W;
+  pb.npixels = P;
   char *base = (char *)ws;
   pb.rec = (SoftPairRec *)(base + off);
   off += align_up(sizeof(SoftPairRec) * (size_t)(tiles * pb.cap));
@@ -82,25 +83,33 @@ __device__ __forceinline__ void tile_pixel(int tx, int ty, int q, int &px, int &
 // ------------------------------------------------------------------------------------------
 // pass A: (pixel, slot, face) records per tile
 // ------------------------------------------------------------------------------------------
-// Lowest `need` set bits of m (need < popc(m)).
+// Lowest `need` set bits of m (0 <= need < popc(m)): binary search for the need-th set bit.
 __device__ __forceinline__ uint64_t lowest_bits(uint64_t m, int need) {
-  uint64_t sel = 0ull;
-  for (int i = 0; i < need; ++i) {
-    const uint64_t lsb = m & (~m + 1ull);
-    sel |= lsb;
-    m ^= lsb;
+  if (need <= 0) return 0ull;
+  int pos = 0, left = need;  // find the bit position of the need-th set bit (1-based)
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) {
+    const uint64_t lowmask = (w == 64) ? ~0ull : ((1ull << w) - 1ull);
+    const int c = __popcll((m >> pos) & lowmask);
+    if (c < left) {
+      left -= c;
+      pos += w;
+    }
   }
-  return sel;
+  // bit `pos` is the need-th set bit: keep bits 0..pos
+  return m & ((pos >= 63) ? ~0ull : ((2ull << pos) - 1ull));
 }
 
 // One 64-face chunk of a wave's sub-list (lane j = chunk entry j): every uncovered pixel lane
 // takes the first K - kid faces of the chunk whose exact enlarged span holds its centre
-// (ascending face index = ascending entry, dibr_soft_mask_cuda.cu:95 and :165-171), then the
-// selections are transposed so that each face lane writes its records, face-major.
+// (ascending face index = ascending entry, dibr_soft_mask_cuda.cu:95 and :165-171).  Records
+// are placed face-major (face j's pixels contiguous, pixels ascending): the transposed
+// selections give each face its record count and offset; each pixel lane then writes its own
+// records (slot = its running close-face count) at offset[j] + rank of the pixel in face j.
 __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
                                                    int K, const TileGeom &t, int64_t lo,
-                                                   int lbase, int &my_kid, uint64_t *s_sel,
-                                                   unsigned short *s_kb, int *s_nrec,
+                                                   int lbase, int &my_kid, uint64_t *s_pm,
+                                                   unsigned short *s_off, int *s_nrec,
                                                    SoftPairRec *rec) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qx = lane & 7, qy = lane >> 3;
@@ -118,14 +127,9 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
     mr = (qy == i) ? br : mr;
   }
   uint64_t sel = (unc && my_kid < K) ? (mc & mr) : 0ull;
-  const int need = K - my_kid;
-  if (__popcll(sel) > need) sel = lowest_bits(sel, need);
-  s_sel[lane] = sel;
-  s_kb[lane] = (unsigned short)my_kid;
-  my_kid += __popcll(sel);
-  wave_lds_sync();
-  // face lanes: pixels that selected this face
-  uint64_t pm = wave_transpose64(sel);
+  if (__popcll(sel) > K - my_kid) sel = lowest_bits(sel, K - my_kid);
+  // face lanes: pixel masks, record counts and offsets
+  const uint64_t pm = wave_transpose64(sel);
   const int cnt = __popcll(pm);
   const int incl = wave_incl_scan(cnt);
   const int tot = __builtin_amdgcn_readlane(incl, 63);
@@ -133,21 +137,25 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
   int base = 0;
   if (lane == 0) base = atomicAdd(s_nrec, tot);
   base = __builtin_amdgcn_readfirstlane(base);
-  int pos = base + incl - cnt;
+  s_pm[lane] = pm;
+  s_off[lane] = (unsigned short)(incl - cnt);
+  wave_lds_sync();
+  // pixel lanes: write own records, slots ascending with the face index
   const uint64_t below = (1ull << lane) - 1ull;
-  const int32_t row = (int32_t)(lo + L.f[k]);
-  const uint32_t lid = (uint32_t)(lbase + k);
-  while (pm) {
-    const int q = __builtin_ctzll(pm);
-    pm &= pm - 1ull;
+  const int tile_q = w * kWave + lane;
+  int slot = my_kid;
+  for (uint64_t m = sel; m; m &= m - 1ull) {
+    const int jj = __builtin_ctzll(m);
+    const int kk = L.sub[w][c * kWave + jj];
     SoftPairRec r;
-    r.row = row;
-    r.lid = lid;
-    r.slot = (uint16_t)(s_kb[q] + __popcll(s_sel[q] & below));
-    r.q = (uint8_t)(w * kWave + q);
+    r.row = (int32_t)(lo + L.f[kk]);
+    r.lid = (uint32_t)(lbase + kk);
+    r.slot = (uint16_t)slot++;
+    r.q = (uint8_t)tile_q;
     r.type = 0;
-    rec[pos++] = r;
+    rec[base + s_off[jj] + __popcll(s_pm[jj] & below)] = r;
   }
+  my_kid = slot;
   wave_lds_sync();
 }
 
@@ -155,8 +163,8 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
   TileClock clk(a.fs.tbuf, 1);
   __shared__ TileLists L;
-  __shared__ uint64_t s_sel[4][kWave];
-  __shared__ unsigned short s_kb[4][kWave];
+  __shared__ uint64_t s_pm[4][kWave];
+  __shared__ unsigned short s_off[4][kWave];
   __shared__ int s_nrec;
 
   const FaceSet<T> &fs = a.fs;
@@ -177,9 +185,9 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairB
   if (__syncthreads_or(unc)) {
     auto stage = [&](int, int64_t) {};  // pass A needs the spans only
     auto round = [&](int nsub, int cnt) {
-      if (wave_unc && !(fs.dbg & 1))
+      if (wave_unc && !(fs.dbg & 1024))
         for (int c = 0; c * kWave < nsub; ++c)
-          soft_chunk_records(L, nsub, c, unc, K, t, lo, lbase, my_kid, s_sel[w], s_kb[w],
+          soft_chunk_records(L, nsub, c, unc, K, t, lo, lbase, my_kid, s_pm[w], s_off[w],
                              &s_nrec, rec);
       lbase += cnt;
     };
@@ -187,7 +195,19 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairB
     auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
     tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg, done);
   }
-  if (t.inimg) pb.npix[p] = unc ? my_kid : 0;
+  if (t.inimg) {
+    pb.npix[p] = unc ? my_kid : 0;
+    // pixels without close faces are final here; the others get soft from kd_soft_reduce
+    if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
+    else if (a.soft && my_kid == 0) a.soft[p] = (T)0.0;
+    if (a.last && my_kid < K) a.last[p] = -1;
+    if (a.prob)  // -1 / 0 / 0 padding (dibr_soft_mask.cpp:86-97 pre-fill)
+      for (int s = my_kid; s < K; ++s) {
+        a.prob[p * K + s] = (T)0;
+        a.cidx[p * K + s] = -1;
+        a.ctype[p * K + s] = 0;
+      }
+  }
   __syncthreads();
   const int n = s_nrec;
   if (tid == 0) {
@@ -267,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
     if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
     const int64_t gp = ((int64_t)b * H + py) * W + px;
     const int64_t o = gp * K + r.slot;
-    pb.sprob[o] = prob;
+    pb.sprob[(int64_t)r.slot * pb.npixels + gp] = prob;
     rp->type = (uint8_t)et;
     if (LISTS) {
       a.prob[o] = prob;
@@ -283,32 +303,32 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
   }
 }
 
-template <typename T, bool LISTS>
+// soft = 1 - prod(1 - p) over the close faces in slot order, for the pixels that have any (the
+// tiles with records); every other pixel was written by kd_soft_pairs.
+template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPairBuf<T> pb) {
-  const int K = a.K;
-  const int64_t total = (int64_t)a.fs.B * a.fs.H * a.fs.W;
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < total;
-       p += (int64_t)gridDim.x * kBlock) {
-    const bool covered = a.face_idx[p] >= 0;
-    const int n = covered ? 0 : pb.npix[p];
+  const int K = a.K, H = a.fs.H, W = a.fs.W;
+  const int ntl = pb.counters[1];
+  for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) {
+    const int64_t tile = pb.tiles[ti];
+    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+    int px, py;
+    tile_pixel(tl % pb.ntx, tl / pb.ntx, threadIdx.x, px, py);
+    if (px >= W || py >= H) continue;
+    const int64_t p = ((int64_t)b * H + py) * W + px;
+    const int n = pb.npix[p];
+    if (n == 0) continue;
     T prod = (T)1.0;
-    const T *sp = pb.sprob + p * K;
+    const T *sp = pb.sprob + p;
     for (int s0 = 0; s0 < n; s0 += 8) {  // 8 loads in flight, then the ordered product
       T v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = s0 + j < n ? sp[s0 + j] : (T)0;
+      for (int j = 0; j < 8; ++j) v[j] = s0 + j < n ? sp[(int64_t)(s0 + j) * pb.npixels] : (T)0;
 #pragma unroll
       for (int j = 0; j < 8; ++j)  // dibr_soft_mask_cuda.cu:174-178, slot order
         if (s0 + j < n) prod = (T)((double)prod * (1.0 - (double)v[j]));
     }
-    a.soft[p] = covered ? (T)1.0 : (T)(1.0 - (double)prod);  // :69, :181
-    if (a.last && n < K) a.last[p] = -1;
-    if (LISTS)  // -1 / 0 / 0 padding (dibr_soft_mask.cpp:86-97 pre-fill)
-      for (int s = n; s < K; ++s) {
-        a.prob[p * K + s] = (T)0;
-        a.cidx[p * K + s] = -1;
-        a.ctype[p * K + s] = 0;
-      }
+    a.soft[p] = (T)(1.0 - (double)prod);  // :181
   }
 }
 
@@ -452,13 +472,7 @@ int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, boo
   }
   if (reduce) {
     ProfScope prof(K_SOFT_REDUCE, stream);
-    const int64_t total = (int64_t)fs.B * fs.H * fs.W;
-    const unsigned blocks = (unsigned)std::min<int64_t>((total + kBlock - 1) / kBlock, 65536);
-    if (a.prob)
-      hipLaunchKernelGGL((kd_soft_reduce<T, true>), dim3(blocks), dim3(kBlock), 0, stream, a, pb);
-    else
-      hipLaunchKernelGGL((kd_soft_reduce<T, false>), dim3(blocks), dim3(kBlock), 0, stream, a,
-                         pb);
+    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a, pb);
   }
   e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
