@@ -1,8 +1,8 @@
 #!/usr/bin/env python
 """DIB-R forward+backward throughput on MI355X (BASELINE.json metric).
 
-One step = prepare_vertices (camera transform, projection, per-face gather, normals; plain
-PyTorch) -> dibr_rasterization (HIP: rasterize + soft mask) -> torch.autograd.backward(
+One step = prepare_vertices (camera transform, projection, per-face gather, normals; fused HIP,
+kaolin_amd/csrc/kd_prepare.hip) -> dibr_rasterization (HIP: rasterize + soft mask) -> torch.autograd.backward(
 [interp, soft_mask], [g_feat, g_soft]) through the HIP backward kernels and the face->vertex
 scatter -> (N > 1) one RCCL all-reduce of the shared vertex gradient.  Inputs are resident in HBM
 before the timed region.  N GPUs: one process per GPU, each renders its own block of views of the
@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from kaolin_amd import _lib, distributed, workloads  # noqa: E402
-from kaolin_amd.render.mesh import dibr, dibr_rasterization  # noqa: E402
+from kaolin_amd.render.mesh import dibr, dibr_rasterization, prepare_vertices  # noqa: E402
 
 METRIC = 'Mpixels/s DIB-R fwd+bwd, 50k-face mesh @512² bs=8, 1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
@@ -106,8 +106,9 @@ def main():
     kw = dict(sigmainv=args.sigmainv, boxlen=args.boxlen, knum=args.knum)
 
     def step():
-        fvc, fvi, nrm = workloads.prepare_vertices(vertices.unsqueeze(0).expand(Bl, -1, -1),
-                                                   faces, proj, cam)
+        # one mesh, Bl cameras: vertices batch 1 broadcast over the views (utils.py:128-175)
+        fvc, fvi, nrm = prepare_vertices(vertices.unsqueeze(0), faces, proj,
+                                         camera_transform=cam)
         interp, soft, face_idx = dibr_rasterization(H, W, fvc[..., 2], fvi, feats, nrm[..., 2],
                                                     **kw)
         torch.autograd.backward([interp, soft], [g_feat, g_soft])

@@ -203,6 +203,44 @@ int kd_dibr_soft_mask_backward_binned_f64(int batch, int height, int width, int6
                                           float sigmainv, double *grad_fvi, void *workspace,
                                           size_t workspace_bytes, int bins_ready, void *stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * prepare_vertices (kaolin/render/mesh/utils.py:128-175 with camera_transform): camera
+ * transform (pad(v, 1) @ T), perspective projection (legacy.py:120-139), per-face gather
+ * (ops/mesh/mesh.py:24-45) and unit face normals (ops/mesh/trianglemesh.py:313-336), fused.
+ * vertices (Bv, V, 3) with Bv == 1 (shared by all views) or Bv == B; faces (F, 3) int64;
+ * camera_proj (3); camera_transform (B, 4, 3).  Outputs fvc (B, F, 3, 3), fvi (B, F, 3, 2),
+ * normals (B, F, 3).
+ * The backward walks each vertex's incident (face, corner) list -- CSR adjacency: adj_offsets
+ * (V + 1) int64, adj (3F) int32 entries f * 3 + corner, grouped by vertex -- and writes
+ * grad_vertices (Bv, V, 3) (summed over the views when Bv == 1; LDS sums per vertex, one float
+ * atomic per workgroup and vertex coordinate).  Any of the three incoming gradients may be NULL
+ * (zero).  fvc is the forward's output.
+ * ------------------------------------------------------------------------------------------- */
+int kd_prepare_vertices_forward_f32(int batch, int vertex_batch, int64_t num_vertices,
+                                    int64_t num_faces, const float *vertices,
+                                    const int64_t *faces, const float *camera_proj,
+                                    const float *camera_transform, float *fvc, float *fvi,
+                                    float *normals, void *stream);
+int kd_prepare_vertices_forward_f64(int batch, int vertex_batch, int64_t num_vertices,
+                                    int64_t num_faces, const double *vertices,
+                                    const int64_t *faces, const double *camera_proj,
+                                    const double *camera_transform, double *fvc, double *fvi,
+                                    double *normals, void *stream);
+int kd_prepare_vertices_backward_f32(int batch, int vertex_batch, int64_t num_vertices,
+                                     int64_t num_faces, const int64_t *faces,
+                                     const float *camera_proj, const float *camera_transform,
+                                     const float *fvc, const float *grad_fvc,
+                                     const float *grad_fvi, const float *grad_normals,
+                                     const int64_t *adj_offsets, const int32_t *adj,
+                                     float *grad_vertices, void *stream);
+int kd_prepare_vertices_backward_f64(int batch, int vertex_batch, int64_t num_vertices,
+                                     int64_t num_faces, const int64_t *faces,
+                                     const double *camera_proj, const double *camera_transform,
+                                     const double *fvc, const double *grad_fvc,
+                                     const double *grad_fvi, const double *grad_normals,
+                                     const int64_t *adj_offsets, const int32_t *adj,
+                                     double *grad_vertices, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -321,6 +321,62 @@ def dibr_soft_mask_backward_binned(grad_soft, soft, selected_face_idx, face_vert
     return g
 
 
+# -------------------------------------------------------------------------------------------
+# prepare_vertices (kaolin/render/mesh/utils.py:128-175), SURVEY §8 f1
+# -------------------------------------------------------------------------------------------
+def vertex_face_adjacency(faces, num_vertices):
+    """CSR of each vertex's incident (face, corner) entries f * 3 + corner, grouped by vertex
+    (stable order).  Returns (offsets (V+1) int64, adj (3F) int32) on the faces' device."""
+    flat = faces.reshape(-1)
+    order = torch.argsort(flat, stable=True)
+    counts = torch.bincount(flat, minlength=num_vertices)
+    offsets = torch.zeros(num_vertices + 1, dtype=torch.long, device=faces.device)
+    torch.cumsum(counts, 0, out=offsets[1:])
+    return offsets, order.to(torch.int32)
+
+
+def prepare_vertices_forward(vertices, faces, camera_proj, camera_transform):
+    """vertices (Bv, V, 3) with Bv in {1, B}, faces (F, 3) int64, camera_proj (3, 1),
+    camera_transform (B, 4, 3) -> (fvc (B, F, 3, 3), fvi (B, F, 3, 2), normals (B, F, 3))."""
+    fn = 'prepare_vertices'
+    dev = _check_same_gpu(fn, vertices=vertices, faces=faces, camera_proj=camera_proj,
+                          camera_transform=camera_transform)
+    Bv, V = vertices.shape[:2]
+    B, F = camera_transform.shape[0], faces.shape[0]
+    _check_size(fn, 'vertices', vertices, (Bv, V, 3))
+    _check_size(fn, 'faces', faces, (F, 3))
+    _check_size(fn, 'camera_transform', camera_transform, (B, 4, 3))
+    if Bv not in (1, B):
+        raise RuntimeError(f'{fn}: vertices batch {Bv} must be 1 or the camera batch {B}')
+    if faces.dtype != torch.int64:
+        raise RuntimeError(f'{fn}: faces must be int64')
+    sfx = _sfx(vertices, fn)
+    _check_dtype(fn, vertices, camera_proj=camera_proj, camera_transform=camera_transform)
+    opts = dict(device=dev, dtype=vertices.dtype)
+    fvc = torch.empty((B, F, 3, 3), **opts)
+    fvi = torch.empty((B, F, 3, 2), **opts)
+    nrm = torch.empty((B, F, 3), **opts)
+    _lib.call(f'kd_prepare_vertices_forward_{sfx}', B, Bv, V, F, _ptr(vertices), _ptr(faces),
+              _ptr(camera_proj), _ptr(camera_transform), _ptr(fvc), _ptr(fvi), _ptr(nrm),
+              _stream(dev))
+    return fvc, fvi, nrm
+
+
+def prepare_vertices_backward(faces, camera_proj, camera_transform, fvc, grad_fvc, grad_fvi,
+                              grad_nrm, adjacency, vertex_batch, num_vertices):
+    """Gradient w.r.t. the vertices (vertex_batch, V, 3); None gradients count as zero."""
+    dev = fvc.device
+    B, F = fvc.shape[:2]
+    sfx = _sfx(fvc, 'prepare_vertices_backward')
+    offsets, adj = adjacency
+    g = torch.empty((vertex_batch, num_vertices, 3), device=dev, dtype=fvc.dtype)
+    _lib.call(f'kd_prepare_vertices_backward_{sfx}', B, vertex_batch, num_vertices, F,
+              _ptr(faces), _ptr(camera_proj), _ptr(camera_transform), _ptr(fvc),
+              _ptr(grad_fvc), _ptr(grad_fvi), _ptr(grad_nrm), _ptr(offsets), _ptr(adj), _ptr(g),
+              _stream(dev))
+    return g
+
+
 render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
     rasterize_backward_cuda=rasterize_backward_cuda,

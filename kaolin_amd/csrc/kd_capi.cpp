@@ -29,7 +29,8 @@ std::vector<Rec> g_recs;
 const char *kNames[K_NUM_KERNELS] = {
     "kd_bin_count", "kd_bin_scan", "kd_bin_scatter", "kd_raster_fwd", "kd_soft_fwd",
     "kd_raster_bwd_tile", "kd_soft_bwd_tile", "kd_raster_bwd_atomic", "kd_soft_bwd_atomic",
-    "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs"};
+    "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs",
+    "kd_prepare_fwd", "kd_prepare_bwd"};
 }  // namespace
 
 ProfScope::ProfScope(int id_, hipStream_t s) : id(id_), stream(s), on(g_prof.load()) {

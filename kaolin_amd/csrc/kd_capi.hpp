@@ -27,6 +27,8 @@ enum KernelId {
   K_SOFT_MATH,
   K_SOFT_REDUCE,
   K_SOFT_BWD_PAIRS,
+  K_PREPARE_FWD,
+  K_PREPARE_BWD,
   K_NUM_KERNELS
 };
 

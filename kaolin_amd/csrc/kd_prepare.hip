@@ -1,0 +1,264 @@
+// kd_prepare.hip -- the DIB-R step's upstream projection and its face->vertex backward, fused
+// (SURVEY.md §8 f1).
+//
+// Reference: kaolin/render/mesh/utils.py:128-175 (prepare_vertices) composes
+//   vertices_camera = pad(vertices, 1) @ camera_transform                 (utils.py:164-167)
+//   vertices_image  = perspective_camera(vertices_camera, camera_proj)    (legacy.py:120-139)
+//   face_vertices_* = index_vertices_by_faces(..., faces)                 (ops/mesh/mesh.py:24-45)
+//   face_normals    = cross(v1 - v0, v2 - v0) / (|.| + 1e-10)             (trianglemesh.py:313-336)
+// as ~15 PyTorch kernels forward and ~25 backward, the largest being the index_add that scatters
+// the (B, F, 3, C) face-corner gradients back onto the vertices (one float atomic per corner
+// coordinate).  Here:
+//   kd_prepare_fwd  one thread per (view, face): transform, project, gather and normal in
+//                   registers, write the three outputs once.
+//   kd_prepare_bwd  one thread per incident (face, corner) entry of the vertex -> corner CSR
+//                   (built once per topology): projection / normal / gather backward and the
+//                   transposed camera transform, summed over the views when the vertices are
+//                   shared; a vertex's entries are summed in LDS and added with one float
+//                   atomic per (workgroup, vertex, coordinate) instead of one per corner.
+#include "../../include/kaolin_dibr.h"
+#include "kd_capi.hpp"
+#include "kd_common.hpp"
+#include "kd_tile.hpp"
+
+namespace kd {
+
+template <typename T>
+struct PrepArgs {
+  int B, Bv;        // views; vertex batches (1 = shared by all views, else B)
+  int64_t V, F;
+  const T *vertices;   // (Bv, V, 3)
+  const int64_t *faces;  // (F, 3)
+  const T *proj;       // (3)
+  const T *tf;         // (B, 4, 3)
+};
+
+template <typename T>
+__device__ __forceinline__ void cam_point(const T *tf, const T *p, T c[3]) {
+#pragma unroll
+  for (int j = 0; j < 3; ++j) c[j] = p[0] * tf[j] + p[1] * tf[3 + j] + p[2] * tf[6 + j] + tf[9 + j];
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_prepare_fwd(PrepArgs<T> a, T *fvc, T *fvi, T *nrm) {
+  const int64_t total = (int64_t)a.B * a.F;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * kBlock) {
+    const int b = (int)(i / a.F);
+    const int64_t f = i - (int64_t)b * a.F;
+    const T *vb = a.vertices + (a.Bv == 1 ? 0 : (int64_t)b * a.V * 3);
+    const T *tf = a.tf + (int64_t)b * 12;
+    T c[3][3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const int64_t v = a.faces[f * 3 + k];
+      cam_point<T>(tf, vb + v * 3, c[k]);
+    }
+    T *oc = fvc + i * 9;
+    T *oi = fvi + i * 6;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      oc[k * 3 + 0] = c[k][0];
+      oc[k * 3 + 1] = c[k][1];
+      oc[k * 3 + 2] = c[k][2];
+      const T pz = c[k][2] * a.proj[2];
+      oi[k * 2 + 0] = c[k][0] * a.proj[0] / pz;
+      oi[k * 2 + 1] = c[k][1] * a.proj[1] / pz;
+    }
+    const T e1[3] = {c[1][0] - c[0][0], c[1][1] - c[0][1], c[1][2] - c[0][2]};
+    const T e2[3] = {c[2][0] - c[0][0], c[2][1] - c[0][1], c[2][2] - c[0][2]};
+    const T n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                    e1[0] * e2[1] - e1[1] * e2[0]};
+    const T len = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]) + (T)1e-10;
+    T *on = nrm + i * 3;
+    on[0] = n[0] / len;
+    on[1] = n[1] / len;
+    on[2] = n[2] / len;
+  }
+}
+
+// Gradient of one face corner w.r.t. its camera-space position: the gather (grad_fvc), the
+// projection (grad_fvi) and the unit normal (grad_nrm, which depends on all three corners).
+template <typename T>
+__device__ __forceinline__ void corner_grad(const T c[3][3], int k, const T proj[3],
+                                            const T *gc, const T *gi, const T *gn, T g[3]) {
+  g[0] = gc ? gc[0] : (T)0;
+  g[1] = gc ? gc[1] : (T)0;
+  g[2] = gc ? gc[2] : (T)0;
+  if (gi) {  // x = P0 cx / (P2 cz), y = P1 cy / (P2 cz)
+    const T pz = c[k][2] * proj[2];
+    const T x = c[k][0] * proj[0] / pz, y = c[k][1] * proj[1] / pz;
+    g[0] += gi[0] * proj[0] / pz;
+    g[1] += gi[1] * proj[1] / pz;
+    g[2] -= (gi[0] * x + gi[1] * y) / c[k][2];
+  }
+  if (gn) {  // n = r / (|r| + 1e-10), r = e1 x e2, e1 = c1 - c0, e2 = c2 - c0
+    const T e1[3] = {c[1][0] - c[0][0], c[1][1] - c[0][1], c[1][2] - c[0][2]};
+    const T e2[3] = {c[2][0] - c[0][0], c[2][1] - c[0][1], c[2][2] - c[0][2]};
+    const T r[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                    e1[0] * e2[1] - e1[1] * e2[0]};
+    const T len = sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    const T d = len + (T)1e-10;
+    const T rg = r[0] * gn[0] + r[1] * gn[1] + r[2] * gn[2];
+    const T s = len > (T)0 ? rg / (len * d * d) : (T)0;
+    const T gr[3] = {gn[0] / d - r[0] * s, gn[1] / d - r[1] * s, gn[2] / d - r[2] * s};
+    // (a x b) . g = a . (b x g) = b . (g x a)
+    const T ge1[3] = {e2[1] * gr[2] - e2[2] * gr[1], e2[2] * gr[0] - e2[0] * gr[2],
+                      e2[0] * gr[1] - e2[1] * gr[0]};
+    const T ge2[3] = {gr[1] * e1[2] - gr[2] * e1[1], gr[2] * e1[0] - gr[0] * e1[2],
+                      gr[0] * e1[1] - gr[1] * e1[0]};
+#pragma unroll
+    for (int j = 0; j < 3; ++j) g[j] += k == 1 ? ge1[j] : k == 2 ? ge2[j] : -(ge1[j] + ge2[j]);
+  }
+}
+
+// One thread per incident (face, corner) entry of the CSR (entries grouped by vertex) and vertex
+// batch: the corner's gradient, transformed back to world space, summed over the views it
+// covers; the entries of one vertex are then summed in LDS (segments of the workgroup's 256
+// entries) and added to the vertex with one float atomic per (workgroup, vertex, coordinate).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T *fvc,
+                                                         const T *gfvc, const T *gfvi,
+                                                         const T *gnrm, const int32_t *adj,
+                                                         T *gvert) {
+  __shared__ T s_acc[kBlock][3];
+  __shared__ int64_t s_vid[kBlock];
+  __shared__ int s_scan[4];
+  const int64_t ne = a.F * 3;
+  const int bv = blockIdx.y;
+  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool valid = e < ne;
+  int64_t v = -1;
+  T g3[3] = {0, 0, 0};
+  if (valid) {
+    const int32_t fc = adj[e];
+    const int64_t f = fc / 3;
+    const int k = fc - (int)f * 3;
+    v = a.faces[f * 3 + k];
+    const int b0 = a.Bv == 1 ? 0 : bv, b1 = a.Bv == 1 ? a.B : bv + 1;
+    for (int b = b0; b < b1; ++b) {
+      const int64_t row = (int64_t)b * a.F + f;
+      T c[3][3];
+      const T *pc = fvc + row * 9;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) c[q / 3][q % 3] = pc[q];
+      T g[3];
+      corner_grad<T>(c, k, a.proj, gfvc ? gfvc + row * 9 + k * 3 : nullptr,
+                     gfvi ? gfvi + row * 6 + k * 2 : nullptr, gnrm ? gnrm + row * 3 : nullptr, g);
+      // cam_j = sum_i p_i tf[i][j] + tf[3][j]  ->  dL/dp_i = sum_j tf[i][j] g_j
+      const T *tf = a.tf + (int64_t)b * 12;
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        g3[q] += tf[q * 3 + 0] * g[0] + tf[q * 3 + 1] * g[1] + tf[q * 3 + 2] * g[2];
+    }
+  }
+  // segments of equal vertex inside the workgroup (entries are grouped by vertex)
+  s_vid[threadIdx.x] = v;
+  __syncthreads();
+  const bool start = valid && (threadIdx.x == 0 || s_vid[threadIdx.x - 1] != v);
+  int nseg;
+  const int seg = wg_exclusive_scan(start ? 1 : 0, s_scan, nseg) + (start ? 0 : -1);
+  if (threadIdx.x < nseg) {
+    s_acc[threadIdx.x][0] = (T)0;
+    s_acc[threadIdx.x][1] = (T)0;
+    s_acc[threadIdx.x][2] = (T)0;
+  }
+  __syncthreads();
+  if (valid) {
+    if (start) s_vid[kBlock - 1 - seg] = v;  // segment -> vertex (upper half of the array)
+    atomicAdd(&s_acc[seg][0], g3[0]);
+    atomicAdd(&s_acc[seg][1], g3[1]);
+    atomicAdd(&s_acc[seg][2], g3[2]);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < nseg * 3; i += kBlock) {
+    const int sg = i / 3, q = i - sg * 3;
+    atomicAdd(gvert + ((int64_t)bv * a.V + s_vid[kBlock - 1 - sg]) * 3 + q, s_acc[sg][q]);
+  }
+}
+
+template <typename T>
+static int prep_fwd(int B, int Bv, int64_t V, int64_t F, const T *vert, const int64_t *faces,
+                    const T *proj, const T *tf, T *fvc, T *fvi, T *nrm, void *stream) {
+  KD_CHECK_ARG(B >= 0 && V >= 0 && F >= 0, "negative size");
+  KD_CHECK_ARG(Bv == 1 || Bv == B, "vertex batch must be 1 or the view count");
+  const int64_t total = (int64_t)B * F;
+  if (total == 0) return KD_OK;
+  PrepArgs<T> a{B, Bv, V, F, vert, faces, proj, tf};
+  const unsigned blocks = (unsigned)std::min<int64_t>((total + kBlock - 1) / kBlock, 65536);
+  {
+    ProfScope prof(K_PREPARE_FWD, (hipStream_t)stream);
+    hipLaunchKernelGGL(kd_prepare_fwd<T>, dim3(blocks), dim3(kBlock), 0, (hipStream_t)stream, a,
+                       fvc, fvi, nrm);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "prepare fwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template <typename T>
+static int prep_bwd(int B, int Bv, int64_t V, int64_t F, const int64_t *faces, const T *proj,
+                    const T *tf, const T *fvc, const T *gfvc, const T *gfvi, const T *gnrm,
+                    const int64_t *adj_off, const int32_t *adj, T *gvert, void *stream) {
+  KD_CHECK_ARG(B >= 0 && V >= 0 && F >= 0, "negative size");
+  KD_CHECK_ARG(Bv == 1 || Bv == B, "vertex batch must be 1 or the view count");
+  KD_CHECK_ARG(F * 3 < (1ll << 31), "too many faces");
+  (void)adj_off;  // the entries carry their vertex through `faces`
+  const int64_t total = (int64_t)Bv * V;
+  if (total == 0) return KD_OK;
+  hipError_t e0 = hipMemsetAsync(gvert, 0, sizeof(T) * total * 3, (hipStream_t)stream);
+  if (e0 != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e0));
+  if (F == 0 || B == 0) return KD_OK;
+  PrepArgs<T> a{B, Bv, V, F, nullptr, faces, proj, tf};
+  const int64_t nb = (F * 3 + kBlock - 1) / kBlock;
+  KD_CHECK_ARG(nb < (1ll << 31), "too many faces");
+  {
+    ProfScope prof(K_PREPARE_BWD, (hipStream_t)stream);
+    hipLaunchKernelGGL(kd_prepare_bwd<T>, dim3((unsigned)nb, Bv), dim3(kBlock), 0,
+                       (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj, gvert);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "prepare bwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+}  // namespace kd
+
+using namespace kd;
+
+extern "C" {
+
+int kd_prepare_vertices_forward_f32(int B, int Bv, int64_t V, int64_t F, const float *vertices,
+                                    const int64_t *faces, const float *camera_proj,
+                                    const float *camera_transform, float *fvc, float *fvi,
+                                    float *normals, void *stream) {
+  return prep_fwd<float>(B, Bv, V, F, vertices, faces, camera_proj, camera_transform, fvc, fvi,
+                         normals, stream);
+}
+int kd_prepare_vertices_forward_f64(int B, int Bv, int64_t V, int64_t F, const double *vertices,
+                                    const int64_t *faces, const double *camera_proj,
+                                    const double *camera_transform, double *fvc, double *fvi,
+                                    double *normals, void *stream) {
+  return prep_fwd<double>(B, Bv, V, F, vertices, faces, camera_proj, camera_transform, fvc, fvi,
+                          normals, stream);
+}
+int kd_prepare_vertices_backward_f32(int B, int Bv, int64_t V, int64_t F, const int64_t *faces,
+                                     const float *camera_proj, const float *camera_transform,
+                                     const float *fvc, const float *grad_fvc,
+                                     const float *grad_fvi, const float *grad_normals,
+                                     const int64_t *adj_offsets, const int32_t *adj,
+                                     float *grad_vertices, void *stream) {
+  return prep_bwd<float>(B, Bv, V, F, faces, camera_proj, camera_transform, fvc, grad_fvc,
+                         grad_fvi, grad_normals, adj_offsets, adj, grad_vertices, stream);
+}
+int kd_prepare_vertices_backward_f64(int B, int Bv, int64_t V, int64_t F, const int64_t *faces,
+                                     const double *camera_proj, const double *camera_transform,
+                                     const double *fvc, const double *grad_fvc,
+                                     const double *grad_fvi, const double *grad_normals,
+                                     const int64_t *adj_offsets, const int32_t *adj,
+                                     double *grad_vertices, void *stream) {
+  return prep_bwd<double>(B, Bv, V, F, faces, camera_proj, camera_transform, fvc, grad_fvc,
+                          grad_fvi, grad_normals, adj_offsets, adj, grad_vertices, stream);
+}
+
+}  // extern "C"

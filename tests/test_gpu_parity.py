@@ -440,3 +440,88 @@ def test_nonfinite_multiplier_rejected():
     with pytest.raises((RuntimeError, ValueError)):
         rasterize(8, 8, z, torch.zeros((1, 2, 3, 2), device=DEV),
                   torch.zeros((1, 2, 3, 1), device=DEV), multiplier=float('inf'))
+
+
+# --------------------------------------------------------------------------------------------
+# prepare_vertices: fused projection / gather / normals and the gather-form
+# backward vs the reference's PyTorch composition in fp64 (tolerances: fp32 1e-5 relative,
+# fp64 1e-10)
+# --------------------------------------------------------------------------------------------
+def _torch_prepare(vertices, faces, proj, tf):
+    padded = torch.nn.functional.pad(vertices, (0, 1), mode='constant', value=1.)
+    vc = padded @ tf
+    pp = vc * proj.view(-1, 1, 3)
+    vi = pp[:, :, :2] / pp[:, :, 2:3]
+    B = vc.shape[0]
+    fvc = vc[:, faces.reshape(-1)].reshape(B, faces.shape[0], 3, 3)
+    fvi = vi[:, faces.reshape(-1)].reshape(B, faces.shape[0], 3, 2)
+    n = torch.cross(fvc[:, :, 1] - fvc[:, :, 0], fvc[:, :, 2] - fvc[:, :, 0], dim=2)
+    return fvc, fvi, n / (n.norm(dim=2, keepdim=True) + 1e-10)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('shared', [True, False])
+@pytest.mark.parametrize('which', ['all', 'fvi'])
+def test_prepare_vertices_vs_torch(dname, shared, which):
+    import math
+
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import prepare_vertices
+    dt = TORCH_DTYPES[dname]
+    verts, faces, _ = workloads.uv_sphere(30, 17, seed=4)
+    B = 3
+    cam = workloads.orbit_cameras(B, 0.4).to(DEV, dt)
+    proj = workloads.generate_perspective_projection(math.pi / 4).to(DEV, dt)
+    faces = faces.to(DEV)
+    v = verts.to(DEV, dt)
+    if not shared:
+        v = (v.unsqueeze(0) + 0.01 * torch.randn((B,) + v.shape, device=DEV, dtype=dt))
+    else:
+        v = v.unsqueeze(0)
+    v1 = v.clone().requires_grad_(True)
+    v2 = v.detach().double().clone().requires_grad_(True)
+    out1 = prepare_vertices(v1, faces, proj, camera_transform=cam)
+    out2 = _torch_prepare(v2, faces, proj.double(), cam.double())
+    rtol = 1e-5 if dname == 'f32' else 1e-10
+    for a, b in zip(out1, out2):
+        torch.testing.assert_close(a.double(), b, rtol=rtol, atol=rtol)
+    g = [torch.randn_like(o) for o in out2]
+    if which == 'fvi':
+        torch.autograd.backward(out1[1], g[1].to(dt))
+        torch.autograd.backward(out2[1], g[1])
+    else:
+        torch.autograd.backward(out1, [x.to(dt) for x in g])
+        torch.autograd.backward(out2, g)
+    if dname == 'f64':
+        torch.testing.assert_close(v1.grad, v2.grad, rtol=1e-9, atol=1e-9)
+    else:
+        # fp32 bar: no worse than 4x the reference composition's own fp32 error (the unit-normal
+        # gradient is ill-conditioned on thin pole triangles) and 1e-5 of the gradient's scale
+        v3 = v.detach().clone().requires_grad_(True)
+        out3 = _torch_prepare(v3, faces, proj, cam)
+        if which == 'fvi':
+            torch.autograd.backward(out3[1], g[1].to(dt))
+        else:
+            torch.autograd.backward(out3, [x.to(dt) for x in g])
+        err = (v1.grad.double() - v2.grad).abs().max().item()
+        err_ref = (v3.grad.double() - v2.grad).abs().max().item()
+        assert err <= 4 * err_ref + 1e-5 * v2.grad.abs().max().item(), (err, err_ref)
+
+
+def test_prepare_vertices_rot_trans_and_camera_grad():
+    from kaolin_amd.render.mesh import prepare_vertices
+    rng = torch.Generator().manual_seed(3)
+    v = torch.randn((2, 50, 3), generator=rng).to(DEV)
+    faces = torch.randint(0, 50, (80, 3), generator=rng).to(DEV)
+    q, _ = torch.linalg.qr(torch.randn((2, 3, 3), generator=rng))
+    rot = q.to(DEV)
+    trans = torch.tensor([[0., 0., 4.], [0.5, -0.2, 5.]], device=DEV)
+    proj = torch.tensor([[1.7], [1.7], [-1.]], device=DEV)
+    fvc, fvi, n = prepare_vertices(v, faces, proj, camera_rot=rot, camera_trans=trans)
+    vc = torch.matmul(v - trans.view(-1, 1, 3), rot.permute(0, 2, 1))
+    torch.testing.assert_close(fvc, vc[:, faces.reshape(-1)].reshape(2, 80, 3, 3),
+                               rtol=1e-5, atol=1e-5)
+    tf = torch.randn((2, 4, 3), device=DEV, requires_grad=True)  # camera grads: composition
+    fvc, fvi, n = prepare_vertices(v, faces, proj, camera_transform=tf)
+    fvi.sum().backward()
+    assert tf.grad is not None
