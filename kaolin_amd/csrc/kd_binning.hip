@@ -1,5 +1,6 @@
 // kd_binning.hip -- see kd_binning.hpp for the algorithm.
 #include "kd_binning.hpp"
+#include "kd_tile.hpp"
 
 #include "kd_capi.hpp"
 
@@ -155,37 +156,53 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(FaceSet<T> fs, BinBuffers
 }
 
 // One workgroup per (coarse tile, view): exclusive scan of counts[b][*][c] over the chunks.
+// Each thread owns a contiguous run of chunks; the run sums are scanned with DPP inside each
+// wave and across the 4 waves through LDS (kd_tile.hpp wg_exclusive_scan, one barrier pair).
 __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb, int B) {
-  __shared__ int s_sum[kBlock];
+  __shared__ int s_w[4];
   const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int nct = bb.g.nct();
   const int n = bb.nchunk;
   const int per = (n + kBlock - 1) / kBlock;
   int *base = bb.counts + (int64_t)b * n * nct + c;
+  constexpr int kMaxPer = 8;  // register-held run (n <= 2048 chunks = 524k faces per view)
+  int v[kMaxPer];
   int local = 0;
-  for (int k = 0; k < per; ++k) {
-    const int j = tid * per + k;
-    if (j < n) local += base[(int64_t)j * nct];
-  }
-  s_sum[tid] = local;
-  __syncthreads();
-  // Hillis-Steele inclusive scan of the 256 thread sums.
-  for (int d = 1; d < kBlock; d <<= 1) {
-    const int v = tid >= d ? s_sum[tid - d] : 0;
-    __syncthreads();
-    s_sum[tid] += v;
-    __syncthreads();
-  }
-  int run = s_sum[tid] - local;  // exclusive prefix of this thread's first chunk
-  for (int k = 0; k < per; ++k) {
-    const int j = tid * per + k;
-    if (j < n) {
-      const int v = base[(int64_t)j * nct];
-      base[(int64_t)j * nct] = run;
-      run += v;
+  if (per <= kMaxPer) {
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k) {
+      const int j = tid * per + k;
+      v[k] = (k < per && j < n) ? base[(int64_t)j * nct] : 0;
+      local += v[k];
+    }
+  } else {
+    for (int k = 0; k < per; ++k) {
+      const int j = tid * per + k;
+      if (j < n) local += base[(int64_t)j * nct];
     }
   }
-  if (tid == kBlock - 1) bb.totals[(int64_t)b * nct + c] = s_sum[kBlock - 1];
+  int total;
+  int run = wg_exclusive_scan(local, s_w, total);  // exclusive prefix of this thread's run
+  if (per <= kMaxPer) {
+#pragma unroll
+    for (int k = 0; k < kMaxPer; ++k) {
+      const int j = tid * per + k;
+      if (k < per && j < n) {
+        base[(int64_t)j * nct] = run;
+        run += v[k];
+      }
+    }
+  } else {
+    for (int k = 0; k < per; ++k) {
+      const int j = tid * per + k;
+      if (j < n) {
+        const int x = base[(int64_t)j * nct];
+        base[(int64_t)j * nct] = run;
+        run += x;
+      }
+    }
+  }
+  if (tid == 0) bb.totals[(int64_t)b * nct + c] = total;
 }
 
 template <typename T>

@@ -474,8 +474,9 @@ def test_prepare_vertices_vs_torch(dname, shared, which):
     proj = workloads.generate_perspective_projection(math.pi / 4).to(DEV, dt)
     faces = faces.to(DEV)
     v = verts.to(DEV, dt)
+    gen = torch.Generator().manual_seed(7)
     if not shared:
-        v = (v.unsqueeze(0) + 0.01 * torch.randn((B,) + v.shape, device=DEV, dtype=dt))
+        v = v.unsqueeze(0) + 0.01 * torch.randn((B,) + v.shape, generator=gen).to(DEV, dt)
     else:
         v = v.unsqueeze(0)
     v1 = v.clone().requires_grad_(True)
@@ -483,9 +484,16 @@ def test_prepare_vertices_vs_torch(dname, shared, which):
     out1 = prepare_vertices(v1, faces, proj, camera_transform=cam)
     out2 = _torch_prepare(v2, faces, proj.double(), cam.double())
     rtol = 1e-5 if dname == 'f32' else 1e-10
-    for a, b in zip(out1, out2):
-        torch.testing.assert_close(a.double(), b, rtol=rtol, atol=rtol)
-    g = [torch.randn_like(o) for o in out2]
+    if dname == 'f64':
+        for a, b in zip(out1, out2):
+            torch.testing.assert_close(a, b, rtol=rtol, atol=rtol)
+    else:  # fp32: within 4x the reference composition's own fp32 error (thin-triangle normals)
+        out32 = _torch_prepare(v.detach(), faces, proj, cam)
+        for a, b, r in zip(out1, out2, out32):
+            err = (a.double() - b).abs().max().item()
+            err_ref = (r.double() - b).abs().max().item()
+            assert err <= 4 * err_ref + 1e-6, (err, err_ref)
+    g = [torch.randn(o.shape, generator=gen, dtype=torch.float64).to(DEV) for o in out2]
     if which == 'fvi':
         torch.autograd.backward(out1[1], g[1].to(dt))
         torch.autograd.backward(out2[1], g[1])
