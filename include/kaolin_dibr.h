@@ -204,6 +204,55 @@ int kd_dibr_soft_mask_backward_binned_f64(int batch, int height, int width, int6
                                           size_t workspace_bytes, int bins_ready, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * dibr_rasterization (kaolin/render/mesh/dibr.py:119-209) fused: rasterize of the faces with
+ * normals_z >= 0 (dibr.py:195) + dibr_soft_mask of all faces (dibr.py:201-208), one binning
+ * pass for both.  fvi UNSCALED (B, F, 3, 2); face_vertices_z read at
+ * fvz[(b * F + f) * fvz_face_stride + j * fvz_corner_stride] and normals_z at
+ * normals_z[(b * F + f) * normals_z_stride] (views of prepare_vertices' outputs: 9, 3 and 3);
+ * normals_z NULL = all faces valid.  Outputs interp (B, H, W, D), face_idx (B, H, W) int64,
+ * weights (B, H, W, 3), soft (B, H, W).  With want_grad the workspace keeps what the backward
+ * needs; pass the same workspace to the backward.  Workspace: kd_dibr_workspace_size().
+ * The backward writes grad_fvi (B, F, 3, 2) = raster + soft-mask gradients (one buffer) and
+ * grad_feat (nullable); grad_interp / grad_soft NULL = zero.
+ * ------------------------------------------------------------------------------------------- */
+size_t kd_dibr_workspace_size(int batch, int height, int width, int64_t num_faces, int knum,
+                              int double_precision);
+int kd_dibr_rasterization_forward_f32(int batch, int height, int width, int64_t num_faces,
+                                      int feat_dim, const float *fvz, int64_t fvz_face_stride,
+                                      int64_t fvz_corner_stride, const float *fvi,
+                                      const float *feat, const float *normals_z,
+                                      int64_t normals_z_stride, double multiplier, float eps,
+                                      float sigmainv, double boxlen, int knum, float *interp,
+                                      int64_t *face_idx, float *weights, float *soft,
+                                      int want_grad, void *workspace, size_t workspace_bytes,
+                                      void *stream);
+int kd_dibr_rasterization_forward_f64(int batch, int height, int width, int64_t num_faces,
+                                      int feat_dim, const double *fvz, int64_t fvz_face_stride,
+                                      int64_t fvz_corner_stride, const double *fvi,
+                                      const double *feat, const double *normals_z,
+                                      int64_t normals_z_stride, double multiplier, float eps,
+                                      float sigmainv, double boxlen, int knum, double *interp,
+                                      int64_t *face_idx, double *weights, double *soft,
+                                      int want_grad, void *workspace, size_t workspace_bytes,
+                                      void *stream);
+int kd_dibr_rasterization_backward_f32(int batch, int height, int width, int64_t num_faces,
+                                       int feat_dim, const float *grad_interp,
+                                       const float *grad_soft, const int64_t *face_idx,
+                                       const float *weights, const float *soft, const float *fvi,
+                                       const float *feat, float eps, double multiplier,
+                                       double boxlen, float sigmainv, int knum, float *grad_fvi,
+                                       float *grad_feat, void *workspace,
+                                       size_t workspace_bytes, void *stream);
+int kd_dibr_rasterization_backward_f64(int batch, int height, int width, int64_t num_faces,
+                                       int feat_dim, const double *grad_interp,
+                                       const double *grad_soft, const int64_t *face_idx,
+                                       const double *weights, const double *soft,
+                                       const double *fvi, const double *feat, float eps,
+                                       double multiplier, double boxlen, float sigmainv,
+                                       int knum, double *grad_fvi, double *grad_feat,
+                                       void *workspace, size_t workspace_bytes, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
  * prepare_vertices (kaolin/render/mesh/utils.py:128-175 with camera_transform): camera
  * transform (pad(v, 1) @ T), perspective projection (legacy.py:120-139), per-face gather
  * (ops/mesh/mesh.py:24-45) and unit face normals (ops/mesh/trianglemesh.py:313-336), fused.

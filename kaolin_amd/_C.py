@@ -377,6 +377,84 @@ def prepare_vertices_backward(faces, camera_proj, camera_transform, fvc, grad_fv
     return g
 
 
+# -------------------------------------------------------------------------------------------
+# dibr_rasterization fused (kd_dibr.hip)
+# -------------------------------------------------------------------------------------------
+def _rows_view(t, F, inner):
+    """(pointer tensor, face stride, inner stride) of a (B, F[, inner]) view whose faces are
+    evenly strided across the batch; a contiguous copy otherwise."""
+    if t.dim() == 2:
+        s0, s1 = t.stride()
+        if s0 == F * s1 or t.shape[0] == 1:
+            return t, s1, 1
+    else:
+        s0, s1, s2 = t.stride()
+        if s0 == F * s1 or t.shape[0] == 1:
+            return t, s1, s2
+    t = t.contiguous()
+    return t, (inner if t.dim() == 3 else 1), 1
+
+
+def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertices_image,
+                                     face_features, face_normals_z, sigmainv, boxlen, knum,
+                                     multiplier, eps, want_grad=True):
+    """rasterize(valid = normals_z >= 0) + dibr_soft_mask in one launch sequence.  Returns
+    (interp, face_idx, weights, soft, workspace)."""
+    fn = 'dibr_rasterization'
+    dev = _check_same_gpu(fn, face_vertices_z=face_vertices_z,
+                          face_vertices_image=face_vertices_image, face_features=face_features,
+                          face_normals_z=face_normals_z)
+    B, F = face_vertices_image.shape[:2]
+    D = face_features.shape[-1]
+    _check_size(fn, 'face_vertices_z', face_vertices_z, (B, F, 3))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'face_features', face_features, (B, F, 3, D))
+    _check_size(fn, 'face_normals_z', face_normals_z, (B, F))
+    sfx = _sfx(face_vertices_image, fn)
+    _check_dtype(fn, face_vertices_image, face_vertices_z=face_vertices_z,
+                 face_features=face_features, face_normals_z=face_normals_z)
+    knum = int(knum)
+    if knum < 1:
+        raise RuntimeError(f'{fn}: knum must be >= 1, got {knum}')
+    fvz, fvz_fs, fvz_cs = _rows_view(face_vertices_z, F, 3)
+    nz, nz_s, _ = _rows_view(face_normals_z, F, 1)
+    fvi = face_vertices_image.contiguous()
+    feat = face_features.contiguous()
+    opts = dict(device=dev, dtype=fvi.dtype)
+    interp = torch.empty((B, height, width, D), **opts)
+    face_idx = torch.empty((B, height, width), device=dev, dtype=torch.long)
+    weights = torch.empty((B, height, width, 3), **opts)
+    soft = torch.empty((B, height, width), **opts)
+    nb = int(_lib.load().kd_dibr_workspace_size(B, height, width, F, knum,
+                                                1 if fvi.dtype == torch.float64 else 0))
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+    _lib.call(f'kd_dibr_rasterization_forward_{sfx}', B, height, width, F, D, _ptr(fvz), fvz_fs,
+              fvz_cs, _ptr(fvi), _ptr(feat), _ptr(nz), nz_s, float(multiplier), float(eps),
+              float(sigmainv), float(boxlen), knum, _ptr(interp), _ptr(face_idx), _ptr(weights),
+              _ptr(soft), 1 if want_grad else 0, _ptr(ws), nb, _stream(dev))
+    return interp, face_idx, weights, soft, ws
+
+
+def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights, soft,
+                                      face_vertices_image, face_features, eps, multiplier,
+                                      boxlen, sigmainv, knum, workspace, need_feat=True):
+    """Gradients (grad_fvi, grad_feat or None) of the fused forward, from its workspace."""
+    dev = face_idx.device
+    B, F = face_vertices_image.shape[:2]
+    H, W = face_idx.shape[1:3]
+    D = face_features.shape[-1]
+    sfx = _sfx(face_vertices_image, 'dibr_rasterization_backward')
+    gfvi = torch.empty_like(face_vertices_image)
+    gfeat = torch.empty_like(face_features) if need_feat else None
+    c = (lambda t: None if t is None else t.contiguous())  # noqa: E731
+    _lib.call(f'kd_dibr_rasterization_backward_{sfx}', B, H, W, F, D, _ptr(c(grad_interp)),
+              _ptr(c(grad_soft)), _ptr(face_idx), _ptr(weights), _ptr(soft),
+              _ptr(face_vertices_image), _ptr(face_features), float(eps), float(multiplier),
+              float(boxlen), float(sigmainv), int(knum), _ptr(gfvi), _ptr(gfeat),
+              _ptr(workspace), workspace.numel(), _stream(dev))
+    return gfvi, gfeat
+
+
 render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
     rasterize_backward_cuda=rasterize_backward_cuda,
@@ -386,4 +464,8 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     rasterize_backward_autograd=rasterize_backward_autograd,
     dibr_soft_mask_forward_fused=dibr_soft_mask_forward_fused,
     dibr_soft_mask_backward_binned=dibr_soft_mask_backward_binned,
+    dibr_rasterization_forward_fused=dibr_rasterization_forward_fused,
+    dibr_rasterization_backward_fused=dibr_rasterization_backward_fused,
+    prepare_vertices_forward=prepare_vertices_forward,
+    prepare_vertices_backward=prepare_vertices_backward,
 ))

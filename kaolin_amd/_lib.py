@@ -38,6 +38,12 @@ _SIGS = {
                                         c_p, c_size, c_p],
     'kd_dibr_soft_mask_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
                                    c_p, c_p, c_float, c_float, c_p, c_p],
+    'kd_dibr_rasterization_forward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_i64, c_i64, c_p,
+                                      c_p, c_p, c_i64, c_double, c_float, c_float, c_double,
+                                      c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_size, c_p],
+    'kd_dibr_rasterization_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,
+                                       c_p, c_p, c_p, c_float, c_double, c_double, c_float,
+                                       c_int, c_p, c_p, c_p, c_size, c_p],
     'kd_prepare_vertices_forward': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p,
                                     c_p, c_p],
     'kd_prepare_vertices_backward': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p,
@@ -64,6 +70,8 @@ def load():
             lib.kd_workspace_size.restype = c_size
             lib.kd_soft_mask_workspace_size.argtypes = [c_int, c_int, c_int, c_i64, c_int, c_int]
             lib.kd_soft_mask_workspace_size.restype = c_size
+            lib.kd_dibr_workspace_size.argtypes = [c_int, c_int, c_int, c_i64, c_int, c_int]
+            lib.kd_dibr_workspace_size.restype = c_size
             lib.kd_last_error.argtypes = []
             lib.kd_last_error.restype = ctypes.c_char_p
             lib.kd_version.restype = c_int

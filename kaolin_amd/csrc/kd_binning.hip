@@ -110,7 +110,15 @@ __device__ void raster_cull_coefs(const float v[6], float M, int H, int W, Span 
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_bin_count(FaceSet<T> fs, BinBuffers bb) {
+struct BinJobs {
+  FaceSet<T> fs[2];
+  BinBuffers bb[2];
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
+  const FaceSet<T> &fs = jobs.fs[blockIdx.z];
+  const BinBuffers &bb = jobs.bb[blockIdx.z];
   __shared__ int s_cnt[kMaxCtiles];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(FaceSet<T> fs, BinBuffers
   __syncthreads();
   if (i < hi) {
     Span s;
-    const bool ok = !fs.valid || fs.valid[i];
+    const bool ok = (!fs.valid || fs.valid[i]) && (!fs.nz || fs.nz[i * fs.nz_stride] >= (T)0);
     if (ok) {
       T v[6], box[4];
       load_corners(fs, i, v);
@@ -158,8 +166,9 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(FaceSet<T> fs, BinBuffers
 // One workgroup per (coarse tile, view): exclusive scan of counts[b][*][c] over the chunks.
 // Each thread owns a contiguous run of chunks; the run sums are scanned with DPP inside each
 // wave and across the 4 waves through LDS (kd_tile.hpp wg_exclusive_scan, one barrier pair).
-__global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb, int B) {
+__global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers bb1) {
   __shared__ int s_w[4];
+  const BinBuffers &bb = blockIdx.z ? bb1 : bb0;
   const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int nct = bb.g.nct();
   const int n = bb.nchunk;
@@ -206,7 +215,9 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb, int B) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_bin_scatter(FaceSet<T> fs, BinBuffers bb) {
+__global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
+  const FaceSet<T> &fs = jobs.fs[blockIdx.z];
+  const BinBuffers &bb = jobs.bb[blockIdx.z];
   // 256-bit membership mask per coarse tile: bit t set <=> face (chunk*256 + t) touches it.
   extern __shared__ uint32_t s_mask[];  // [nct][8]
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
@@ -249,33 +260,98 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(FaceSet<T> fs, BinBuffe
 }
 
 template <typename T>
-hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t stream) {
+static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream) {
+  const FaceSet<T> &fs = jobs.fs[0];
+  const BinBuffers &bb = jobs.bb[0];
   if (bb.nchunk <= 0 || fs.B <= 0) {
     // no faces: totals (and the counters kd_bin_count would clear) must still read zero
-    if (bb.clear && bb.n_clear > 0) {
-      const hipError_t e = hipMemsetAsync(bb.clear, 0, sizeof(int) * bb.n_clear, stream);
+    for (int j = 0; j < njobs; ++j) {
+      const BinBuffers &b = jobs.bb[j];
+      if (b.clear && b.n_clear > 0) {
+        const hipError_t e = hipMemsetAsync(b.clear, 0, sizeof(int) * b.n_clear, stream);
+        if (e != hipSuccess) return e;
+      }
+      const hipError_t e = hipMemsetAsync(
+          b.totals, 0, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * b.g.nct(), stream);
       if (e != hipSuccess) return e;
     }
-    return hipMemsetAsync(bb.totals, 0, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * bb.g.nct(),
-                          stream);
+    return hipSuccess;
   }
-  const dim3 grid_c(bb.nchunk, fs.B), grid_t(bb.g.nct(), fs.B);
+  const dim3 grid_c(bb.nchunk, fs.B, njobs), grid_t(bb.g.nct(), fs.B, njobs);
   {
     ProfScope prof(K_BIN_COUNT, stream);
-    hipLaunchKernelGGL(kd_bin_count<T>, grid_c, dim3(kBlock), 0, stream, fs, bb);
+    hipLaunchKernelGGL(kd_bin_count<T>, grid_c, dim3(kBlock), 0, stream, jobs);
   }
   {
     ProfScope prof(K_BIN_SCAN, stream);
-    hipLaunchKernelGGL(kd_bin_scan, grid_t, dim3(kBlock), 0, stream, bb, fs.B);
+    hipLaunchKernelGGL(kd_bin_scan, grid_t, dim3(kBlock), 0, stream, jobs.bb[0],
+                       jobs.bb[njobs - 1]);
   }
   {
     ProfScope prof(K_BIN_SCATTER, stream);
     hipLaunchKernelGGL(kd_bin_scatter<T>, grid_c, dim3(kBlock),
-                       sizeof(uint32_t) * 8 * bb.g.nct(), stream, fs, bb);
+                       sizeof(uint32_t) * 8 * bb.g.nct(), stream, jobs);
   }
   return hipGetLastError();
 }
 
+template <typename T>
+hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t stream) {
+  BinJobs<T> jobs;
+  jobs.fs[0] = jobs.fs[1] = fs;
+  jobs.bb[0] = jobs.bb[1] = bb;
+  return bin_jobs<T>(jobs, 1, stream);
+}
+
+template <typename T>
+hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSet<T> &fs1,
+                      const BinBuffers &bb1, hipStream_t stream) {
+  // both sets must describe the same views, faces and image (same chunking and tile grid)
+  if (fs0.B != fs1.B || fs0.N != fs1.N || fs0.H != fs1.H || fs0.W != fs1.W ||
+      bb0.nchunk != bb1.nchunk || bb0.g.nct() != bb1.g.nct())
+    return hipErrorInvalidValue;
+  BinJobs<T> jobs;
+  jobs.fs[0] = fs0;
+  jobs.fs[1] = fs1;
+  jobs.bb[0] = bb0;
+  jobs.bb[1] = bb1;
+  return bin_jobs<T>(jobs, 2, stream);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_zero2(T *p0, int64_t n0, T *p1, int64_t n1) {
+  const int64_t n = n0 + n1;
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (i < n0)
+      p0[i] = (T)0;
+    else
+      p1[i - n0] = (T)0;
+  }
+}
+
+template <typename T>
+int zero_buffers(T *p0, int64_t n0, T *p1, int64_t n1, hipStream_t stream) {
+  if (!p0) n0 = 0;
+  if (!p1) n1 = 0;
+  const int64_t n = n0 + n1;
+  if (n == 0) return KD_OK;
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 2048);
+  {
+    ProfScope prof(K_ZERO, stream);
+    hipLaunchKernelGGL(kd_zero2<T>, dim3(blocks), dim3(kBlock), 0, stream, p0, n0, p1, n1);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "zero: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template hipError_t bin_faces2<float>(const FaceSet<float> &, const BinBuffers &,
+                                      const FaceSet<float> &, const BinBuffers &, hipStream_t);
+template hipError_t bin_faces2<double>(const FaceSet<double> &, const BinBuffers &,
+                                       const FaceSet<double> &, const BinBuffers &, hipStream_t);
+template int zero_buffers<float>(float *, int64_t, float *, int64_t, hipStream_t);
+template int zero_buffers<double>(double *, int64_t, double *, int64_t, hipStream_t);
 template hipError_t bin_faces<float>(const FaceSet<float> &, const BinBuffers &, hipStream_t);
 template hipError_t bin_faces<double>(const FaceSet<double> &, const BinBuffers &, hipStream_t);
 

@@ -50,6 +50,15 @@ BinBuffers bin_carve(void *ws, size_t &offset, int B, int H, int W, int64_t N,
 
 template <typename T>
 hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t stream);
+// Two face sets of the same views and image (e.g. the raster's and the soft mask's boxes) binned
+// by the same three launches (blockIdx.z selects the set).
+template <typename T>
+hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSet<T> &fs1,
+                      const BinBuffers &bb1, hipStream_t stream);
+
+// Zeroes n0 elements at p0 and n1 at p1 (either may be null / 0) in one launch.
+template <typename T>
+int zero_buffers(T *p0, int64_t n0, T *p1, int64_t n1, hipStream_t stream);
 
 inline size_t align_up(size_t x, size_t a = 256) { return (x + a - 1) / a * a; }
 

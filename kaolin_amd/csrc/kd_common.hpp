@@ -209,6 +209,8 @@ struct FaceSet {
   T margin;                  // computed box enlarged by +-margin when has_margin
   int has_margin;
   const uint8_t *valid;      // (N) uint8 or nullptr
+  const T *nz;               // or: face i valid iff nz[i * nz_stride] >= 0 (normals z), nullable
+  int64_t nz_stride;
   float M;                   // float multiplier of the pixel centres
   int dbg;                   // diagnostic ablation flags (0 in production)
   long long *tbuf;           // diagnostic per-tile clock buffer (nullptr in production)

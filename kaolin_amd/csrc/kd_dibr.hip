@@ -1,0 +1,198 @@
+// kd_dibr.hip -- dibr_rasterization (kaolin/render/mesh/dibr.py:119-209) as one forward and one
+// backward launch sequence.
+//
+// The reference composes rasterize (valid faces = face_normals_z >= 0, dibr.py:195) and
+// dibr_soft_mask (all faces, dibr.py:201-208) as two autograd functions.  Fused here:
+//   forward   one binning pass for both face sets (the raster's tight boxes of the valid faces
+//             and the soft mask's enlarged boxes of all faces: kd_binning bin_faces2), the
+//             raster kernel, then the soft-mask pair pipeline on its face_idx.  face_vertices_z
+//             and face_normals_z are read through strides, so views of prepare_vertices'
+//             outputs need no copies.
+//   backward  one zero fill for both gradients, the raster backward and the soft-mask backward
+//             accumulating into the same grad_fvi (no separate buffers and no sum kernel).
+// Results are exactly those of rasterize + dibr_soft_mask.
+#include "../../include/kaolin_dibr.h"
+#include "kd_raster.hpp"
+#include "kd_soft.hpp"
+
+namespace kd {
+
+size_t dibr_workspace_bytes(int B, int H, int W, int64_t F, int K, int esize) {
+  const int64_t N = (int64_t)B * F;
+  return bin_workspace_bytes(B, H, W, N, F) + soft_pair_workspace_bytes(B, H, W, N, F, K, esize);
+}
+
+template <typename T>
+struct DibrBuffers {
+  BinBuffers rbb;      // raster bins (+ cull coefficients)
+  BinBuffers sbb;      // soft-mask bins
+  SoftPairBuf<T> pb;   // soft-mask records
+};
+
+template <typename T>
+static DibrBuffers<T> dibr_carve(void *ws, int B, int H, int W, int64_t F, int K) {
+  const int64_t N = (int64_t)B * F;
+  DibrBuffers<T> d;
+  size_t off = 0;
+  d.rbb = bin_carve(ws, off, B, H, W, N, F);
+  d.sbb = bin_carve(ws, off, B, H, W, N, F);  // soft_pair_workspace_bytes starts with these bins
+  d.pb = soft_pair_carve<T>(ws, off, B, H, W, K);
+  return d;
+}
+
+template <typename T>
+static FaceSet<T> dibr_faceset(int B, int H, int W, int64_t F, const T *fvi, double M) {
+  FaceSet<T> fs{};
+  fs.B = B;
+  fs.H = H;
+  fs.W = W;
+  fs.N = (int64_t)B * F;
+  fs.F = F;
+  fs.fvi = fvi;
+  fs.scale = (T)M;
+  fs.M = (float)M;
+  return fs;
+}
+
+template <typename T>
+static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t fvz_fs,
+                    int64_t fvz_cs, const T *fvi, const T *feat, const T *nz, int64_t nz_stride,
+                    double M, float eps, float sigmainv, double boxlen, int K, T *interp,
+                    int64_t *face_idx, T *weights, T *soft, int want_grad, void *ws,
+                    size_t wsb, void *stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
+  KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
+  KD_CHECK_ARG(H < 32768 && W < 32768, "image side must be < 32768");
+  KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
+  KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
+  const size_t need = dibr_workspace_bytes(B, H, W, F, K, sizeof(T));
+  if (wsb < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
+  if (B == 0 || H == 0 || W == 0) return KD_OK;
+  DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
+  // raster: valid faces (normals z >= 0, dibr.py:195), tight boxes; soft: all faces, +-boxlen*M
+  FaceSet<T> rfs = dibr_faceset<T>(B, H, W, F, fvi, M);
+  rfs.nz = nz;
+  rfs.nz_stride = nz_stride;
+  FaceSet<T> sfs = dibr_faceset<T>(B, H, W, F, fvi, M);
+  sfs.margin = (T)(boxlen * M);
+  sfs.has_margin = 1;
+  if (!raster_uses_cull<T>()) d.rbb.cull = nullptr;
+  d.rbb.cull_eps = eps;
+  d.sbb.cull = nullptr;
+  d.sbb.clear = d.pb.counters;
+  d.sbb.n_clear = 2;
+  hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream);
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
+  RasterFwdArgs<T> ra{rfs, d.rbb, fvz, fvz_fs, fvz_cs, feat, D, eps, interp, face_idx, weights};
+  int rc = raster_launch<T>(ra, stream);
+  if (rc != KD_OK) return rc;
+  SoftArgs<T> sa{};
+  sa.fs = sfs;
+  sa.bb = d.sbb;
+  sa.face_idx = face_idx;
+  sa.K = K;
+  sa.sigmainv = sigmainv;
+  sa.soft = soft;
+  return soft_pairs_launch<T>(sa, d.pb, want_grad != 0, true, stream);
+}
+
+template <typename T>
+static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
+                    const T *grad_soft, const int64_t *face_idx, const T *weights, const T *soft,
+                    const T *fvi, const T *feat, float eps, double M, double boxlen,
+                    float sigmainv, int K, T *gfvi, T *gfeat, void *ws, size_t wsb,
+                    void *stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
+  KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
+  KD_CHECK_ARG(gfvi, "grad_fvi is NULL");
+  const size_t need = dibr_workspace_bytes(B, H, W, F, K, sizeof(T));
+  if (wsb < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
+  const int64_t nf = (int64_t)B * F;
+  int rc = zero_buffers<T>(gfvi, nf * 6, gfeat, gfeat ? nf * 3 * D : 0, stream);
+  if (rc != KD_OK || B == 0 || H == 0 || W == 0) return rc;
+  if (grad_interp) {
+    rc = raster_backward_launch<T>(B, H, W, F, D, grad_interp, face_idx, weights, fvi, feat, eps,
+                                   gfvi, gfeat, stream);
+    if (rc != KD_OK) return rc;
+  }
+  if (grad_soft) {
+    DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
+    SoftArgs<T> sa{};
+    sa.fs = dibr_faceset<T>(B, H, W, F, fvi, M);
+    sa.fs.margin = (T)(boxlen * M);
+    sa.fs.has_margin = 1;
+    sa.bb = d.sbb;
+    sa.face_idx = face_idx;
+    sa.K = K;
+    sa.sigmainv = sigmainv;
+    sa.grad_soft = grad_soft;
+    sa.soft_in = soft;
+    sa.grad_fvi = gfvi;
+    rc = soft_pairs_backward_launch<T>(sa, d.pb, stream);
+  }
+  return rc;
+}
+
+}  // namespace kd
+
+using namespace kd;
+
+extern "C" {
+
+size_t kd_dibr_workspace_size(int B, int H, int W, int64_t F, int knum, int double_precision) {
+  if (B < 0 || H < 0 || W < 0 || F < 0 || knum < 1) return 0;
+  return dibr_workspace_bytes(B, H, W, F, knum, double_precision ? 8 : 4);
+}
+
+int kd_dibr_rasterization_forward_f32(int B, int H, int W, int64_t F, int D, const float *fvz,
+                                      int64_t fvz_face_stride, int64_t fvz_corner_stride,
+                                      const float *fvi, const float *feat,
+                                      const float *normals_z, int64_t normals_z_stride, double M,
+                                      float eps, float sigmainv, double boxlen, int knum,
+                                      float *interp, int64_t *face_idx, float *weights,
+                                      float *soft, int want_grad, void *ws, size_t wsb,
+                                      void *stream) {
+  return dibr_fwd<float>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
+                         normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
+                         face_idx, weights, soft, want_grad, ws, wsb, stream);
+}
+int kd_dibr_rasterization_forward_f64(int B, int H, int W, int64_t F, int D, const double *fvz,
+                                      int64_t fvz_face_stride, int64_t fvz_corner_stride,
+                                      const double *fvi, const double *feat,
+                                      const double *normals_z, int64_t normals_z_stride,
+                                      double M, float eps, float sigmainv, double boxlen,
+                                      int knum, double *interp, int64_t *face_idx,
+                                      double *weights, double *soft, int want_grad, void *ws,
+                                      size_t wsb, void *stream) {
+  return dibr_fwd<double>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
+                          normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
+                          face_idx, weights, soft, want_grad, ws, wsb, stream);
+}
+int kd_dibr_rasterization_backward_f32(int B, int H, int W, int64_t F, int D,
+                                       const float *grad_interp, const float *grad_soft,
+                                       const int64_t *face_idx, const float *weights,
+                                       const float *soft, const float *fvi, const float *feat,
+                                       float eps, double M, double boxlen, float sigmainv,
+                                       int knum, float *grad_fvi, float *grad_feat, void *ws,
+                                       size_t wsb, void *stream) {
+  return dibr_bwd<float>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
+                         feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat, ws, wsb,
+                         stream);
+}
+int kd_dibr_rasterization_backward_f64(int B, int H, int W, int64_t F, int D,
+                                       const double *grad_interp, const double *grad_soft,
+                                       const int64_t *face_idx, const double *weights,
+                                       const double *soft, const double *fvi,
+                                       const double *feat, float eps, double M, double boxlen,
+                                       float sigmainv, int knum, double *grad_fvi,
+                                       double *grad_feat, void *ws, size_t wsb, void *stream) {
+  return dibr_bwd<double>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
+                          feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat, ws, wsb,
+                          stream);
+}
+
+}  // extern "C"

@@ -18,24 +18,13 @@
 #include "../../include/kaolin_dibr.h"
 #include "kd_binning.hpp"
 #include "kd_capi.hpp"
+#include "kd_raster.hpp"
 #include "kd_tile.hpp"
 
 #include <type_traits>
 
 namespace kd {
 
-template <typename T>
-struct RasterFwdArgs {
-  FaceSet<T> fs;
-  BinBuffers bb;
-  const T *fvz;
-  const T *feat;
-  int D;
-  float eps;
-  T *interp;
-  int64_t *face_idx;
-  T *weights;
-};
 
 template <typename T>
 struct ScaleUp {  // 2^(-min normal exponent): |w| * value >= |norm| => |w / norm| >= min normal
@@ -104,10 +93,10 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
     load_corners(fs, fi, v);
 #pragma unroll
     for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
-    const T *zz = a.fvz + fi * 3;
+    const T *zz = a.fvz + fi * a.fvz_fs;
     s_geo[6][k] = zz[0];
-    s_geo[7][k] = zz[1];
-    s_geo[8][k] = zz[2];
+    s_geo[7][k] = zz[a.fvz_cs];
+    s_geo[8][k] = zz[2 * a.fvz_cs];
   };
   auto round = [&](int nsub, int) {
     if (nsub == 0 || (fs.dbg & 1)) return;
@@ -217,10 +206,10 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
     load_corners(fs, fi, v);
 #pragma unroll
     for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
-    const float *zz = a.fvz + fi * 3;
+    const float *zz = a.fvz + fi * a.fvz_fs;
     s_geo[6][k] = zz[0];
-    s_geo[7][k] = zz[1];
-    s_geo[8][k] = zz[2];
+    s_geo[7][k] = zz[a.fvz_cs];
+    s_geo[8][k] = zz[2 * a.fvz_cs];
     s_cull[0][k] = a.bb.cull[2 * fi];
     s_cull[1][k] = a.bb.cull[2 * fi + 1];
   };
@@ -323,10 +312,10 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
       if (!pspan_has(pack_span(a.bb.spans[lo + f]), t.px, t.py)) continue;
       float v[6];
       load_corners(fs, lo + f, v);
-      const float *zz = a.fvz + (lo + f) * 3;
+      const float *zz = a.fvz + (lo + f) * a.fvz_fs;
       float w0, w1, w2, z0;
-      if (!raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[1],
-                                   zz[2], a.eps, w0, w1, w2, z0))
+      if (!raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0],
+                                   zz[a.fvz_cs], zz[2 * a.fvz_cs], a.eps, w0, w1, w2, z0))
         continue;
       if (z0 <= max_z0) continue;
       max_z0 = z0;
@@ -339,10 +328,10 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
     best = (int)(0xffffffffu - (uint32_t)(s_key[w][lane] & 0xffffffffull));
     float v[6];
     load_corners(fs, lo + best, v);
-    const float *zz = a.fvz + (lo + best) * 3;
+    const float *zz = a.fvz + (lo + best) * a.fvz_fs;
     float z0;
-    raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[1], zz[2],
-                            a.eps, bw0, bw1, bw2, z0);
+    raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[a.fvz_cs],
+                            zz[2 * a.fvz_cs], a.eps, bw0, bw1, bw2, z0);
   }
   a.face_idx[p] = best;
   float *wo = a.weights + p * 3;
@@ -567,6 +556,33 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
 // host launchers
 // ------------------------------------------------------------------------------------------
 template <typename T>
+bool raster_uses_cull() {
+  return std::is_same<T, float>::value && !(debug_flags() & 8);
+}
+
+template <typename T>
+int raster_launch(RasterFwdArgs<T> &a, hipStream_t stream) {
+  const FaceSet<T> &fs = a.fs;
+  a.fs.dbg = debug_flags();
+  a.fs.tbuf = debug_tile_buffer();
+  const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
+  {
+    ProfScope prof(K_RASTER_FWD, stream);
+    if constexpr (std::is_same<T, float>::value) {
+      if (a.bb.cull)
+        hipLaunchKernelGGL(kd_raster_fwd_pairs, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+      else
+        hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+    } else {
+      hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+    }
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster fwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template <typename T>
 int raster_forward(const FaceSet<T> &fs, int64_t max_per_view, const T *fvz, const T *feat,
                    int D, float eps, T *interp, int64_t *face_idx, T *weights, void *ws,
                    size_t ws_bytes, hipStream_t stream) {
@@ -576,42 +592,20 @@ int raster_forward(const FaceSet<T> &fs, int64_t max_per_view, const T *fvz, con
   if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
   size_t off = 0;
   BinBuffers bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, max_per_view);
-  const int dbg = debug_flags();
-  const bool pairs = std::is_same<T, float>::value && !(dbg & 8);
-  if (!pairs) bb.cull = nullptr;
+  if (!raster_uses_cull<T>()) bb.cull = nullptr;
   bb.cull_eps = eps;
   hipError_t e = bin_faces<T>(fs, bb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
-  RasterFwdArgs<T> a{fs, bb, fvz, feat, D, eps, interp, face_idx, weights};
-  a.fs.dbg = dbg;
-  a.fs.tbuf = debug_tile_buffer();
-  const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
-  {
-    ProfScope prof(K_RASTER_FWD, stream);
-    if constexpr (std::is_same<T, float>::value) {
-      if (pairs)
-        hipLaunchKernelGGL(kd_raster_fwd_pairs, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-      else
-        hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-    } else {
-      hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-    }
-  }
-  e = hipGetLastError();
-  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster fwd: %s", hipGetErrorString(e));
-  return KD_OK;
+  RasterFwdArgs<T> a{fs, bb, fvz, 3, 1, feat, D, eps, interp, face_idx, weights};
+  return raster_launch<T>(a, stream);
 }
 
+// The tile kernel only (gfvi / gfeat must hold zeros or partial sums to add to).
 template <typename T>
-int raster_backward(int B, int H, int W, int64_t F, int D, const T *grad, const int64_t *fidx,
-                    const T *weights, const T *fvi, const T *feat, float eps, T *gfvi, T *gfeat,
-                    hipStream_t stream) {
+int raster_backward_launch(int B, int H, int W, int64_t F, int D, const T *grad,
+                           const int64_t *fidx, const T *weights, const T *fvi, const T *feat,
+                           float eps, T *gfvi, T *gfeat, hipStream_t stream) {
   const int64_t nf = (int64_t)B * F;
-  if (nf > 0) {
-    hipError_t e = hipMemsetAsync(gfvi, 0, sizeof(T) * nf * 6, stream);
-    if (e == hipSuccess && gfeat) e = hipMemsetAsync(gfeat, 0, sizeof(T) * nf * 3 * D, stream);
-    if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
-  }
   const int64_t total = (int64_t)B * H * W;
   if (total > 0 && nf > 0) {
     const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
@@ -635,6 +629,31 @@ int raster_backward(int B, int H, int W, int64_t F, int D, const T *grad, const 
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster bwd: %s", hipGetErrorString(e));
   return KD_OK;
 }
+
+template <typename T>
+int raster_backward(int B, int H, int W, int64_t F, int D, const T *grad, const int64_t *fidx,
+                    const T *weights, const T *fvi, const T *feat, float eps, T *gfvi, T *gfeat,
+                    hipStream_t stream) {
+  const int64_t nf = (int64_t)B * F;
+  if (nf > 0) {
+    const int rc = zero_buffers<T>(gfvi, nf * 6, gfeat, gfeat ? nf * 3 * D : 0, stream);
+    if (rc != KD_OK) return rc;
+  }
+  return raster_backward_launch<T>(B, H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi,
+                                   gfeat, stream);
+}
+
+template bool raster_uses_cull<float>();
+template bool raster_uses_cull<double>();
+template int raster_launch<float>(RasterFwdArgs<float> &, hipStream_t);
+template int raster_launch<double>(RasterFwdArgs<double> &, hipStream_t);
+template int raster_backward_launch<float>(int, int, int, int64_t, int, const float *,
+                                           const int64_t *, const float *, const float *,
+                                           const float *, float, float *, float *, hipStream_t);
+template int raster_backward_launch<double>(int, int, int, int64_t, int, const double *,
+                                            const int64_t *, const double *, const double *,
+                                            const double *, float, double *, double *,
+                                            hipStream_t);
 
 }  // namespace kd
 

@@ -208,6 +208,17 @@ struct SoftPairBuf {
 
 // bins + pair buffers for B views of F faces, K close faces, element size esize
 size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize);
+// pair buffers carved from a workspace after the soft mask's bins
+template <typename T>
+SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K);
+// pass A + pair math (+ backward coefficients when grad) + (when reduce) the soft mask, over
+// already built bins (a.bb) whose kd_bin_count cleared pb.counters
+template <typename T>
+int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce,
+                      hipStream_t stream);
+// the backward over the records of soft_pairs_launch(grad = true), adding into a.grad_fvi
+template <typename T>
+int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream);
 // bins + pass A + pair math (+ backward coefficients when grad) + (when reduce) the soft mask
 template <typename T>
 int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, bool reduce,

@@ -434,23 +434,11 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_pairs(SoftArgs<T> a, SoftP
 // host launchers
 // ------------------------------------------------------------------------------------------
 template <typename T>
-int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, bool reduce,
-                       hipStream_t stream) {
+int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce,
+                      hipStream_t stream) {
   const FaceSet<T> &fs = a.fs;
-  const size_t need = soft_pair_workspace_bytes(fs.B, fs.H, fs.W, fs.N, fs.F, a.K, sizeof(T));
-  if (ws_bytes < need || (need && !ws))
-    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", ws_bytes, need);
-  if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
-  size_t off = 0;
-  a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
-  a.bb.cull = nullptr;
-  SoftPairBuf<T> pb = soft_pair_carve<T>(ws, off, fs.B, fs.H, fs.W, a.K);
-  a.bb.clear = pb.counters;
-  a.bb.n_clear = 2;
   a.fs.dbg = debug_flags();
   a.fs.tbuf = debug_tile_buffer();
-  hipError_t e = bin_faces<T>(fs, a.bb, stream);
-  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   {
     ProfScope prof(K_SOFT_PAIRS, stream);
     hipLaunchKernelGGL(kd_soft_pairs<T>, dim3((unsigned)pb.ntiles, fs.B), dim3(kBlock), 0, stream,
@@ -474,8 +462,41 @@ int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, boo
     ProfScope prof(K_SOFT_REDUCE, stream);
     hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a, pb);
   }
-  e = hipGetLastError();
+  const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template <typename T>
+int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, bool reduce,
+                       hipStream_t stream) {
+  const FaceSet<T> &fs = a.fs;
+  const size_t need = soft_pair_workspace_bytes(fs.B, fs.H, fs.W, fs.N, fs.F, a.K, sizeof(T));
+  if (ws_bytes < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", ws_bytes, need);
+  if (fs.B == 0 || fs.H == 0 || fs.W == 0) return KD_OK;
+  size_t off = 0;
+  a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
+  a.bb.cull = nullptr;
+  SoftPairBuf<T> pb = soft_pair_carve<T>(ws, off, fs.B, fs.H, fs.W, a.K);
+  a.bb.clear = pb.counters;
+  a.bb.n_clear = 2;
+  hipError_t e = bin_faces<T>(fs, a.bb, stream);
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
+  return soft_pairs_launch<T>(a, pb, grad, reduce, stream);
+}
+
+template <typename T>
+int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream) {
+  a.fs.dbg = debug_flags();
+  a.fs.tbuf = debug_tile_buffer();
+  {
+    ProfScope prof(K_SOFT_BWD_PAIRS, stream);
+    hipLaunchKernelGGL(kd_soft_bwd_pairs<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a,
+                       pb);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
   return KD_OK;
 }
 
@@ -489,18 +510,19 @@ int soft_pairs_backward(SoftArgs<T> &a, void *ws, size_t ws_bytes, hipStream_t s
   size_t off = 0;
   a.bb = bin_carve(ws, off, fs.B, fs.H, fs.W, fs.N, fs.F);
   SoftPairBuf<T> pb = soft_pair_carve<T>(ws, off, fs.B, fs.H, fs.W, a.K);
-  a.fs.dbg = debug_flags();
-  a.fs.tbuf = debug_tile_buffer();
-  {
-    ProfScope prof(K_SOFT_BWD_PAIRS, stream);
-    hipLaunchKernelGGL(kd_soft_bwd_pairs<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a,
-                       pb);
-  }
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
-  return KD_OK;
+  return soft_pairs_backward_launch<T>(a, pb, stream);
 }
 
+template SoftPairBuf<float> soft_pair_carve<float>(void *, size_t &, int, int, int, int);
+template SoftPairBuf<double> soft_pair_carve<double>(void *, size_t &, int, int, int, int);
+template int soft_pairs_launch<float>(SoftArgs<float> &, SoftPairBuf<float> &, bool, bool,
+                                      hipStream_t);
+template int soft_pairs_launch<double>(SoftArgs<double> &, SoftPairBuf<double> &, bool, bool,
+                                       hipStream_t);
+template int soft_pairs_backward_launch<float>(SoftArgs<float> &, SoftPairBuf<float> &,
+                                               hipStream_t);
+template int soft_pairs_backward_launch<double>(SoftArgs<double> &, SoftPairBuf<double> &,
+                                                hipStream_t);
 template int soft_pairs_forward<float>(SoftArgs<float> &, void *, size_t, bool, bool,
                                        hipStream_t);
 template int soft_pairs_forward<double>(SoftArgs<double> &, void *, size_t, bool, bool,

@@ -76,15 +76,72 @@ def dibr_soft_mask(face_vertices_image, selected_face_idx, sigmainv=7000, boxlen
                                   multiplier)
 
 
+class DibrRasterizationHip(Function):
+    """Fused dibr_rasterization (kd_dibr.hip): one binning pass for the raster and the soft
+    mask, one backward writing both gradients into one buffer.  Same results as
+    rasterize + dibr_soft_mask."""
+
+    @staticmethod
+    def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features,
+                face_normals_z, sigmainv, boxlen, knum, multiplier, eps):
+        want_grad = face_vertices_image.requires_grad or face_features.requires_grad
+        interp, face_idx, weights, soft, ws = _C.render.mesh.dibr_rasterization_forward_fused(
+            height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z,
+            sigmainv, boxlen, knum, multiplier, eps, want_grad=want_grad)
+        ctx.save_for_backward(face_idx, weights, soft, face_vertices_image, face_features)
+        ctx.workspace = ws if want_grad else None
+        ctx.params = (eps, multiplier, boxlen, sigmainv, knum)
+        ctx.mark_non_differentiable(face_idx)
+        ctx.set_materialize_grads(False)
+        return interp, soft, face_idx
+
+    @staticmethod
+    def backward(ctx, grad_interp, grad_soft, grad_face_idx):
+        need_fvi, need_feat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+        if not (need_fvi or need_feat) or (grad_interp is None and grad_soft is None):
+            return (None,) * 11
+        face_idx, weights, soft, fvi, feat = ctx.saved_tensors
+        eps, multiplier, boxlen, sigmainv, knum = ctx.params
+        gfvi, gfeat = _C.render.mesh.dibr_rasterization_backward_fused(
+            grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier, boxlen,
+            sigmainv, knum, ctx.workspace, need_feat=need_feat)
+        ctx.workspace = None
+        return (None, None, None, gfvi if need_fvi else None, gfeat, None, None, None, None,
+                None, None)
+
+
 def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face_features,
                        face_normals_z, sigmainv=7000, boxlen=0.02, knum=30, multiplier=None,
                        eps=None, rast_backend='cuda'):
     r"""DIB-R renderer (dibr.py:119-209): rasterize the front faces (normal z >= 0), then the
-    soft mask over all faces.  Returns (interpolated_features, soft_mask, face_idx)."""
-    interpolated_features, face_idx = rasterize(
-        height, width, face_vertices_z, face_vertices_image, face_features,
-        face_normals_z >= 0., multiplier, eps, rast_backend)
+    soft mask over all faces.  Returns (interpolated_features, soft_mask, face_idx).
+
+    Runs as one fused forward / backward (DibrRasterizationHip); with ``SAVE_CLOSE_LISTS`` it is
+    the reference composition of ``rasterize`` and ``dibr_soft_mask`` instead."""
+    if rast_backend != 'cuda':
+        raise ValueError(f'"{rast_backend}" is not a valid backend, valid choices are ["cuda"] '
+                         '(nvdiffrast is not available on MI355X)')
     _multiplier = 1000. if multiplier is None else multiplier
-    soft_mask = dibr_soft_mask(face_vertices_image, face_idx, sigmainv, boxlen, knum,
-                               _multiplier)
-    return interpolated_features, soft_mask, face_idx
+    if SAVE_CLOSE_LISTS:
+        interpolated_features, face_idx = rasterize(
+            height, width, face_vertices_z, face_vertices_image, face_features,
+            face_normals_z >= 0., multiplier, eps, rast_backend)
+        soft_mask = dibr_soft_mask(face_vertices_image, face_idx, sigmainv, boxlen, knum,
+                                   _multiplier)
+        return interpolated_features, soft_mask, face_idx
+    _eps = 1e-8 if eps is None else eps
+    _rmult = 1000 if multiplier is None else multiplier  # rasterize's default (an int)
+    if float(_rmult) != float(_multiplier):
+        raise RuntimeError('internal: multiplier defaults disagree')
+    feats = torch.cat(face_features, dim=-1) \
+        if isinstance(face_features, (list, tuple)) else face_features
+    interp, soft, face_idx = DibrRasterizationHip.apply(
+        height, width, face_vertices_z, face_vertices_image, feats, face_normals_z, sigmainv,
+        boxlen, knum, _multiplier, _eps)
+    if isinstance(face_features, (list, tuple)):
+        out, cur = [], 0
+        for f in face_features:
+            out.append(interp[..., cur:cur + f.shape[-1]])
+            cur += f.shape[-1]
+        interp = tuple(out)
+    return interp, soft, face_idx

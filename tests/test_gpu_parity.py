@@ -533,3 +533,39 @@ def test_prepare_vertices_rot_trans_and_camera_grad():
     fvc, fvi, n = prepare_vertices(v, faces, proj, camera_transform=tf)
     fvi.sum().backward()
     assert tf.grad is not None
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_dibr_rasterization_fused_matches_composition(dname):
+    """The fused dibr_rasterization (one binning pass, one backward buffer) against rasterize +
+    dibr_soft_mask run separately: identical forward, gradients to summation-order tolerance."""
+    import math
+
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import dibr_rasterization, dibr_soft_mask, prepare_vertices, \
+        rasterize
+    dt = TORCH_DTYPES[dname]
+    verts, faces, uvs = workloads.uv_sphere(40, 21, seed=2)
+    B, h, w = 2, 96, 80
+    cam = workloads.orbit_cameras(B, 0.5).to(DEV, dt)
+    proj = workloads.generate_perspective_projection(math.pi / 4).to(DEV, dt)
+    v = verts.to(DEV, dt).unsqueeze(0)
+    fvc, fvi, nrm = prepare_vertices(v, faces.to(DEV), proj, camera_transform=cam)
+    feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], -1).to(DEV, dt)
+    feats = feats.unsqueeze(0).repeat(B, 1, 1, 1)
+    gen = torch.Generator().manual_seed(5)
+    g1 = torch.rand((B, h, w, 3), generator=gen, dtype=torch.float64).to(DEV, dt)
+    g2 = torch.rand((B, h, w), generator=gen, dtype=torch.float64).to(DEV, dt)
+    fvi_a = fvi.detach().clone().requires_grad_(True)
+    ft_a = feats.clone().requires_grad_(True)
+    i_a, s_a, f_a = dibr_rasterization(h, w, fvc[..., 2], fvi_a, ft_a, nrm[..., 2])
+    torch.autograd.backward([i_a, s_a], [g1, g2])
+    fvi_b = fvi.detach().clone().requires_grad_(True)
+    ft_b = feats.clone().requires_grad_(True)
+    i_b, f_b = rasterize(h, w, fvc[..., 2].contiguous(), fvi_b, ft_b, nrm[..., 2] >= 0)
+    s_b = dibr_soft_mask(fvi_b, f_b)
+    torch.autograd.backward([i_b, s_b], [g1, g2])
+    assert torch.equal(f_a, f_b) and torch.equal(i_a, i_b) and torch.equal(s_a, s_b)
+    tol = dict(rtol=1e-4, atol=1e-5) if dname == 'f32' else dict(rtol=1e-9, atol=1e-10)
+    torch.testing.assert_close(fvi_a.grad, fvi_b.grad, **tol)
+    torch.testing.assert_close(ft_a.grad, ft_b.grad, **tol)
