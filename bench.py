@@ -24,7 +24,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from kaolin_amd import _lib, distributed, workloads  # noqa: E402
+from kaolin_amd import _C, _lib, distributed, workloads  # noqa: E402
 from kaolin_amd.render.mesh import dibr, dibr_rasterization, prepare_vertices  # noqa: E402
 
 METRIC = 'Mpixels/s DIB-R fwd+bwd, 50k-face mesh @512² bs=8, 1/2/4/8 GPU'
@@ -39,24 +39,46 @@ CONFIGS = {
 }
 
 
-def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, esize=4):
-    """Bytes each kernel must move at minimum per launch (every tensor of its contract read or
-    written once), SURVEY.md §8(d) decomposed per kernel.  P pixels, F faces, Fv front faces
-    (raster set), D features, K knum.  Stated in DESIGN.md."""
+def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4):
+    """Bytes each kernel must move at minimum per launch: every tensor of its contract read or
+    written once (SURVEY.md §8(d) decomposed per kernel).  P pixels, F faces
+    (all views), Fv valid (front) faces, D features, K knum, pairs = (pixel, close face) pairs of
+    the soft mask, V vertices.  None where a term is unknown."""
     e = esize
-    if kernel == 'kd_soft_fwd':
-        return P * (8 + e + 4 + (K * (e + 8 + 1) if lists else 0)) + F * 6 * e
-    if kernel == 'kd_raster_fwd':
+    if kernel == 'kd_raster_fwd':      # out: face_idx, weights, interp; in: valid faces' rows
         return P * (8 + 3 * e + D * e) + Fv * (6 * e + 3 * e + 3 * D * e) + F * 1
-    if kernel == 'kd_raster_bwd_tile':   # reads idx, weights, grad; face rows read + added once
+    if kernel == 'kd_raster_bwd_tile':  # in: idx, weights, grad; face rows read + added once
         return P * (8 + 3 * e + D * e) + F * (6 * e + 3 * D * e) * 2
-    if kernel == 'kd_soft_bwd_tile':     # reads idx, grad_soft, soft; corners read, grads added
-        return P * (8 + e + e) + F * 6 * e * 2
-    if kernel == 'kd_bin_count':
-        return F * (6 * e + 1 + 8)
-    if kernel == 'kd_bin_scatter':
-        return F * (8 + 4)
+    if kernel == 'kd_bin_count':       # both face sets: corners (+ normal z) in, spans (+ cull) out
+        return F * (6 * e + e + 8 + 32) + F * (6 * e + 8)
+    if kernel == 'kd_bin_scatter':     # both sets: spans in, >= one bin entry out per face
+        return 2 * F * (8 + 4)
+    if kernel == 'kd_zero':
+        return F * (6 + 3 * D) * e
+    if kernel == 'kd_prepare_fwd':     # vertices + faces in; fvc, fvi, normals out
+        return V * 3 * e + F * (9 + 6 + 3) * e
+    if kernel == 'kd_prepare_bwd':     # fvc + grad_fvi in, vertex grads out
+        return F * (9 + 6) * e + V * 3 * e
+    if pairs is None:
+        return None
+    if kernel == 'kd_soft_pairs':      # face_idx in; records, counts, soft out
+        return P * (8 + 4 + e) + pairs * 12
+    if kernel == 'kd_soft_pair_math':  # records in; probabilities, types, coefficients out
+        return pairs * (12 + e + 1 + 4 * e)
+    if kernel == 'kd_soft_reduce':     # probabilities in, soft out
+        return pairs * e
+    if kernel == 'kd_soft_bwd_pairs':  # records + coefficients, grad/soft in; face grads added
+        return pairs * (12 + 4 * e) + P * 2 * e + F * 6 * e * 2
     return None
+
+
+def survey_step_bytes(P, F, D, K, esize=4):
+    """SURVEY.md §8(d) whole-step formula (K-lists counted as the reference writes them, the
+    N_read term omitted): bytes of one DIB-R fwd+bwd step."""
+    e = esize
+    pix = (8 + 3 * e + D * e) + (8 + e + 13 * K) + (D * e + 8 + 3 * e) + (e + e + 8)
+    face = (e * (3 + 6 + 3 * D) + 4) + 24 + 2 * (24 + 12 * D) + 2 * 24
+    return P * pix + F * face
 
 
 def main():
@@ -153,15 +175,25 @@ def main():
     fv = int((face_idx >= 0).sum().item())  # covered pixels (for the record)
 
     with torch.no_grad():
-        fvc, fvi, nrm = workloads.prepare_vertices(vertices.unsqueeze(0).expand(Bl, -1, -1),
-                                                   faces, proj, cam)
+        fvc, fvi, nrm = prepare_vertices(vertices.unsqueeze(0), faces, proj,
+                                         camera_transform=cam)
         Fv = int((nrm[..., 2] >= 0).sum().item())
     P = Bl * H * W
     Ftot = Bl * F
+    V = vertices.shape[0]
+    pairs = None
+    if not args.lists:
+        with torch.no_grad():
+            _, _, _, _, ws = _C.render.mesh.dibr_rasterization_forward_fused(
+                H, W, fvc[..., 2], fvi, feats, nrm[..., 2], args.sigmainv, args.boxlen,
+                args.knum, 1000., 1e-8, want_grad=True)
+            pairs = int(_lib.load().kd_dibr_pair_count(ws.data_ptr(), Bl, H, W, F, args.knum, 0,
+                                                       torch.cuda.current_stream(dev).cuda_stream))
+            del ws
     kernels = {}
     for name, (ms, n) in prof.items():
         avg_us = ms * 1e3 / n
-        ab = algorithmic_bytes(name, P, Ftot, Fv, D, args.knum, args.lists)
+        ab = algorithmic_bytes(name, P, Ftot, Fv, D, args.knum, args.lists, pairs, V)
         kernels[name] = {'avg_us': round(avg_us, 2), 'launches': n,
                          'share': round(ms / max(sum(v[0] for v in prof.values()), 1e-9), 3)}
         if ab is not None:
@@ -172,7 +204,7 @@ def main():
     if dom is not None:
         ms, n = prof[dom]
         avg_s = ms / n / 1e3
-        ab = algorithmic_bytes(dom, P, Ftot, Fv, D, args.knum, args.lists)
+        ab = algorithmic_bytes(dom, P, Ftot, Fv, D, args.knum, args.lists, pairs, V)
         achieved = ab / avg_s / 1e9 if ab else None
         traffic = None
         if os.path.exists(args.pmc):
@@ -190,6 +222,14 @@ def main():
                     'frac': None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
                     'traffic': traffic,
                     'alg_bytes_per_launch': ab, 'avg_launch_us': round(avg_s * 1e6, 2)}
+
+    sb = survey_step_bytes(P, Ftot, D, args.knum)
+    step_roof = {'formula': 'SURVEY.md §8(d): 482 B/px + 268 B/face at D=3, K=30 (K-lists as '
+                            'the reference writes them, N_read omitted)',
+                 'bytes_per_step_per_gpu': sb,
+                 'achieved': round(sb / (ms_per_step * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
+                 'unit': 'GB/s', 'frac': round(sb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                 'pairs_per_step': pairs}
 
     # ---- CPU baseline: the oracle (C port of the reference kernels), rank 0, N == 1 -------
     cpu = None
@@ -211,6 +251,7 @@ def main():
                    'close_lists': 'materialised' if args.lists else 'not materialised',
                    'covered_px_per_step': fv, 'front_faces': Fv},
         'roofline': roofline,
+        'step_roofline': step_roof,
         'cpu_baseline': cpu,
         'kernels': kernels,
     }

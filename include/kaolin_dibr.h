@@ -217,6 +217,10 @@ int kd_dibr_soft_mask_backward_binned_f64(int batch, int height, int width, int6
  * ------------------------------------------------------------------------------------------- */
 size_t kd_dibr_workspace_size(int batch, int height, int width, int64_t num_faces, int knum,
                               int double_precision);
+/* Diagnostics: number of (pixel, close face) pairs a forward left in `workspace` (synchronises
+ * `stream`, copies the per-tile counts to the host). */
+int64_t kd_dibr_pair_count(const void *workspace, int batch, int height, int width,
+                           int64_t num_faces, int knum, int double_precision, void *stream);
 int kd_dibr_rasterization_forward_f32(int batch, int height, int width, int64_t num_faces,
                                       int feat_dim, const float *fvz, int64_t fvz_face_stride,
                                       int64_t fvz_corner_stride, const float *fvi,

@@ -72,6 +72,8 @@ def load():
             lib.kd_soft_mask_workspace_size.restype = c_size
             lib.kd_dibr_workspace_size.argtypes = [c_int, c_int, c_int, c_i64, c_int, c_int]
             lib.kd_dibr_workspace_size.restype = c_size
+            lib.kd_dibr_pair_count.argtypes = [c_p, c_int, c_int, c_int, c_i64, c_int, c_int, c_p]
+            lib.kd_dibr_pair_count.restype = c_i64
             lib.kd_last_error.argtypes = []
             lib.kd_last_error.restype = ctypes.c_char_p
             lib.kd_version.restype = c_int

@@ -15,6 +15,8 @@
 #include "kd_raster.hpp"
 #include "kd_soft.hpp"
 
+#include <vector>
+
 namespace kd {
 
 size_t dibr_workspace_bytes(int B, int H, int W, int64_t F, int K, int esize) {
@@ -146,6 +148,24 @@ extern "C" {
 size_t kd_dibr_workspace_size(int B, int H, int W, int64_t F, int knum, int double_precision) {
   if (B < 0 || H < 0 || W < 0 || F < 0 || knum < 1) return 0;
   return dibr_workspace_bytes(B, H, W, F, knum, double_precision ? 8 : 4);
+}
+
+int64_t kd_dibr_pair_count(const void *ws, int B, int H, int W, int64_t F, int knum,
+                           int double_precision, void *stream) {
+  if (!ws || B <= 0 || H <= 0 || W <= 0 || knum < 1) return 0;
+  void *w = const_cast<void *>(ws);
+  const int32_t *ntile = double_precision ? dibr_carve<double>(w, B, H, W, F, knum).pb.ntile
+                                          : dibr_carve<float>(w, B, H, W, F, knum).pb.ntile;
+  const int64_t tiles =
+      (int64_t)B * ((W + kTile - 1) / kTile) * (int64_t)((H + kTile - 1) / kTile);
+  std::vector<int32_t> nt((size_t)tiles * 2);
+  if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -1;
+  if (hipMemcpy(nt.data(), ntile, sizeof(int32_t) * nt.size(), hipMemcpyDeviceToHost) !=
+      hipSuccess)
+    return -1;
+  int64_t n = 0;
+  for (int64_t i = 0; i < tiles; ++i) n += nt[2 * i];
+  return n;
 }
 
 int kd_dibr_rasterization_forward_f32(int B, int H, int W, int64_t F, int D, const float *fvz,

@@ -11,7 +11,12 @@ import sys
 SLOT = {
     'kd::kd_raster_fwd_pairs': 'kd_raster_fwd', 'kd::kd_raster_fwd<float>': 'kd_raster_fwd',
     'kd::kd_soft_fwd<float, false>': 'kd_soft_fwd', 'kd::kd_soft_fwd<float, true>': 'kd_soft_fwd',
-    'kd::kd_soft_bwd_tile<float>': 'kd_soft_bwd_tile',
+    'kd::kd_soft_pairs<float>': 'kd_soft_pairs',
+    'kd::kd_soft_pair_math<float, true, false>': 'kd_soft_pair_math',
+    'kd::kd_soft_reduce<float>': 'kd_soft_reduce',
+    'kd::kd_soft_bwd_pairs<float>': 'kd_soft_bwd_pairs',
+    'kd::kd_prepare_fwd<float>': 'kd_prepare_fwd', 'kd::kd_prepare_bwd<float>': 'kd_prepare_bwd',
+    'kd::kd_zero2<float>': 'kd_zero',
     'kd::kd_raster_bwd_tile<float, 4>': 'kd_raster_bwd_tile',
     'kd::kd_bin_count<float>': 'kd_bin_count', 'kd::kd_bin_scan': 'kd_bin_scan',
     'kd::kd_bin_scatter<float>': 'kd_bin_scatter',
