@@ -299,6 +299,11 @@ __device__ __forceinline__ int wg_compact(bool pred, int *s_cnt, int &total) {
 // ------------------------------------------------------------------------------------------
 // coarse-bin geometry shared by host and device
 // ------------------------------------------------------------------------------------------
+#ifndef KD_COARSE_TILE0
+#define KD_COARSE_TILE0 32
+#endif
+constexpr int kCoarseTile0 = KD_COARSE_TILE0;  // smallest coarse tile (px); grows to <= 32 per side
+
 struct BinGeom {
   int ct;        // coarse tile edge in pixels (multiple of kTile)
   int nctx, ncty;
@@ -307,7 +312,7 @@ struct BinGeom {
 
 __host__ __device__ inline BinGeom bin_geom(int H, int W) {
   int m = H > W ? H : W;
-  int ct = 32;
+  int ct = kCoarseTile0;
   while (((m + ct - 1) / ct) > 32) ct *= 2;
   BinGeom g;
   g.ct = ct;
