@@ -8,6 +8,10 @@
 
 namespace kd {
 
+static int64_t fine_tiles(int H, int W) {
+  return (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+}
+
 size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view) {
   const BinGeom g = bin_geom(H, W);
   const int64_t nchunk = (max_per_view + kChunk - 1) / kChunk;
@@ -17,6 +21,7 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view)
   s += align_up(sizeof(int) * (size_t)B * g.nct());
   s += align_up(sizeof(int) * (size_t)g.nct() * (size_t)(N > 0 ? N : 1));
   s += align_up(sizeof(float4) * 2 * (size_t)N);
+  s += align_up(sizeof(int32_t) * (size_t)B * fine_tiles(H, W));
   return s;
 }
 
@@ -36,6 +41,8 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   off += align_up(sizeof(int) * (size_t)bb.g.nct() * (size_t)(N > 0 ? N : 1));
   bb.cull = (float4 *)(base + off);
   off += align_up(sizeof(float4) * 2 * (size_t)N);
+  bb.order = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * (size_t)B * fine_tiles(H, W));
   bb.cull_eps = 0.f;
   bb.clear = nullptr;
   bb.n_clear = 0;
@@ -259,6 +266,78 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
     }
 }
 
+// Dispatch order of the tile kernels: (view, fine tile) by descending bit length of its coarse
+// bin's face count (a proxy for its work), so the heaviest tiles start first and the grid's
+// tail is short.  One 1024-thread workgroup per job, one coarse tile (and its <= (ct/16)^2 fine
+// tiles) per thread and pass; histograms and cursors are kept per wave.  Order within a bucket
+// follows the (view, coarse tile) index; results never depend on the order.
+__global__ __launch_bounds__(1024) void kd_tile_order(BinBuffers bb0, BinBuffers bb1, int B,
+                                                      int ntx, int nty) {
+  constexpr int kNB = 33, kWaves = 16, kPer = 4;
+  __shared__ int s_cnt[kWaves][kNB];
+  __shared__ int s_base, s_next;
+  const BinBuffers &bb = blockIdx.x ? bb1 : bb0;
+  const int tid = threadIdx.x, w = tid >> 6;
+  const int nct = bb.g.nct(), n = B * nct;
+  const int per = bb.g.ct / kTile;  // fine tiles per coarse tile side
+  auto fine_count = [&](int v) {    // fine tiles of (view, coarse tile) v inside the image
+    const int c = v % nct;
+    const int cx = c % bb.g.nctx, cy = c / bb.g.nctx;
+    return (min(cx * per + per, ntx) - cx * per) * (min(cy * per + per, nty) - cy * per);
+  };
+  if (tid == 0) s_base = 0;
+  for (int v0 = 0; v0 < n; v0 += 1024 * kPer) {
+    for (int i = tid; i < kWaves * kNB; i += 1024) (&s_cnt[0][0])[i] = 0;
+    __syncthreads();
+    int bk[kPer], nf[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {  // coalesced: consecutive threads, consecutive bins
+      const int v = v0 + k * 1024 + tid;
+      bk[k] = v < n ? 32 - __clz((unsigned)bb.totals[v]) : -1;
+      nf[k] = v < n ? fine_count(v) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      if (bk[k] >= 0) atomicAdd(&s_cnt[w][bk[k]], nf[k]);
+    __syncthreads();
+    if (w == 0) {  // exclusive offsets, buckets heaviest first then waves: lane = bucket
+      const int lane = tid & 63;
+      const int kb = kNB - 1 - lane;  // lane 0 = heaviest bucket
+      int c[kWaves];
+      int tot = 0;
+#pragma unroll
+      for (int ww = 0; ww < kWaves; ++ww) {
+        c[ww] = kb >= 0 ? s_cnt[ww][kb] : 0;
+        tot += c[ww];
+      }
+      int run = s_base + wave_incl_scan(tot) - tot;
+      if (kb >= 0) {
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ++ww) {
+          s_cnt[ww][kb] = run;
+          run += c[ww];
+        }
+      }
+      const int all = __builtin_amdgcn_readlane(wave_incl_scan(tot), 63);
+      if (lane == 0) s_next = s_base + all;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      if (bk[k] < 0) continue;
+      const int v = v0 + k * 1024 + tid;
+      const int b = v / nct, c = v - b * nct;
+      const int cx = c % bb.g.nctx, cy = c / bb.g.nctx;
+      int pos = atomicAdd(&s_cnt[w][bk[k]], nf[k]);
+      for (int ty = cy * per; ty < min(cy * per + per, nty); ++ty)
+        for (int tx = cx * per; tx < min(cx * per + per, ntx); ++tx)
+          bb.order[pos++] = (b * nty + ty) * ntx + tx;
+    }
+    __syncthreads();
+    if (tid == 0) s_base = s_next;
+  }
+}
+
 template <typename T>
 static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream) {
   const FaceSet<T> &fs = jobs.fs[0];
@@ -291,6 +370,12 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
     ProfScope prof(K_BIN_SCATTER, stream);
     hipLaunchKernelGGL(kd_bin_scatter<T>, grid_c, dim3(kBlock),
                        sizeof(uint32_t) * 8 * bb.g.nct(), stream, jobs);
+  }
+  {
+    ProfScope prof(K_TILE_ORDER, stream);
+    hipLaunchKernelGGL(kd_tile_order, dim3(njobs), dim3(1024), 0, stream, jobs.bb[0],
+                       jobs.bb[njobs - 1], fs.B, (fs.W + kTile - 1) / kTile,
+                       (fs.H + kTile - 1) / kTile);
   }
   return hipGetLastError();
 }

@@ -19,6 +19,7 @@
 //                        room for the view's whole face count.
 //   cull   [N][2]        float4: fp32 raster edge-culling coefficients (raster_cull_coefs), only
 //                        written when BinBuffers::cull is set (fp32 rasterization).
+//   order  [B * tiles]   int32 (view * tiles + fine tile), heaviest coarse bin first.
 #pragma once
 
 #include "kd_common.hpp"
@@ -34,6 +35,8 @@ struct BinBuffers {
   float cull_eps;  // the raster eps (cull coefficients only)
   int *clear;      // nullable: n_clear ints zeroed by kd_bin_count (counters of later passes)
   int n_clear;
+  int32_t *order;  // [B * fine tiles] (view, tile) sorted by the coarse bin's face count,
+                   // heaviest first (kd_tile_order): the tile kernels' dispatch order
   int nchunk;
   BinGeom g;
 };

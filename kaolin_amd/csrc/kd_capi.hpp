@@ -29,6 +29,7 @@ enum KernelId {
   K_SOFT_BWD_PAIRS,
   K_PREPARE_FWD,
   K_PREPARE_BWD,
+  K_TILE_ORDER,
   K_NUM_KERNELS
 };
 

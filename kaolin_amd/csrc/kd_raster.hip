@@ -77,10 +77,11 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
-  const int b = blockIdx.y;
+  int b, tl;
+  tile_of_block(a.bb, H, W, b, tl);
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const TileGeom t = tile_geom(H, W);
+  const TileGeom t = tile_geom(H, W, tl);
   const T x0 = (T)px_cx(fs.M, W, t.px);
   const T y0 = (T)px_cy(fs.M, H, t.py);
 
@@ -186,11 +187,12 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
   const FaceSet<float> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const float M = fs.M;
-  const int b = blockIdx.y;
+  int b, tl;
+  tile_of_block(a.bb, H, W, b, tl);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const TileGeom t = tile_geom(H, W);
+  const TileGeom t = tile_geom(H, W, tl);
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
   s_key[w][lane] = 0ull;
   if (lane == 0) s_nan[w] = 0ull;

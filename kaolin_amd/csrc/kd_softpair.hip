@@ -169,15 +169,16 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairB
 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
-  const int b = blockIdx.y;
+  int b, tl;
+  tile_of_block(a.bb, H, W, b, tl);
   const int tid = threadIdx.x, w = tid >> 6;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const TileGeom t = tile_geom(H, W);
+  const TileGeom t = tile_geom(H, W, tl);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const bool unc = t.inimg && a.face_idx[p] < 0;
   const bool wave_unc = __ballot(unc) != 0ull;
-  const int64_t tile = (int64_t)b * pb.ntiles + blockIdx.x;
+  const int64_t tile = (int64_t)b * pb.ntiles + tl;
   SoftPairRec *rec = pb.rec + tile * pb.cap;
   int my_kid = 0, lbase = 0;
   if (tid == 0) s_nrec = 0;

@@ -30,9 +30,24 @@ struct TileGeom {
   bool inimg, wave_live;
 };
 
-__device__ __forceinline__ TileGeom tile_geom(int H, int W) {
+// (view, fine tile) of this workgroup: the bins' heaviest-first order (kd_tile_order) when the
+// bins were built, else (blockIdx.y, blockIdx.x).
+__device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W, int &b,
+                                              int &tile) {
+  if (bb.order && bb.nchunk > 0) {
+    const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    const int v = bb.order[blockIdx.y * gridDim.x + blockIdx.x];
+    b = v / ntiles;
+    tile = v - b * ntiles;
+  } else {
+    b = blockIdx.y;
+    tile = blockIdx.x;
+  }
+}
+
+__device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
   const int ntx = (W + kTile - 1) / kTile;
-  const int tx = blockIdx.x % ntx, ty = blockIdx.x / ntx;
+  const int tx = tile % ntx, ty = tile / ntx;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   TileGeom t;
   t.X0 = tx * kTile;
@@ -49,6 +64,7 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W) {
   t.wave_live = t.WX0 < W && t.WY0 < H;
   return t;
 }
+__device__ __forceinline__ TileGeom tile_geom(int H, int W) { return tile_geom(H, W, blockIdx.x); }
 
 struct TileLists {
   int f[kCap];                   // local face index (ascending)

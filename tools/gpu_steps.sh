@@ -1,7 +1,6 @@
 #!/bin/bash
-# Runs "label:::seconds:::command" steps in order on the GPU box.  A step that fails normally
-# (exit 1, e.g. a test assertion) does not stop the sequence; a crash, abort, segfault, time
-# limit or any other status ends it (no further GPU work in this call).
+# Runs "label:::seconds:::command" steps in order on the GPU box.  Any failing step ends the
+# sequence (no further GPU work in this call): a failed test may hide a GPU fault.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 mkdir -p gpurun_out
@@ -12,5 +11,5 @@ for step in "$@"; do
   rc=$?
   echo "=== [$label] rc=$rc"
   tail -n 25 "gpurun_out/$label.log"
-  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "=== stopping after [$label] (rc=$rc)"; exit $rc; fi
+  if [ $rc -ne 0 ]; then echo "=== stopping after [$label] (rc=$rc)"; exit $rc; fi
 done
