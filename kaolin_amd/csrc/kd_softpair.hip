@@ -235,7 +235,8 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairB
 template <typename T>
 __device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et, T prob, float M,
                                                T h[4]) {
-  const double s = (double)prob / (1.0 - (double)prob + KD_SOFT_EPS) / (double)M;
+  // the backward's coefficients need gradient accuracy, not bit-exactness: reciprocals
+  const double s = (double)prob * (1.0 / ((1.0 - (double)prob + KD_SOFT_EPS) * (double)M));
   if (et >= 3) {
     const int ps = (et - 3) * 2;
     h[0] = (T)(s * (double)((T)2 * (v[ps] - x0)));
@@ -248,11 +249,11 @@ __device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et,
     const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
     const T up = A * x0 + Bc * y0 + C;
     const T down = A * A + Bc * Bc;
-    const double dd = (double)down + KD_SOFT_EPS;
-    const T dissquare = (T)((double)(up * up) / dd);
-    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) / dd);
-    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) / dd);
-    const T dzdC = (T)((double)((T)2 * up) / dd);
+    const double rd = 1.0 / ((double)down + KD_SOFT_EPS);
+    const T dissquare = (T)((double)(up * up) * rd);
+    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) * rd);
+    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) * rd);
+    const T dzdC = (T)((double)((T)2 * up) * rd);
     h[0] = (T)(s * (double)(dzdB - y2 * dzdC));
     h[1] = (T)(s * (double)(x2 * dzdC - dzdA));
     h[2] = (T)(s * (double)(y1 * dzdC - dzdB));
@@ -287,10 +288,10 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
     T prob = (T)0;
     if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
     const int64_t gp = ((int64_t)b * H + py) * W + px;
-    const int64_t o = gp * K + r.slot;
     pb.sprob[(int64_t)r.slot * pb.npixels + gp] = prob;
     rp->type = (uint8_t)et;
     if (LISTS) {
+      const int64_t o = gp * K + r.slot;
       a.prob[o] = prob;
       a.cidx[o] = (int64_t)r.row - lo;
       a.ctype[o] = (uint8_t)(et + 1);
@@ -461,7 +462,8 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   if (reduce) {
     ProfScope prof(K_SOFT_REDUCE, stream);
-    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a, pb);
+    const unsigned g = (a.fs.dbg & 2048) ? 256 : (a.fs.dbg & 4096) ? 8192 : kPersistentBlocks;
+    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(g), dim3(kBlock), 0, stream, a, pb);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
