@@ -116,11 +116,6 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
   const int64_t nf = (int64_t)B * F;
   int rc = zero_buffers<T>(gfvi, nf * 6, gfeat, gfeat ? nf * 3 * D : 0, stream);
   if (rc != KD_OK || B == 0 || H == 0 || W == 0) return rc;
-  if (grad_interp) {
-    rc = raster_backward_launch<T>(B, H, W, F, D, grad_interp, face_idx, weights, fvi, feat, eps,
-                                   gfvi, gfeat, stream);
-    if (rc != KD_OK) return rc;
-  }
   if (grad_soft) {
     DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
     SoftArgs<T> sa{};
@@ -135,7 +130,11 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
     sa.soft_in = soft;
     sa.grad_fvi = gfvi;
     rc = soft_pairs_backward_launch<T>(sa, d.pb, stream);
+    if (rc != KD_OK) return rc;
   }
+  if (grad_interp)
+    rc = raster_backward_launch<T>(B, H, W, F, D, grad_interp, face_idx, weights, fvi, feat, eps,
+                                   gfvi, gfeat, stream);
   return rc;
 }
 
