@@ -117,10 +117,11 @@ __device__ inline void span_x(T lo, T hi, float M, int W, int &a, int &b) {
     span_monotone<T>(lo, hi, W, false, [&](int i) { return px_cx(M, W, i); }, a, b);
     return;
   }
+  const double rs = 1.0 / (double)s;  // estimate only: the loops below settle it exactly
   if (isnan(lo)) {
     a = 0;
   } else {
-    double t = ((double)lo / (double)s + (double)(W - 1)) * 0.5;
+    double t = ((double)lo * rs + (double)(W - 1)) * 0.5;
     t = fmin(fmax(t, -1.0), (double)W);
     a = (int)ceil(t);
     a = a < 0 ? 0 : (a > W ? W : a);
@@ -130,7 +131,7 @@ __device__ inline void span_x(T lo, T hi, float M, int W, int &a, int &b) {
   if (isnan(hi)) {
     b = W - 1;
   } else {
-    double t = ((double)hi / (double)s + (double)(W - 1)) * 0.5;
+    double t = ((double)hi * rs + (double)(W - 1)) * 0.5;
     t = fmin(fmax(t, -1.0), (double)W + 1.0);
     b = (int)ceil(t) - 1;
     b = b < -1 ? -1 : (b > W - 1 ? W - 1 : b);
@@ -147,10 +148,11 @@ __device__ inline void span_y(T lo, T hi, float M, int H, int &c, int &d) {
     return;
   }
   // rows accepted: !(cy < lo) && !(cy >= hi); cy decreases with h.
+  const double rs = 1.0 / (double)s;  // estimate only: the loops below settle it exactly
   if (isnan(hi)) {
     c = 0;
   } else {  // first h with cy(h) < hi
-    double t = ((double)(H - 1) - (double)hi / (double)s) * 0.5;
+    double t = ((double)(H - 1) - (double)hi * rs) * 0.5;
     t = fmin(fmax(t, -2.0), (double)H);
     c = (int)floor(t) + 1;
     c = c < 0 ? 0 : (c > H ? H : c);
@@ -160,7 +162,7 @@ __device__ inline void span_y(T lo, T hi, float M, int H, int &c, int &d) {
   if (isnan(lo)) {
     d = H - 1;
   } else {  // last h with cy(h) >= lo
-    double t = ((double)(H - 1) - (double)lo / (double)s) * 0.5;
+    double t = ((double)(H - 1) - (double)lo * rs) * 0.5;
     t = fmin(fmax(t, -2.0), (double)H);
     d = (int)floor(t);
     d = d < -1 ? -1 : (d > H - 1 ? H - 1 : d);
