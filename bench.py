@@ -100,10 +100,13 @@ def main():
     ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
     args = ap.parse_args()
 
-    rank, world, local = distributed.init_from_env('nccl')
+    # KD_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (ranks share cuda:0;
+    # RCCL refuses two ranks on one device).  The default is RCCL ("nccl").
+    backend = os.environ.get('KD_BENCH_BACKEND', 'nccl')
+    rank, world, local = distributed.init_from_env(backend)
     if world != args.gpus and rank == 0:
         print(f'[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}', file=sys.stderr)
-    dev = torch.device('cuda', local)
+    dev = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     _lib.load()
     dibr.SAVE_CLOSE_LISTS = args.lists

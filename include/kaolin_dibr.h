@@ -294,6 +294,53 @@ int kd_prepare_vertices_backward_f64(int batch, int vertex_batch, int64_t num_ve
                                      const int64_t *adj_offsets, const int32_t *adj,
                                      double *grad_vertices, void *stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * mask_iou (kaolin/metrics/render.py:18-40): loss = 1 - mean_b(U_b / (D_b + 1e-10)) with
+ * U_b = sum(l * r), D_b = sum(l + r - l * r) over the `pixels` elements of view b.  lhs / rhs
+ * (B, pixels) contiguous.  The forward writes the scalar loss, stats (B, 2) = (U_b, D_b) for the
+ * backward and, when `iou` is not NULL, the per-view IoU (B).  Workspace:
+ * kd_mask_iou_workspace_size.  The backward reads the incoming gradient from the DEVICE scalar
+ * grad_loss and writes grad_lhs / grad_rhs (either may be NULL).
+ * ------------------------------------------------------------------------------------------- */
+size_t kd_mask_iou_workspace_size(int batch, int64_t pixels, int double_precision);
+int kd_mask_iou_forward_f32(int batch, int64_t pixels, const float *lhs, const float *rhs,
+                            float *loss, float *stats, float *iou, void *workspace,
+                            size_t workspace_bytes, void *stream);
+int kd_mask_iou_forward_f64(int batch, int64_t pixels, const double *lhs, const double *rhs,
+                            double *loss, double *stats, double *iou, void *workspace,
+                            size_t workspace_bytes, void *stream);
+int kd_mask_iou_backward_f32(int batch, int64_t pixels, const float *lhs, const float *rhs,
+                             const float *stats, const float *grad_loss, float *grad_lhs,
+                             float *grad_rhs, void *stream);
+int kd_mask_iou_backward_f64(int batch, int64_t pixels, const double *lhs, const double *rhs,
+                             const double *stats, const double *grad_loss, double *grad_lhs,
+                             double *grad_rhs, void *stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * texture_mapping (kaolin/render/mesh/utils.py:23-76): clamp uv to [0, 1], flip v, then
+ * grid_sample(align_corners=False, padding_mode='border').  coords (B, N, 2) with N = h * w for a
+ * dense image or the number of points; texture (Bt, C, Ht, Wt) contiguous per view with
+ * tex_batch_stride C * Ht * Wt (Bt == B) or 0 (one texture shared by every view); out (B, N, C).
+ * mode 0 = nearest, 1 = bilinear.  The backward zeroes and fills grad_tex (the texture's layout
+ * and batch stride; shared texture: summed over views) and grad_coords (B, N, 2); either may be
+ * NULL.
+ * ------------------------------------------------------------------------------------------- */
+int kd_texture_mapping_forward_f32(int batch, int64_t num_samples, int channels, int tex_height,
+                                   int tex_width, const float *coords, const float *tex,
+                                   int64_t tex_batch_stride, int mode, float *out, void *stream);
+int kd_texture_mapping_forward_f64(int batch, int64_t num_samples, int channels, int tex_height,
+                                   int tex_width, const double *coords, const double *tex,
+                                   int64_t tex_batch_stride, int mode, double *out, void *stream);
+int kd_texture_mapping_backward_f32(int batch, int64_t num_samples, int channels, int tex_height,
+                                    int tex_width, const float *coords, const float *tex,
+                                    int64_t tex_batch_stride, int mode, const float *grad_out,
+                                    float *grad_tex, float *grad_coords, void *stream);
+int kd_texture_mapping_backward_f64(int batch, int64_t num_samples, int channels,
+                                    int tex_height, int tex_width, const double *coords,
+                                    const double *tex, int64_t tex_batch_stride, int mode,
+                                    const double *grad_out, double *grad_tex,
+                                    double *grad_coords, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

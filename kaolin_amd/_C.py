@@ -455,6 +455,102 @@ def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights,
     return gfvi, gfeat
 
 
+# -------------------------------------------------------------------------------------------
+# mask_iou (kaolin/metrics/render.py:18-40) and texture_mapping (render/mesh/utils.py:23-76),
+# SURVEY §8 f2
+# -------------------------------------------------------------------------------------------
+def mask_iou_forward(lhs, rhs):
+    """lhs, rhs (B, H, W) -> (loss (), stats (B, 2) = (U_b, D_b), iou (B,))."""
+    fn = 'mask_iou'
+    dev = _check_same_gpu(fn, lhs_mask=lhs, rhs_mask=rhs)
+    if lhs.dim() != 3:
+        raise RuntimeError(f'{fn}: expected (batch, height, width) masks, got {list(lhs.shape)}')
+    _check_size(fn, 'rhs_mask', rhs, lhs.shape)
+    sfx = _sfx(lhs, fn)
+    _check_dtype(fn, lhs, rhs_mask=rhs)
+    B = lhs.shape[0]
+    P = lhs.shape[1] * lhs.shape[2]
+    lhs, rhs = lhs.contiguous(), rhs.contiguous()
+    opts = dict(device=dev, dtype=lhs.dtype)
+    loss = torch.empty((), **opts)
+    stats = torch.empty((B, 2), **opts)
+    iou = torch.empty((B,), **opts)
+    nb = int(_lib.load().kd_mask_iou_workspace_size(B, P, 1 if lhs.dtype == torch.float64 else 0))
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+    _lib.call(f'kd_mask_iou_forward_{sfx}', B, P, _ptr(lhs), _ptr(rhs), _ptr(loss), _ptr(stats),
+              _ptr(iou), _ptr(ws), nb, _stream(dev))
+    return loss, stats, iou
+
+
+def mask_iou_backward(grad_loss, lhs, rhs, stats, need_lhs=True, need_rhs=True):
+    """Gradients (grad_lhs or None, grad_rhs or None); grad_loss is a device scalar."""
+    dev = lhs.device
+    B = lhs.shape[0]
+    P = lhs.shape[1] * lhs.shape[2]
+    sfx = _sfx(lhs, 'mask_iou_backward')
+    lhs, rhs = lhs.contiguous(), rhs.contiguous()
+    g = grad_loss.reshape(()).to(lhs.dtype).contiguous()
+    gl = torch.empty_like(lhs) if need_lhs else None
+    gr = torch.empty_like(rhs) if need_rhs else None
+    _lib.call(f'kd_mask_iou_backward_{sfx}', B, P, _ptr(lhs), _ptr(rhs), _ptr(stats), _ptr(g),
+              _ptr(gl), _ptr(gr), _stream(dev))
+    return gl, gr
+
+
+_TEX_MODES = {'nearest': 0, 'bilinear': 1}
+
+
+def _texture_args(fn, coords, tex, mode):
+    dev = _check_same_gpu(fn, texture_coordinates=coords, texture_maps=tex)
+    if mode not in _TEX_MODES:
+        raise RuntimeError(f'{fn}: mode must be "nearest" or "bilinear", got {mode!r}')
+    if coords.shape[-1] != 2 or coords.dim() < 3:
+        raise RuntimeError(f'{fn}: texture_coordinates must be (batch, ..., 2), got '
+                           f'{list(coords.shape)}')
+    if tex.dim() != 4:
+        raise RuntimeError(f'{fn}: texture_maps must be (batch, channels, h, w), got '
+                           f'{list(tex.shape)}')
+    B = coords.shape[0]
+    if tex.shape[0] not in (1, B):
+        raise RuntimeError(f'{fn}: texture batch {tex.shape[0]} must be 1 or the coordinate '
+                           f'batch {B}')
+    sfx = _sfx(tex, fn)
+    _check_dtype(fn, tex, texture_coordinates=coords)
+    C, Ht, Wt = tex.shape[1:]
+    tex_c = tex.contiguous()
+    # a batch-1 texture is shared by every view (read in place, batch stride 0)
+    bstride = C * Ht * Wt if tex.shape[0] == B else 0
+    N = coords[0, ..., 0].numel() if B > 0 else 0
+    return dev, sfx, B, N, C, Ht, Wt, tex_c, bstride
+
+
+def texture_mapping_forward(coords, tex, mode):
+    """coords (B, ..., 2), texture (B, C, Ht, Wt) -> (B, ..., C)."""
+    fn = 'texture_mapping'
+    dev, sfx, B, N, C, Ht, Wt, tex_c, bs = _texture_args(fn, coords, tex, mode)
+    coords = coords.contiguous()
+    out = torch.empty((*coords.shape[:-1], C), device=dev, dtype=tex.dtype)
+    _lib.call(f'kd_texture_mapping_forward_{sfx}', B, N, C, Ht, Wt, _ptr(coords), _ptr(tex_c), bs,
+              _TEX_MODES[mode], _ptr(out), _stream(dev))
+    return out
+
+
+def texture_mapping_backward(grad_out, coords, tex, mode, need_coords=True, need_tex=True):
+    """(grad_coords or None, grad_tex or None); a shared (batch-1) texture gets the gradient
+    summed over the views."""
+    fn = 'texture_mapping_backward'
+    dev, sfx, B, N, C, Ht, Wt, tex_c, bs = _texture_args(fn, coords, tex, mode)
+    coords = coords.contiguous()
+    go = grad_out.contiguous()
+    gc = torch.empty_like(coords) if need_coords else None
+    gt = None
+    if need_tex:
+        gt = torch.empty(tex.shape, device=dev, dtype=tex.dtype)
+    _lib.call(f'kd_texture_mapping_backward_{sfx}', B, N, C, Ht, Wt, _ptr(coords), _ptr(tex_c),
+              bs, _TEX_MODES[mode], _ptr(go), _ptr(gt), _ptr(gc), _stream(dev))
+    return gc, gt
+
+
 render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
     rasterize_backward_cuda=rasterize_backward_cuda,
@@ -468,4 +564,8 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     dibr_rasterization_backward_fused=dibr_rasterization_backward_fused,
     prepare_vertices_forward=prepare_vertices_forward,
     prepare_vertices_backward=prepare_vertices_backward,
+    texture_mapping_forward=texture_mapping_forward,
+    texture_mapping_backward=texture_mapping_backward,
 ))
+metrics = types.SimpleNamespace(mask_iou_forward=mask_iou_forward,
+                                mask_iou_backward=mask_iou_backward)

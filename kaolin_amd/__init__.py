@@ -7,5 +7,6 @@ include/kaolin_dibr.h and bound here with ctypes (kaolin_amd/_lib.py).
 """
 from . import _C  # noqa: F401
 from . import render  # noqa: F401
+from . import metrics  # noqa: F401
 
 __version__ = '0.1.0'

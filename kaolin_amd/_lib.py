@@ -51,6 +51,12 @@ _SIGS = {
     'kd_dibr_soft_mask_backward_binned': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,
                                           c_double, c_double, c_float, c_p, c_p, c_size, c_int,
                                           c_p],
+    'kd_mask_iou_forward': [c_int, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_size, c_p],
+    'kd_mask_iou_backward': [c_int, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
+    'kd_texture_mapping_forward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
+                                   c_p, c_p],
+    'kd_texture_mapping_backward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
+                                    c_p, c_p, c_p, c_p],
 }
 
 
@@ -74,6 +80,8 @@ def load():
             lib.kd_dibr_workspace_size.restype = c_size
             lib.kd_dibr_pair_count.argtypes = [c_p, c_int, c_int, c_int, c_i64, c_int, c_int, c_p]
             lib.kd_dibr_pair_count.restype = c_i64
+            lib.kd_mask_iou_workspace_size.argtypes = [c_int, c_i64, c_int]
+            lib.kd_mask_iou_workspace_size.restype = c_size
             lib.kd_last_error.argtypes = []
             lib.kd_last_error.restype = ctypes.c_char_p
             lib.kd_version.restype = c_int

@@ -30,6 +30,10 @@ enum KernelId {
   K_PREPARE_FWD,
   K_PREPARE_BWD,
   K_TILE_ORDER,
+  K_IOU_FWD,
+  K_IOU_BWD,
+  K_TEX_FWD,
+  K_TEX_BWD,
   K_NUM_KERNELS
 };
 

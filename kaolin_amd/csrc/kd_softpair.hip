@@ -309,7 +309,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
 // tiles with records); every other pixel was written by kd_soft_pairs.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPairBuf<T> pb) {
-  const int K = a.K, H = a.fs.H, W = a.fs.W;
+  const int H = a.fs.H, W = a.fs.W;
   const int ntl = pb.counters[1];
   for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) {
     const int64_t tile = pb.tiles[ti];

@@ -1,4 +1,5 @@
-"""``prepare_vertices`` -- drop-in for kaolin/render/mesh/utils.py:128-175.
+"""``prepare_vertices`` -- drop-in for kaolin/render/mesh/utils.py:128-175, and
+``texture_mapping`` -- drop-in for utils.py:23-76 (at the end of this file).
 
 The reference moves the vertices to each camera (``pad(v, 1) @ camera_transform``, or
 ``(v - trans) @ rot^T`` via camera.rotate_translate_points, legacy.py:22-37), projects them
@@ -19,7 +20,7 @@ from torch.autograd import Function
 
 from ... import _C
 
-__all__ = ['prepare_vertices']
+__all__ = ['prepare_vertices', 'texture_mapping']
 
 _ADJ_CACHE = {}  # id(faces) -> (weakref(faces), version, num_vertices, adjacency)
 
@@ -113,3 +114,41 @@ def prepare_vertices(vertices, faces, camera_proj, camera_rot=None, camera_trans
     if camera_proj.requires_grad or camera_transform.requires_grad:
         return _reference_composition(vertices, faces, camera_proj, camera_transform)
     return PrepareVerticesHip.apply(vertices, faces, camera_proj, camera_transform)
+
+
+class TextureMappingHip(Function):
+    """torch.autograd.Function over kd_texture_mapping_forward / _backward."""
+
+    @staticmethod
+    def forward(ctx, texture_coordinates, texture_maps, mode):
+        out = _C.render.mesh.texture_mapping_forward(texture_coordinates, texture_maps, mode)
+        ctx.save_for_backward(texture_coordinates, texture_maps)
+        ctx.mode = mode
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        coords, tex = ctx.saved_tensors
+        gc, gt = _C.render.mesh.texture_mapping_backward(
+            grad_out, coords, tex, ctx.mode, need_coords=ctx.needs_input_grad[0],
+            need_tex=ctx.needs_input_grad[1])
+        return gc, gt, None
+
+
+def texture_mapping(texture_coordinates, texture_maps, mode='nearest'):
+    r"""Interpolate texture_maps at texture_coordinates (kaolin/render/mesh/utils.py:23-76).
+
+    Args:
+        texture_coordinates (torch.Tensor): (batch_size, h, w, 2) dense image uvs or
+            (batch_size, num_points, 2) sparse uvs, in [0, 1] (clamped), OpenGL convention
+            (v from bottom to top).
+        texture_maps (torch.Tensor): (batch_size, num_channels, h', w').  As an extension of the
+            reference a batch of 1 is shared by every view (no ``repeat`` needed; its gradient
+            is summed over the views).
+        mode (str): 'nearest' or 'bilinear' (grid_sample, align_corners=False, border padding).
+
+    Returns:
+        (torch.Tensor): (batch_size, h, w, num_channels) or (batch_size, num_points,
+        num_channels).
+    """
+    return TextureMappingHip.apply(texture_coordinates, texture_maps, mode)
