@@ -341,6 +341,20 @@ int kd_texture_mapping_backward_f64(int batch, int64_t num_samples, int channels
                                     const double *grad_out, double *grad_tex,
                                     double *grad_coords, void *stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * nvdiffrast_fwd compatibility (kaolin/render/mesh/rasterization.py:145-241): from an external
+ * forward's rast buffer (B, H, W, 4) = (u, v, z/w, triangle_id + 1) and the per-face features
+ * (B, F, 3, D), writes interp (B, H, W, D) (u * a0 + v * a1 + (1 - (u + v)) * a2, 0 where empty),
+ * face_idx (B, H, W) = id - 1 and weights (B, H, W, 3) = (u, v, 1 - (u + v)) -- the inputs of
+ * kd_rasterize_backward_*.
+ * ------------------------------------------------------------------------------------------- */
+int kd_rast_interpolate_f32(int batch, int height, int width, int64_t num_faces, int feat_dim,
+                            const float *rast, const float *feat, float *interp,
+                            int64_t *face_idx, float *weights, void *stream);
+int kd_rast_interpolate_f64(int batch, int height, int width, int64_t num_faces, int feat_dim,
+                            const double *rast, const double *feat, double *interp,
+                            int64_t *face_idx, double *weights, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -551,6 +551,33 @@ def texture_mapping_backward(grad_out, coords, tex, mode, need_coords=True, need
     return gc, gt
 
 
+# -------------------------------------------------------------------------------------------
+# nvdiffrast_fwd compatibility (rasterization.py:145-241), SURVEY §8 f4
+# -------------------------------------------------------------------------------------------
+def rast_interpolate(rast, face_features):
+    """rast (B, H, W, 4) from an external forward, features (B, F, 3, D) ->
+    (interp (B, H, W, D), face_idx (B, H, W) int64, weights (B, H, W, 3))."""
+    fn = 'rast_interpolate'
+    dev = _check_same_gpu(fn, rast=rast, face_features=face_features)
+    if rast.dim() != 4 or rast.shape[-1] != 4:
+        raise RuntimeError(f'{fn}: rast must be (batch, height, width, 4), got {list(rast.shape)}')
+    B, H, W = rast.shape[:3]
+    if face_features.dim() != 4 or face_features.shape[0] != B or face_features.shape[2] != 3:
+        raise RuntimeError(f'{fn}: face_features must be (batch, num_faces, 3, D), got '
+                           f'{list(face_features.shape)}')
+    F, D = face_features.shape[1], face_features.shape[3]
+    sfx = _sfx(face_features, fn)
+    rast = rast.to(face_features.dtype).contiguous()
+    feat = face_features.contiguous()
+    opts = dict(device=dev, dtype=feat.dtype)
+    interp = torch.empty((B, H, W, D), **opts)
+    face_idx = torch.empty((B, H, W), device=dev, dtype=torch.long)
+    weights = torch.empty((B, H, W, 3), **opts)
+    _lib.call(f'kd_rast_interpolate_{sfx}', B, H, W, F, D, _ptr(rast), _ptr(feat), _ptr(interp),
+              _ptr(face_idx), _ptr(weights), _stream(dev))
+    return interp, face_idx, weights
+
+
 render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
     rasterize_backward_cuda=rasterize_backward_cuda,
@@ -566,6 +593,7 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     prepare_vertices_backward=prepare_vertices_backward,
     texture_mapping_forward=texture_mapping_forward,
     texture_mapping_backward=texture_mapping_backward,
+    rast_interpolate=rast_interpolate,
 ))
 metrics = types.SimpleNamespace(mask_iou_forward=mask_iou_forward,
                                 mask_iou_backward=mask_iou_backward)

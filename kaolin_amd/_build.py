@@ -17,7 +17,8 @@ LIB = os.path.join(LIBDIR, 'libkaolin_dibr.so')
 OBJDIR = os.path.join(PKG, 'build')
 
 SOURCES = ['kd_capi.cpp', 'kd_binning.hip', 'kd_raster.hip', 'kd_softmask.hip', 'kd_softpair.hip',
-           'kd_prepare.hip', 'kd_dibr.hip', 'kd_metrics.hip', 'kd_texture.hip']
+           'kd_prepare.hip', 'kd_dibr.hip', 'kd_metrics.hip', 'kd_texture.hip',
+           'kd_rastcompat.hip']
 HEADERS = ['kd_common.hpp', 'kd_binning.hpp', 'kd_capi.hpp']
 ARCH = os.environ.get('KAOLIN_AMD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')

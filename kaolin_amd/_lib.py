@@ -55,6 +55,7 @@ _SIGS = {
     'kd_mask_iou_backward': [c_int, c_i64, c_p, c_p, c_p, c_p, c_p, c_p, c_p],
     'kd_texture_mapping_forward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
                                    c_p, c_p],
+    'kd_rast_interpolate': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_p],
     'kd_texture_mapping_backward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
                                     c_p, c_p, c_p, c_p],
 }

@@ -34,6 +34,7 @@ enum KernelId {
   K_IOU_BWD,
   K_TEX_FWD,
   K_TEX_BWD,
+  K_RAST_INTERP,
   K_NUM_KERNELS
 };
 

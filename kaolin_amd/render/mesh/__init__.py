@@ -1,4 +1,4 @@
 """Mirror of kaolin/render/mesh/__init__.py (hot-path functions)."""
-from .rasterization import rasterize  # noqa: F401
+from .rasterization import rasterize, rasterize_from_rast  # noqa: F401
 from .dibr import dibr_soft_mask, dibr_rasterization  # noqa: F401
 from .utils import prepare_vertices, texture_mapping  # noqa: F401

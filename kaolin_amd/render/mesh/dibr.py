@@ -118,11 +118,9 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
 
     Runs as one fused forward / backward (DibrRasterizationHip); with ``SAVE_CLOSE_LISTS`` it is
     the reference composition of ``rasterize`` and ``dibr_soft_mask`` instead."""
-    if rast_backend != 'cuda':
-        raise ValueError(f'"{rast_backend}" is not a valid backend, valid choices are ["cuda"] '
-                         '(nvdiffrast is not available on MI355X)')
     _multiplier = 1000. if multiplier is None else multiplier
-    if SAVE_CLOSE_LISTS:
+    if SAVE_CLOSE_LISTS or rast_backend != 'cuda':
+        # the reference composition (dibr.py:193-208); other backends go through rasterize
         interpolated_features, face_idx = rasterize(
             height, width, face_vertices_z, face_vertices_image, face_features,
             face_normals_z >= 0., multiplier, eps, rast_backend)

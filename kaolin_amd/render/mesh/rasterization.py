@@ -1,4 +1,10 @@
-"""``rasterize`` -- drop-in for kaolin/render/mesh/rasterization.py:390-506 (backend 'cuda').
+"""``rasterize`` -- drop-in for kaolin/render/mesh/rasterization.py:390-506.
+
+Backends: 'cuda' (the gfx950 kernels below) and, for the reference's nvdiffrast backends
+(rasterization.py:31-241), 'nvdiffrast_fwd' = an external forward's ``rast`` buffer
++ our HIP interpolation and backward (``rasterize_from_rast``), 'nvdiffrast' = the external
+library end to end.  nvdiffrast itself is an NVIDIA library; when it is not importable these two
+backends raise the reference's ValueError.
 
 The reference's ``RasterizeCuda`` (rasterization.py:243-388) packs the valid faces with
 ``torch.where`` (a device->host sync), scales, builds boxes, calls the packed kernel and remaps
@@ -7,12 +13,87 @@ raster, kaolin_amd/csrc/kd_raster.hip) with no host sync; the outputs are bit-id
 The backward is the tile kernel (per-tile LDS sums, one atomic per tile and face), same math
 as rasterization_cuda.cu:238-402.
 """
+import warnings
+
 import torch
 from torch.autograd import Function
 
 from ... import _C
 
-__all__ = ['rasterize']
+__all__ = ['rasterize', 'rasterize_from_rast']
+
+try:  # the reference's optional dependency (rasterization.py:24-29); absent on ROCm
+    import nvdiffrast.torch as nvdiff
+    _has_nvdiffrast = True
+except ImportError:
+    nvdiff = None
+    _has_nvdiffrast = False
+
+_nvdiff_glctx = {}
+
+
+def _get_nvdiff_glctx(device):
+    """One RasterizeGLContext per device (rasterization.py:31-38)."""
+    if device not in _nvdiff_glctx:
+        _nvdiff_glctx[device] = nvdiff.RasterizeGLContext(output_db=False, device=device)
+    return _nvdiff_glctx[device]
+
+
+def _legacy_to_opengl(face_vertices_image, face_vertices_z, valid_faces=None):
+    """Kaolin's face-vertex layout -> nvdiffrast's clip-space positions and triangles
+    (rasterization.py:41-79): pos (B, 3F, 4) = (x, -y, z normalised by max |z|, +-1 for
+    valid / invalid faces), tri (F, 3) = arange."""
+    z = -face_vertices_z / (abs(face_vertices_z).max() + 1e-6)
+    fvi = face_vertices_image.reshape(*face_vertices_image.shape[:-3], -1, 2)
+    pos = torch.stack([fvi[..., 0], -fvi[..., 1], z.reshape(*z.shape[:-2], -1)], dim=-1)
+    if valid_faces is None:
+        pos = torch.nn.functional.pad(pos, (0, 1), value=1.)
+    else:
+        pad = (valid_faces.unsqueeze(-1) * 2. - 1.).expand(*valid_faces.shape, 3)
+        pos = torch.cat([pos, pad.reshape(*valid_faces.shape[:-1], -1, 1)], dim=-1)
+    tri = torch.arange(pos.shape[-2], device=pos.device, dtype=torch.int).reshape(-1, 3)
+    return pos, tri
+
+
+def _require_nvdiffrast():
+    if not _has_nvdiffrast:
+        raise ValueError("nvdiffrast must be installed to be used as backend, but failed to "
+                         "import. See https://nvlabs.github.io/nvdiffrast/#installation for "
+                         "installation instructions.")
+
+
+class RasterizeFromRastHip(Function):
+    """The nvdiffrast_fwd path (NvdiffRasterizeFwdCudaBwd, rasterization.py:145-241) from the
+    external forward's ``rast`` on: HIP interpolation + weights + face index
+    (kd_rast_interpolate), HIP rasterize backward."""
+
+    @staticmethod
+    def forward(ctx, rast, face_vertices_image, face_features, eps):
+        face_vertices_image = face_vertices_image.contiguous()
+        face_features = face_features.contiguous()
+        interp, face_idx, weights = _C.render.mesh.rast_interpolate(rast, face_features)
+        ctx.save_for_backward(face_idx, weights, face_vertices_image, face_features)
+        ctx.mark_non_differentiable(face_idx)
+        ctx.eps = eps
+        return interp, face_idx
+
+    @staticmethod
+    def backward(ctx, grad_interp, grad_face_idx):
+        face_idx, weights, fvi, feat = ctx.saved_tensors
+        need_fvi, need_feat = ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        if not (need_fvi or need_feat):
+            return None, None, None, None
+        gfvi, gfeat = _C.render.mesh.rasterize_backward_autograd(
+            grad_interp.contiguous(), face_idx, weights, fvi, feat, ctx.eps, need_feat=need_feat)
+        return None, gfvi if need_fvi else None, gfeat, None
+
+
+def rasterize_from_rast(rast, face_vertices_image, face_features, eps=1e-8):
+    """Features and face index from an external rasterizer's nvdiffrast-format buffer
+    ``rast`` (B, H, W, 4) = (u, v, z/w, triangle_id + 1) over ``_legacy_to_opengl``'s triangles,
+    differentiable w.r.t. face_vertices_image and face_features through the HIP rasterize
+    backward -- what backend 'nvdiffrast_fwd' does after nvdiff.rasterize."""
+    return RasterizeFromRastHip.apply(rast, face_vertices_image, face_features, eps)
 
 
 class RasterizeCuda(Function):
@@ -53,22 +134,41 @@ def rasterize(height, width, face_vertices_z, face_vertices_image, face_features
     Args and returns are the reference's: ``face_vertices_z`` (B, F, 3),
     ``face_vertices_image`` (B, F, 3, 2), ``face_features`` (B, F, 3, D) or a list of such,
     ``valid_faces`` (B, F) bool; returns (features (B, H, W, D) or tuple, face_idx (B, H, W)
-    int64 with -1 for empty).  Defaults: multiplier 1000, eps 1e-8.  ``backend`` must be 'cuda'
-    (the name is kept for drop-in compatibility; it runs the gfx950 kernels).  The nvdiffrast
-    backends of the reference are not provided (NVIDIA-only OpenGL).
+    int64 with -1 for empty).  Defaults: multiplier 1000, eps 1e-8.  ``backend`` 'cuda' (the
+    name is kept for drop-in compatibility; it runs the gfx950 kernels), 'nvdiffrast_fwd' or
+    'nvdiffrast' (need the nvdiffrast package; see the module docstring).
     """
     if multiplier is None:
         multiplier = 1000
+    elif backend in ['nvdiffrast', 'nvdiffrast_fwd']:
+        warnings.warn(f'in "rasterize": multiplier is ignored with backend "{backend}"',
+                      UserWarning)
     if eps is None:
         eps = 1e-8
-    if backend != 'cuda':
-        raise ValueError(f'"{backend}" is not a valid backend, valid choices are ["cuda"] '
-                         '(nvdiffrast is not available on MI355X)')
+    elif backend == 'nvdiffrast':
+        warnings.warn(f'in "rasterize": eps is ignored with backend "{backend}"', UserWarning)
     _face_features = torch.cat(face_features, dim=-1) \
         if isinstance(face_features, (list, tuple)) else face_features
-    image_features, face_idx = RasterizeCuda.apply(
-        height, width, face_vertices_z, face_vertices_image, _face_features, valid_faces,
-        multiplier, eps)
+    if backend == 'cuda':
+        image_features, face_idx = RasterizeCuda.apply(
+            height, width, face_vertices_z, face_vertices_image, _face_features, valid_faces,
+            multiplier, eps)
+    elif backend in ('nvdiffrast', 'nvdiffrast_fwd'):
+        _require_nvdiffrast()
+        glctx = _get_nvdiff_glctx(face_vertices_z.device)
+        pos, tri = _legacy_to_opengl(face_vertices_image, face_vertices_z, valid_faces)
+        rast = nvdiff.rasterize(glctx, pos, tri, (height, width), grad_db=False)[0]
+        if backend == 'nvdiffrast_fwd':
+            image_features, face_idx = rasterize_from_rast(rast, face_vertices_image,
+                                                           _face_features, eps)
+        else:  # the external library end to end (rasterization.py:81-143)
+            feats = _face_features.reshape(*_face_features.shape[:-3],
+                                           _face_features.shape[-3] * 3, -1)
+            image_features = nvdiff.interpolate(feats, rast, tri)[0]
+            face_idx = (rast[..., -1].long() - 1).contiguous()
+    else:
+        raise ValueError(f'"{backend}" is not a valid backend, valid choices are '
+                         '["cuda", "nvdiffrast", "nvdiffrast_fwd"]')
     if isinstance(face_features, (list, tuple)):
         _image_features = []
         cur_idx = 0
