@@ -355,6 +355,40 @@ int kd_rast_interpolate_f64(int batch, int height, int width, int64_t num_faces,
                             const double *rast, const double *feat, double *interp,
                             int64_t *face_idx, double *weights, void *stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * deftet_sparse_render (kaolin/render/mesh/deftet.py:269-417 -> deftet.cpp / deftet_cuda.cu):
+ * per pixel (pixel_coords (B, P, 2), any image coordinates; render_ranges (B, P, 2) = [min, max)
+ * depth) the first knum faces by index whose box holds the pixel, whose eps-normalised
+ * barycentric weights are >= 0 and whose interpolated depth is in range, sorted by depth
+ * descending (ties: face order).  Outputs: interp (B, P, knum, D), face_idx (B, P, knum) (-1 =
+ * empty), weights (B, P, knum, 3) = (w0, w1, 1 - (w0 + w1)) for the backward.  Workspace:
+ * kd_deftet_workspace_size.  The backward writes grad_fvi (B, F, 3, 2) and grad_feat
+ * (B, F, 3, D) (NULL: skipped).
+ * ------------------------------------------------------------------------------------------- */
+size_t kd_deftet_workspace_size(int batch, int64_t num_faces, int double_precision);
+int kd_deftet_sparse_render_forward_f32(int batch, int64_t num_pixels, int64_t num_faces,
+                                        int knum, int feat_dim, const float *pixel_coords,
+                                        const float *render_ranges, const float *fvz,
+                                        const float *fvi, const float *feat, float eps,
+                                        float *interp, int64_t *face_idx, float *weights,
+                                        void *workspace, size_t workspace_bytes, void *stream);
+int kd_deftet_sparse_render_forward_f64(int batch, int64_t num_pixels, int64_t num_faces,
+                                        int knum, int feat_dim, const double *pixel_coords,
+                                        const double *render_ranges, const double *fvz,
+                                        const double *fvi, const double *feat, float eps,
+                                        double *interp, int64_t *face_idx, double *weights,
+                                        void *workspace, size_t workspace_bytes, void *stream);
+int kd_deftet_sparse_render_backward_f32(int batch, int64_t num_pixels, int64_t num_faces,
+                                         int knum, int feat_dim, const float *grad_interp,
+                                         const int64_t *face_idx, const float *weights,
+                                         const float *fvi, const float *feat, float eps,
+                                         float *grad_fvi, float *grad_feat, void *stream);
+int kd_deftet_sparse_render_backward_f64(int batch, int64_t num_pixels, int64_t num_faces,
+                                         int knum, int feat_dim, const double *grad_interp,
+                                         const int64_t *face_idx, const double *weights,
+                                         const double *fvi, const double *feat, float eps,
+                                         double *grad_fvi, double *grad_feat, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -578,6 +578,60 @@ def rast_interpolate(rast, face_features):
     return interp, face_idx, weights
 
 
+# -------------------------------------------------------------------------------------------
+# deftet_sparse_render (deftet.py:269-417 -> deftet.cpp), SURVEY §8 f3
+# -------------------------------------------------------------------------------------------
+def deftet_sparse_render_forward(pixel_coords, render_ranges, face_vertices_z,
+                                 face_vertices_image, face_features, knum, eps):
+    """-> (interp (B, P, knum, D), face_idx (B, P, knum), weights (B, P, knum, 3))."""
+    fn = 'deftet_sparse_render'
+    dev = _check_same_gpu(fn, pixel_coords=pixel_coords, render_ranges=render_ranges,
+                          face_vertices_z=face_vertices_z,
+                          face_vertices_image=face_vertices_image, face_features=face_features)
+    B, F = face_vertices_z.shape[:2]
+    P = pixel_coords.shape[1]
+    D = face_features.shape[-1]
+    _check_size(fn, 'pixel_coords', pixel_coords, (B, P, 2))
+    _check_size(fn, 'render_ranges', render_ranges, (B, P, 2))
+    _check_size(fn, 'face_vertices_z', face_vertices_z, (B, F, 3))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'face_features', face_features, (B, F, 3, D))
+    sfx = _sfx(face_vertices_image, fn)
+    _check_dtype(fn, face_vertices_image, pixel_coords=pixel_coords, render_ranges=render_ranges,
+                 face_vertices_z=face_vertices_z, face_features=face_features)
+    knum = int(knum)
+    if knum < 1:
+        raise RuntimeError(f'{fn}: knum must be >= 1, got {knum}')
+    c = [t.contiguous() for t in (pixel_coords, render_ranges, face_vertices_z,
+                                  face_vertices_image, face_features)]
+    opts = dict(device=dev, dtype=face_vertices_image.dtype)
+    interp = torch.empty((B, P, knum, D), **opts)
+    face_idx = torch.empty((B, P, knum), device=dev, dtype=torch.long)
+    weights = torch.empty((B, P, knum, 3), **opts)
+    nb = int(_lib.load().kd_deftet_workspace_size(B, F, 1 if sfx == 'f64' else 0))
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+    _lib.call(f'kd_deftet_sparse_render_forward_{sfx}', B, P, F, knum, D, *(_ptr(t) for t in c),
+              float(eps), _ptr(interp), _ptr(face_idx), _ptr(weights), _ptr(ws), nb,
+              _stream(dev))
+    return interp, face_idx, weights
+
+
+def deftet_sparse_render_backward(grad_interp, face_idx, weights, face_vertices_image,
+                                  face_features, eps, need_feat=True):
+    """-> (grad_face_vertices_image, grad_face_features or None)."""
+    dev = face_idx.device
+    B, P, K = face_idx.shape
+    F, D = face_vertices_image.shape[1], face_features.shape[-1]
+    sfx = _sfx(face_vertices_image, 'deftet_sparse_render_backward')
+    gfvi = torch.empty_like(face_vertices_image)
+    gfeat = torch.empty_like(face_features) if need_feat else None
+    _lib.call(f'kd_deftet_sparse_render_backward_{sfx}', B, P, F, K, D,
+              _ptr(grad_interp.contiguous()), _ptr(face_idx), _ptr(weights),
+              _ptr(face_vertices_image), _ptr(face_features), float(eps), _ptr(gfvi),
+              _ptr(gfeat), _stream(dev))
+    return gfvi, gfeat
+
+
 render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
     rasterize_backward_cuda=rasterize_backward_cuda,
@@ -594,6 +648,8 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     texture_mapping_forward=texture_mapping_forward,
     texture_mapping_backward=texture_mapping_backward,
     rast_interpolate=rast_interpolate,
+    deftet_sparse_render_forward=deftet_sparse_render_forward,
+    deftet_sparse_render_backward=deftet_sparse_render_backward,
 ))
 metrics = types.SimpleNamespace(mask_iou_forward=mask_iou_forward,
                                 mask_iou_backward=mask_iou_backward)

@@ -56,6 +56,10 @@ _SIGS = {
     'kd_texture_mapping_forward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
                                    c_p, c_p],
     'kd_rast_interpolate': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_p],
+    'kd_deftet_sparse_render_forward': [c_int, c_i64, c_i64, c_int, c_int, c_p, c_p, c_p, c_p,
+                                        c_p, c_float, c_p, c_p, c_p, c_p, c_size, c_p],
+    'kd_deftet_sparse_render_backward': [c_int, c_i64, c_i64, c_int, c_int, c_p, c_p, c_p, c_p,
+                                         c_p, c_float, c_p, c_p, c_p],
     'kd_texture_mapping_backward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
                                     c_p, c_p, c_p, c_p],
 }
@@ -83,6 +87,8 @@ def load():
             lib.kd_dibr_pair_count.restype = c_i64
             lib.kd_mask_iou_workspace_size.argtypes = [c_int, c_i64, c_int]
             lib.kd_mask_iou_workspace_size.restype = c_size
+            lib.kd_deftet_workspace_size.argtypes = [c_int, c_i64, c_int]
+            lib.kd_deftet_workspace_size.restype = c_size
             lib.kd_last_error.argtypes = []
             lib.kd_last_error.restype = ctypes.c_char_p
             lib.kd_version.restype = c_int

@@ -2,3 +2,4 @@
 from .rasterization import rasterize, rasterize_from_rast  # noqa: F401
 from .dibr import dibr_soft_mask, dibr_rasterization  # noqa: F401
 from .utils import prepare_vertices, texture_mapping  # noqa: F401
+from .deftet import deftet_sparse_render  # noqa: F401
