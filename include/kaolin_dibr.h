@@ -323,7 +323,8 @@ int kd_mask_iou_backward_f64(int batch, int64_t pixels, const double *lhs, const
  * tex_batch_stride C * Ht * Wt (Bt == B) or 0 (one texture shared by every view); out (B, N, C).
  * mode 0 = nearest, 1 = bilinear.  The backward zeroes and fills grad_tex (the texture's layout
  * and batch stride; shared texture: summed over views) and grad_coords (B, N, 2); either may be
- * NULL.
+ * NULL.  sample_row = w for a dense (h, w) image (samples are grouped in 16 x 16 blocks whose
+ * texture gradient is summed in LDS), 0 for sparse points.
  * ------------------------------------------------------------------------------------------- */
 int kd_texture_mapping_forward_f32(int batch, int64_t num_samples, int channels, int tex_height,
                                    int tex_width, const float *coords, const float *tex,
@@ -333,13 +334,14 @@ int kd_texture_mapping_forward_f64(int batch, int64_t num_samples, int channels,
                                    int64_t tex_batch_stride, int mode, double *out, void *stream);
 int kd_texture_mapping_backward_f32(int batch, int64_t num_samples, int channels, int tex_height,
                                     int tex_width, const float *coords, const float *tex,
-                                    int64_t tex_batch_stride, int mode, const float *grad_out,
-                                    float *grad_tex, float *grad_coords, void *stream);
+                                    int64_t tex_batch_stride, int mode, int64_t sample_row,
+                                    const float *grad_out, float *grad_tex, float *grad_coords,
+                                    void *stream);
 int kd_texture_mapping_backward_f64(int batch, int64_t num_samples, int channels,
                                     int tex_height, int tex_width, const double *coords,
                                     const double *tex, int64_t tex_batch_stride, int mode,
-                                    const double *grad_out, double *grad_tex,
-                                    double *grad_coords, void *stream);
+                                    int64_t sample_row, const double *grad_out,
+                                    double *grad_tex, double *grad_coords, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * nvdiffrast_fwd compatibility (kaolin/render/mesh/rasterization.py:145-241): from an external

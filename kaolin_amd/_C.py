@@ -546,8 +546,9 @@ def texture_mapping_backward(grad_out, coords, tex, mode, need_coords=True, need
     gt = None
     if need_tex:
         gt = torch.empty(tex.shape, device=dev, dtype=tex.dtype)
+    row = coords.shape[2] if coords.dim() == 4 else 0  # dense (B, h, w, 2): 16 x 16 blocks
     _lib.call(f'kd_texture_mapping_backward_{sfx}', B, N, C, Ht, Wt, _ptr(coords), _ptr(tex_c),
-              bs, _TEX_MODES[mode], _ptr(go), _ptr(gt), _ptr(gc), _stream(dev))
+              bs, _TEX_MODES[mode], row, _ptr(go), _ptr(gt), _ptr(gc), _stream(dev))
     return gc, gt
 
 

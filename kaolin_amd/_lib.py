@@ -61,7 +61,7 @@ _SIGS = {
     'kd_deftet_sparse_render_backward': [c_int, c_i64, c_i64, c_int, c_int, c_p, c_p, c_p, c_p,
                                          c_p, c_float, c_p, c_p, c_p],
     'kd_texture_mapping_backward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
-                                    c_p, c_p, c_p, c_p],
+                                    c_i64, c_p, c_p, c_p, c_p],
 }
 
 

@@ -14,9 +14,10 @@
 // or a batch stride of 0 (one texture shared by all views: `expand` instead of the reference's
 // `repeat`), output (B, N, C) -- the reference's permuted result written directly.
 // One thread per sample, all C channels; each tap is C loads a plane apart.  Backward: the
-// texture gradient by float atomics (texels of neighbouring samples coincide) into a buffer zeroed
-// here, and for bilinear the coordinate gradient through border clipping, the y flip, the affine
-// map and the clamp (0 outside [0, 1], like torch.clamp's backward).
+// texture gradient summed per 16 x 16 sample block in LDS and flushed with one float atomic per
+// touched texel (kd_tex_bwd) into a buffer zeroed here, and for bilinear the coordinate gradient
+// through border clipping, the y flip, the affine map and the clamp (0 outside [0, 1], like
+// torch.clamp's backward).
 #include "kd_capi.hpp"
 #include "kd_common.hpp"
 
@@ -105,74 +106,152 @@ __global__ __launch_bounds__(kBlock) void kd_tex_fwd(TexArgs<T> a) {
   }
 }
 
+// Workgroup sample block: 16 x 16 samples of a dense image (row > 0: row length), otherwise 256
+// consecutive samples.
+__device__ __forceinline__ int64_t tex_sample(int64_t N, int64_t row, bool &ok) {
+  const int tid = threadIdx.x;
+  if (row > 0) {
+    const int64_t ntx = (row + 15) / 16, nrows = N / row;
+    const int64_t ty = blockIdx.x / ntx, tx = blockIdx.x - ty * ntx;
+    const int64_t x = tx * 16 + (tid & 15), y = ty * 16 + (tid >> 4);
+    ok = x < row && y < nrows;
+    return y * row + x;
+  }
+  const int64_t n = (int64_t)blockIdx.x * kBlock + tid;
+  ok = n < N;
+  return n;
+}
+
+__device__ __forceinline__ int wg_min_max(int lo, int hi, int *s, int &hi_out) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    lo = min(lo, __shfl_xor(lo, d));
+    hi = max(hi, __shfl_xor(hi, d));
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s[w] = lo;
+    s[4 + w] = hi;
+  }
+  __syncthreads();
+  lo = min(min(s[0], s[1]), min(s[2], s[3]));
+  hi_out = max(max(s[4], s[5]), max(s[6], s[7]));
+  __syncthreads();
+  return lo;
+}
+
+// Backward.  The texture gradient of a sample block is summed in LDS over the block's texel
+// footprint (neighbouring samples hit the same texels; same-address global atomics serialise in
+// L2) and flushed with one global atomic per touched texel and channel.  A footprint too large for
+// the LDS buffer falls back to per-sample global atomics.  Zero incoming gradients (the masked
+// background of an image loss) add nothing and are skipped.  The uv gradient is per sample.
 template <typename T, int MODE>
-__global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a) {
+__global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) {
+  constexpr int kLds = 32768 / sizeof(T);
+  __shared__ T s_acc[kLds];
+  __shared__ int s_red[8];
   const int b = blockIdx.y;
-  const int64_t n = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (n >= a.N) return;
+  bool ok;
+  const int64_t n = tex_sample(a.N, row, ok);
   const int64_t s = (int64_t)b * a.N + n;
-  T ix, iy, mx, my, cu, cv;
-  tex_coord<T>(a.coords + 2 * s, ix, iy, mx, my, cu, cv, a.Wt, a.Ht);
   const int64_t plane = (int64_t)a.Ht * a.Wt;
+  T ix = 0, iy = 0, mx = 0, my = 0, cu = 0, cv = 0;
+  if (ok) tex_coord<T>(a.coords + 2 * s, ix, iy, mx, my, cu, cv, a.Wt, a.Ht);
   const T *go = a.grad_out + s * a.C;
   T *gt = a.grad_tex ? a.grad_tex + (int64_t)b * a.tex_bstride : nullptr;
+  // taps: nearest (x0, y0) only; bilinear the 2 x 2 block at (x0, y0)
+  int x0, y0;
+  T ex = 0, wx = 0, ey = 0, wy = 0;
   if (MODE == KD_TEX_NEAREST) {
-    if (gt) {
-      const int x = (int)rint(ix), y = (int)rint(iy);
-      if (x >= 0 && x < a.Wt && y >= 0 && y < a.Ht)
-        for (int c = 0; c < a.C; ++c) atomicAdd(gt + c * plane + (int64_t)y * a.Wt + x, go[c]);
-    }
-    if (a.grad_coords) {  // nearest sampling has no coordinate gradient
-      a.grad_coords[2 * s] = (T)0;
-      a.grad_coords[2 * s + 1] = (T)0;
-    }
-    return;
+    x0 = (int)rint(ix);
+    y0 = (int)rint(iy);
+  } else {
+    x0 = (int)floor(ix);
+    y0 = (int)floor(iy);
+    ex = (T)(x0 + 1) - ix;
+    wx = ix - (T)x0;
+    ey = (T)(y0 + 1) - iy;
+    wy = iy - (T)y0;
   }
-  const T fx = floor(ix), fy = floor(iy);
-  const int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
-  const T ex = (T)x1 - ix, wx = ix - (T)x0, ey = (T)y1 - iy, wy = iy - (T)y0;
-  const bool vx0 = x0 >= 0 && x0 < a.Wt, vx1 = x1 >= 0 && x1 < a.Wt;
-  const bool vy0 = y0 >= 0 && y0 < a.Ht, vy1 = y1 >= 0 && y1 < a.Ht;
-  const int64_t o = (int64_t)y0 * a.Wt + x0;
-  const T *tex = a.tex + (int64_t)b * a.tex_bstride + o;
+  constexpr int kExt = MODE == KD_TEX_NEAREST ? 0 : 1;
+  bool act = false;
+  if (ok && gt)
+    for (int c = 0; c < a.C; ++c) act |= go[c] != (T)0;
+  // texel footprint of the block's contributing samples
+  int hx, hy;
+  const int lx = wg_min_max(act ? x0 : INT_MAX, act ? x0 + kExt : INT_MIN, s_red, hx);
+  const int ly = wg_min_max(act ? y0 : INT_MAX, act ? y0 + kExt : INT_MIN, s_red, hy);
+  const int64_t bw = (int64_t)hx - lx + 1, bh = (int64_t)hy - ly + 1;
+  const bool any = hx >= lx;
+  const bool lds = any && bw * bh * a.C <= kLds;
+  const int64_t nl = lds ? bw * bh * a.C : 0;
+  for (int64_t i = threadIdx.x; i < nl; i += kBlock) s_acc[i] = (T)0;
+  if (lds) __syncthreads();
+  auto add = [&](int c, int x, int y, T v) {
+    if (x < 0 || x >= a.Wt || y < 0 || y >= a.Ht) return;
+    if (lds)
+      atomicAdd(&s_acc[((int64_t)c * bh + (y - ly)) * bw + (x - lx)], v);
+    else
+      atomicAdd(gt + c * plane + (int64_t)y * a.Wt + x, v);
+  };
   T gix = (T)0, giy = (T)0;
-  for (int c = 0; c < a.C; ++c) {
-    const T g = go[c];
-    const T *tc = tex + c * plane;
-    if (gt) {
-      T *gc = gt + c * plane + o;
-      if (vy0 && vx0) atomicAdd(gc, ex * ey * g);
-      if (vy0 && vx1) atomicAdd(gc + 1, wx * ey * g);
-      if (vy1 && vx0) atomicAdd(gc + a.Wt, ex * wy * g);
-      if (vy1 && vx1) atomicAdd(gc + a.Wt + 1, wx * wy * g);
+  if (ok) {
+    const T *tex = a.tex + (int64_t)b * a.tex_bstride;
+    const bool vx0 = x0 >= 0 && x0 < a.Wt, vx1 = x0 + 1 >= 0 && x0 + 1 < a.Wt;
+    const bool vy0 = y0 >= 0 && y0 < a.Ht, vy1 = y0 + 1 >= 0 && y0 + 1 < a.Ht;
+    const T *t0 = tex + (int64_t)y0 * a.Wt + x0;
+    for (int c = 0; c < a.C; ++c) {
+      const T g = go[c];
+      if (act && g != (T)0) {
+        if (MODE == KD_TEX_NEAREST) {
+          add(c, x0, y0, g);
+        } else {
+          add(c, x0, y0, ex * ey * g);
+          add(c, x0 + 1, y0, wx * ey * g);
+          add(c, x0, y0 + 1, ex * wy * g);
+          add(c, x0 + 1, y0 + 1, wx * wy * g);
+        }
+      }
+      if (MODE == KD_TEX_BILINEAR && a.grad_coords) {
+        const T *tc = t0 + c * plane;
+        if (vy0 && vx0) {
+          const T v = tc[0];
+          gix -= v * ey * g;
+          giy -= v * ex * g;
+        }
+        if (vy0 && vx1) {
+          const T v = tc[1];
+          gix += v * ey * g;
+          giy -= v * wx * g;
+        }
+        if (vy1 && vx0) {
+          const T v = tc[a.Wt];
+          gix -= v * wy * g;
+          giy += v * ex * g;
+        }
+        if (vy1 && vx1) {
+          const T v = tc[a.Wt + 1];
+          gix += v * wy * g;
+          giy += v * wx * g;
+        }
+      }
     }
     if (a.grad_coords) {
-      if (vy0 && vx0) {
-        const T v = tc[0];
-        gix -= v * ey * g;
-        giy -= v * ex * g;
-      }
-      if (vy0 && vx1) {
-        const T v = tc[1];
-        gix += v * ey * g;
-        giy -= v * wx * g;
-      }
-      if (vy1 && vx0) {
-        const T v = tc[a.Wt];
-        gix -= v * wy * g;
-        giy += v * ex * g;
-      }
-      if (vy1 && vx1) {
-        const T v = tc[a.Wt + 1];
-        gix += v * wy * g;
-        giy += v * wx * g;
-      }
+      // nearest sampling has no coordinate gradient; bilinear: grid gradient -> [-1, 1] coords
+      // (x mx, y my) -> y flip and * 2 -> clamp mask
+      a.grad_coords[2 * s] = MODE == KD_TEX_BILINEAR && cu != (T)0 ? (mx * gix) * (T)2 : (T)0;
+      a.grad_coords[2 * s + 1] =
+          MODE == KD_TEX_BILINEAR && cv != (T)0 ? -(my * giy) * (T)2 : (T)0;
     }
   }
-  if (a.grad_coords) {
-    // grid gradient -> [-1, 1] coords (x mx, y my) -> y flip and *2 -> clamp mask
-    a.grad_coords[2 * s] = cu != (T)0 ? (mx * gix) * (T)2 : (T)0;
-    a.grad_coords[2 * s + 1] = cv != (T)0 ? -(my * giy) * (T)2 : (T)0;
+  if (!lds) return;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < nl; i += kBlock) {  // one atomic per touched texel
+    const T v = s_acc[i];
+    if (v == (T)0) continue;
+    const int64_t c = i / (bw * bh), r = i - c * bw * bh;
+    const int64_t y = ly + r / bw, x = lx + r % bw;
+    atomicAdd(gt + c * plane + y * a.Wt + x, v);
   }
 }
 
@@ -217,8 +296,8 @@ static int tex_forward(int B, int64_t N, int C, int Ht, int Wt, const T *coords,
 
 template <typename T>
 static int tex_backward(int B, int64_t N, int C, int Ht, int Wt, const T *coords, const T *tex,
-                        int64_t tex_bstride, int mode, const T *grad_out, T *grad_tex,
-                        T *grad_coords, hipStream_t stream) {
+                        int64_t tex_bstride, int mode, int64_t row, const T *grad_out,
+                        T *grad_tex, T *grad_coords, hipStream_t stream) {
   int rc = tex_check<T>(B, N, C, Ht, Wt, mode, tex_bstride);
   if (rc != KD_OK) return rc;
   KD_CHECK_ARG(grad_out || (!grad_tex && !grad_coords), "texture_mapping: grad_out is NULL");
@@ -231,14 +310,20 @@ static int tex_backward(int B, int64_t N, int C, int Ht, int Wt, const T *coords
     }
   }
   if (B == 0 || N == 0 || (!grad_tex && !grad_coords)) return KD_OK;
+  KD_CHECK_ARG(row >= 0 && (row == 0 || N % row == 0),
+               "texture_mapping: sample_row must be 0 or divide the sample count");
   TexArgs<T> a{N, C, Ht, Wt, coords, tex, tex_bstride, nullptr, grad_out, grad_tex, grad_coords};
-  const dim3 grid((unsigned)((N + kBlock - 1) / kBlock), (unsigned)B);
+  const int64_t blocks =
+      row > 0 ? ((row + 15) / 16) * ((N / row + 15) / 16) : (N + kBlock - 1) / kBlock;
+  KD_CHECK_ARG(blocks < (1ll << 31), "texture_mapping: too many samples");
+  const dim3 grid((unsigned)blocks, (unsigned)B);
   {
     ProfScope prof(K_TEX_BWD, stream);
     if (mode == KD_TEX_NEAREST)
-      hipLaunchKernelGGL((kd_tex_bwd<T, KD_TEX_NEAREST>), grid, dim3(kBlock), 0, stream, a);
+      hipLaunchKernelGGL((kd_tex_bwd<T, KD_TEX_NEAREST>), grid, dim3(kBlock), 0, stream, a, row);
     else
-      hipLaunchKernelGGL((kd_tex_bwd<T, KD_TEX_BILINEAR>), grid, dim3(kBlock), 0, stream, a);
+      hipLaunchKernelGGL((kd_tex_bwd<T, KD_TEX_BILINEAR>), grid, dim3(kBlock), 0, stream, a,
+                         row);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)
@@ -266,17 +351,18 @@ int kd_texture_mapping_forward_f64(int B, int64_t N, int C, int Ht, int Wt, cons
 }
 int kd_texture_mapping_backward_f32(int B, int64_t N, int C, int Ht, int Wt, const float *coords,
                                     const float *tex, int64_t tex_batch_stride, int mode,
-                                    const float *grad_out, float *grad_tex, float *grad_coords,
-                                    void *stream) {
-  return tex_backward<float>(B, N, C, Ht, Wt, coords, tex, tex_batch_stride, mode, grad_out,
-                             grad_tex, grad_coords, (hipStream_t)stream);
+                                    int64_t sample_row, const float *grad_out, float *grad_tex,
+                                    float *grad_coords, void *stream) {
+  return tex_backward<float>(B, N, C, Ht, Wt, coords, tex, tex_batch_stride, mode, sample_row,
+                             grad_out, grad_tex, grad_coords, (hipStream_t)stream);
 }
 int kd_texture_mapping_backward_f64(int B, int64_t N, int C, int Ht, int Wt,
                                     const double *coords, const double *tex,
-                                    int64_t tex_batch_stride, int mode, const double *grad_out,
-                                    double *grad_tex, double *grad_coords, void *stream) {
-  return tex_backward<double>(B, N, C, Ht, Wt, coords, tex, tex_batch_stride, mode, grad_out,
-                              grad_tex, grad_coords, (hipStream_t)stream);
+                                    int64_t tex_batch_stride, int mode, int64_t sample_row,
+                                    const double *grad_out, double *grad_tex,
+                                    double *grad_coords, void *stream) {
+  return tex_backward<double>(B, N, C, Ht, Wt, coords, tex, tex_batch_stride, mode, sample_row,
+                              grad_out, grad_tex, grad_coords, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -246,3 +246,45 @@ def test_texture_edge_cases():
         texture_mapping(torch.zeros((2, 4, 2), device=DEV), tex, mode='bicubic')
     with pytest.raises(RuntimeError):
         texture_mapping(torch.zeros((3, 4, 2), device=DEV), tex, mode='nearest')
+
+
+@pytest.mark.parametrize('k', ['f32', 'f64'])
+@pytest.mark.parametrize('mode', MODES)
+def test_texture_coherent_uvs_vs_torch(k, mode):
+    """Smooth uv fields (the LDS-summed texture gradient of 16 x 16 sample blocks) with a masked
+    background (zero gradient, uv = 0), odd image sizes (partial blocks), a shared texture."""
+    from kaolin_amd.render.mesh import texture_mapping
+    gen = torch.Generator(device='cpu').manual_seed(11)
+    B, h, w = 3, 77, 101
+    yy, xx = torch.meshgrid(torch.linspace(0, 1, h, dtype=torch.float64),
+                            torch.linspace(0, 1, w, dtype=torch.float64), indexing='ij')
+    uv = torch.stack([0.2 + 0.6 * xx + 0.05 * torch.sin(7 * yy),
+                      0.1 + 0.7 * yy + 0.05 * torch.cos(5 * xx)], -1)
+    uv = uv.unsqueeze(0).repeat(B, 1, 1, 1) + 0.01 * torch.rand((B, h, w, 2), generator=gen,
+                                                               dtype=torch.float64)
+    mask = ((xx - 0.5) ** 2 + (yy - 0.5) ** 2 < 0.16).unsqueeze(-1)
+    uv = torch.where(mask, uv, torch.zeros_like(uv))
+    go = torch.rand((B, h, w, 3), generator=gen, dtype=torch.float64) * mask
+    for tb in (B, 1):
+        tex = torch.rand((tb, 3, 64, 48), generator=gen, dtype=torch.float64)
+        u, t = uv.to(DEV, DT[k]).requires_grad_(True), tex.to(DEV, DT[k]).requires_grad_(True)
+        out = texture_mapping(u, t, mode=mode)
+        gu, gt = torch.autograd.grad(out, [u, t], go.to(DEV, DT[k]))
+        u2 = uv.clone().requires_grad_(True)
+        t2 = tex.clone().requires_grad_(True)
+        ref = torch_texture_mapping(u2, t2.expand(B, -1, -1, -1), mode)
+        ru, rt = torch.autograd.grad(ref, [u2, t2], go, allow_unused=True)
+        t_ = dict(rtol=1e-5, atol=1e-5) if k == 'f32' else dict(rtol=1e-11, atol=1e-11)
+        if mode == 'nearest':
+            # uvs on a linspace grid land on exact texel halves, where ATen's CPU kernel and the
+            # restated formula may round the source index differently: check the oracle
+            ou = uv.to(DT[k]).numpy()
+            np.testing.assert_array_equal(N(out), f2.texture_mapping(ou, N(t), mode))
+            _, ot = f2.texture_mapping_backward(go.to(DT[k]).numpy(), ou, N(t), mode)
+            np.testing.assert_allclose(N(gt), ot, **t_)
+            continue
+        np.testing.assert_allclose(N(out), ref.detach().numpy(), **t_)
+        np.testing.assert_allclose(N(gt), rt.numpy(), **t_)
+        if mode == 'bilinear':
+            gtol = dict(rtol=1e-3, atol=1e-3) if k == 'f32' else dict(rtol=1e-9, atol=1e-9)
+            np.testing.assert_allclose(N(gu), ru.numpy(), **gtol)
