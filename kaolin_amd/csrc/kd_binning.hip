@@ -21,7 +21,7 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view)
   s += align_up(sizeof(int) * (size_t)B * g.nct());
   s += align_up(sizeof(int) * (size_t)g.nct() * (size_t)(N > 0 ? N : 1));
   s += align_up(sizeof(float4) * 2 * (size_t)N);
-  s += align_up(sizeof(int32_t) * (size_t)B * fine_tiles(H, W));
+  s += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
   return s;
 }
 
@@ -41,8 +41,8 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   off += align_up(sizeof(int) * (size_t)bb.g.nct() * (size_t)(N > 0 ? N : 1));
   bb.cull = (float4 *)(base + off);
   off += align_up(sizeof(float4) * 2 * (size_t)N);
-  bb.order = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * (size_t)B * fine_tiles(H, W));
+  bb.order = (int2 *)(base + off);
+  off += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
   bb.cull_eps = 0.f;
   bb.clear = nullptr;
   bb.n_clear = 0;
@@ -289,11 +289,12 @@ __global__ __launch_bounds__(1024) void kd_tile_order(BinBuffers bb0, BinBuffers
   for (int v0 = 0; v0 < n; v0 += 1024 * kPer) {
     for (int i = tid; i < kWaves * kNB; i += 1024) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
-    int bk[kPer], nf[kPer];
+    int bk[kPer], nf[kPer], tot[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {  // coalesced: consecutive threads, consecutive bins
       const int v = v0 + k * 1024 + tid;
-      bk[k] = v < n ? 32 - __clz((unsigned)bb.totals[v]) : -1;
+      tot[k] = v < n ? bb.totals[v] : 0;
+      bk[k] = v < n ? 32 - __clz((unsigned)tot[k]) : -1;
       nf[k] = v < n ? fine_count(v) : 0;
     }
 #pragma unroll
@@ -331,7 +332,7 @@ __global__ __launch_bounds__(1024) void kd_tile_order(BinBuffers bb0, BinBuffers
       int pos = atomicAdd(&s_cnt[w][bk[k]], nf[k]);
       for (int ty = cy * per; ty < min(cy * per + per, nty); ++ty)
         for (int tx = cx * per; tx < min(cx * per + per, ntx); ++tx)
-          bb.order[pos++] = (b * nty + ty) * ntx + tx;
+          bb.order[pos++] = make_int2((b * nty + ty) * ntx + tx, tot[k]);
     }
     __syncthreads();
     if (tid == 0) s_base = s_next;

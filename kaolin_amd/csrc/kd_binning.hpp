@@ -19,7 +19,8 @@
 //                        room for the view's whole face count.
 //   cull   [N][2]        float4: fp32 raster edge-culling coefficients (raster_cull_coefs), only
 //                        written when BinBuffers::cull is set (fp32 rasterization).
-//   order  [B * tiles]   int32 (view * tiles + fine tile), heaviest coarse bin first.
+//   order  [B * tiles]   int2 (view * tiles + fine tile, coarse bin face count), heaviest
+//                        coarse bin first (the count saves the tile kernels a dependent load).
 #pragma once
 
 #include "kd_common.hpp"
@@ -35,7 +36,7 @@ struct BinBuffers {
   float cull_eps;  // the raster eps (cull coefficients only)
   int *clear;      // nullable: n_clear ints zeroed by kd_bin_count (counters of later passes)
   int n_clear;
-  int32_t *order;  // [B * fine tiles] (view, tile) sorted by the coarse bin's face count,
+  int2 *order;     // [B * fine tiles] (view * tiles + tile, its coarse bin's face count),
                    // heaviest first (kd_tile_order): the tile kernels' dispatch order
   int nchunk;
   BinGeom g;

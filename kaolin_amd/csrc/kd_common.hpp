@@ -18,7 +18,9 @@ namespace kd {
 // Bits: 1 skip the per-pixel face tests of the forward kernels, 2 skip staging face data,
 //       4 skip the per-batch work entirely (bin walk only), 8 fp32 raster: lane-per-pixel
 //       kernel instead of the pair pipeline, 16 / 32 skip the per-pair pass of the fp32
-//       raster / soft mask, 64 record per-tile durations into the kd_debug_buffer array.
+//       raster / soft mask, 64 record per-tile durations into the kd_debug_buffer array,
+//       8192 skip the fp32 raster's per-pixel epilogue (winner reload, output writes),
+//       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
 int debug_flags();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
 

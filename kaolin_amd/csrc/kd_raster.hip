@@ -77,11 +77,12 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
-  int b, tl;
-  tile_of_block(a.bb, H, W, b, tl);
+  int b, tl, nbin;
+  tile_of_block(a.bb, H, W, b, tl, nbin);
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const TileGeom t = tile_geom(H, W, tl);
+  TileGeom t = tile_geom(H, W, tl);
+  t.nbin = nbin;
   const T x0 = (T)px_cx(fs.M, W, t.px);
   const T y0 = (T)px_cy(fs.M, H, t.py);
 
@@ -187,12 +188,14 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
   const FaceSet<float> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const float M = fs.M;
-  int b, tl;
-  tile_of_block(a.bb, H, W, b, tl);
+  if (a.fs.dbg & 16384) return;  // diagnostics: dispatch cost only
+  int b, tl, nbin;
+  tile_of_block(a.bb, H, W, b, tl, nbin);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const TileGeom t = tile_geom(H, W, tl);
+  TileGeom t = tile_geom(H, W, tl);
+  t.nbin = nbin;
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
   s_key[w][lane] = 0ull;
   if (lane == 0) s_nan[w] = 0ull;
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<floa
   };
   tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
 
-  if (!t.inimg) return;
+  if (!t.inimg || (fs.dbg & 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const float x0 = px_cx(M, W, t.px), y0 = px_cy(M, H, t.py);
   int best = -1;

@@ -169,12 +169,14 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairB
 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
-  int b, tl;
-  tile_of_block(a.bb, H, W, b, tl);
+  if (fs.dbg & 16384) return;  // diagnostics: dispatch cost only
+  int b, tl, nbin;
+  tile_of_block(a.bb, H, W, b, tl, nbin);
   const int tid = threadIdx.x, w = tid >> 6;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const TileGeom t = tile_geom(H, W, tl);
+  TileGeom t = tile_geom(H, W, tl);
+  t.nbin = nbin;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const bool unc = t.inimg && a.face_idx[p] < 0;
   const bool wave_unc = __ballot(unc) != 0ull;

@@ -28,20 +28,23 @@ struct TileGeom {
   int WX0, WX1, WY0, WY1;  // this wave's 8x8 sub-tile
   int px, py;              // this lane's pixel
   bool inimg, wave_live;
+  int nbin;                // faces in the tile's coarse bin when known (tile order), else -1
 };
 
 // (view, fine tile) of this workgroup: the bins' heaviest-first order (kd_tile_order) when the
 // bins were built, else (blockIdx.y, blockIdx.x).
 __device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W, int &b,
-                                              int &tile) {
+                                              int &tile, int &nbin) {
   if (bb.order && bb.nchunk > 0) {
     const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    const int v = bb.order[blockIdx.y * gridDim.x + blockIdx.x];
-    b = v / ntiles;
-    tile = v - b * ntiles;
+    const int2 v = bb.order[blockIdx.y * gridDim.x + blockIdx.x];
+    b = v.x / ntiles;
+    tile = v.x - b * ntiles;
+    nbin = v.y;
   } else {
     b = blockIdx.y;
     tile = blockIdx.x;
+    nbin = -1;
   }
 }
 
@@ -62,6 +65,7 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
   t.py = t.WY0 + (lane >> 3);
   t.inimg = t.px < W && t.py < H;
   t.wave_live = t.WX0 < W && t.WY0 < H;
+  t.nbin = -1;
   return t;
 }
 __device__ __forceinline__ TileGeom tile_geom(int H, int W) { return tile_geom(H, W, blockIdx.x); }
@@ -125,7 +129,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 / g.ct) * g.nctx + (t.X0 / g.ct);
-  const int n = bb.totals[(int64_t)b * g.nct() + ct];
+  const int n = t.nbin >= 0 ? t.nbin : bb.totals[(int64_t)b * g.nct() + ct];
   const int *bin = bb.bins + (int64_t)ct * N + lo;
   int cnt = 0;
   // kPrefetch chunks of bin entries and their spans are loaded up front (two dependent
