@@ -19,7 +19,7 @@ OBJDIR = os.path.join(PKG, 'build')
 SOURCES = ['kd_capi.cpp', 'kd_binning.hip', 'kd_raster.hip', 'kd_softmask.hip', 'kd_softpair.hip',
            'kd_prepare.hip', 'kd_dibr.hip', 'kd_metrics.hip', 'kd_texture.hip',
            'kd_rastcompat.hip', 'kd_deftet.hip']
-HEADERS = ['kd_common.hpp', 'kd_binning.hpp', 'kd_capi.hpp']
+HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith('.hpp'))  # every source depends on all
 ARCH = os.environ.get('KAOLIN_AMD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', f'--offload-arch={ARCH}',

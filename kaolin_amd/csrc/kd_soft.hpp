@@ -196,7 +196,7 @@ template <typename T>
 struct SoftPairBuf {
   SoftPairRec *rec;   // [B * ntiles][cap]
   SoftCoef<T> *coef;  // [B * ntiles][cap] backward coefficients
-  T *sprob;           // [K][B * H * W] probability by (slot, pixel)
+  T *sprob;           // [B * ntiles][cap] probability of each record
   int32_t *npix;      // [B * H * W] close faces of each uncovered pixel
   int32_t *ntile;     // [B * ntiles][2]: records, faces in the tile list
   int2 *items;        // [B * ntiles * ceil(cap / 256)] (tile, 256-record chunk) work items

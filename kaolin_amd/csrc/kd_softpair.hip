@@ -36,7 +36,7 @@ size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int 
   size_t s = bin_workspace_bytes(B, H, W, N, F);
   s += align_up(sizeof(SoftPairRec) * (size_t)(tiles * cap));
   s += align_up((size_t)esize * 4 * (size_t)(tiles * cap));
-  s += align_up((size_t)esize * (size_t)(P * K));
+  s += align_up((size_t)esize * (size_t)(tiles * cap));
   s += align_up(sizeof(int32_t) * (size_t)P);
   s += align_up(sizeof(int32_t) * 2 * (size_t)tiles);
   s += align_up(sizeof(int2) * (size_t)(tiles * ((cap + kBlock - 1) / kBlock)));
@@ -59,7 +59,7 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   pb.coef = (SoftCoef<T> *)(base + off);
   off += align_up(sizeof(T) * 4 * (size_t)(tiles * pb.cap));
   pb.sprob = (T *)(base + off);
-  off += align_up(sizeof(T) * (size_t)(P * K));
+  off += align_up(sizeof(T) * (size_t)(tiles * pb.cap));
   pb.npix = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)P);
   pb.ntile = (int32_t *)(base + off);
@@ -263,6 +263,54 @@ __device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et,
   }
 }
 
+// soft = 1 - prod(1 - p) over the close faces of the 256 pixels of one tile, in slot order
+// (dibr_soft_mask_cuda.cu:174-181, double-promoted product).  The probabilities are stored in
+// record order; kReduceSlots slots at a time are placed into an LDS table by (slot, pixel) and
+// each pixel lane multiplies its slots in order.  Pixels without close faces were written by
+// kd_soft_pairs.
+constexpr int kReduceSlots = 32;
+
+template <typename T>
+__device__ __forceinline__ void soft_reduce_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
+                                                 int64_t tile, T (*s_p)[kBlock]) {
+  const int K = a.K, H = a.fs.H, W = a.fs.W;
+  const int tid = threadIdx.x;
+  const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+  const int n = pb.ntile[2 * tile];
+  int px, py;
+  tile_pixel(tl % pb.ntx, tl / pb.ntx, tid, px, py);
+  const bool in = px < W && py < H;
+  const int64_t p = ((int64_t)b * H + py) * W + px;
+  const int np = in ? pb.npix[p] : 0;
+  const SoftPairRec *rec = pb.rec + tile * pb.cap;
+  const T *pr = pb.sprob + tile * pb.cap;
+  T prod = (T)1.0;
+  for (int s0 = 0; s0 < K; s0 += kReduceSlots) {
+    __syncthreads();  // the previous pass is done with s_p
+    for (int i = tid; i < n; i += kBlock) {
+      const uint32_t sq = __builtin_nontemporal_load((const uint32_t *)(rec + i) + 2);
+      const int s = (int)(sq & 0xffffu) - s0;  // slot | q << 16 | type << 24
+      if (s >= 0 && s < kReduceSlots) s_p[s][(sq >> 16) & 0xffu] = pr[i];
+    }
+    __syncthreads();
+    const int e = min(np - s0, kReduceSlots);
+    for (int s = 0; s < e; ++s) prod = (T)((double)prod * (1.0 - (double)s_p[s][tid]));
+    if (__syncthreads_and(np <= s0 + kReduceSlots)) break;
+  }
+  if (np > 0) a.soft[p] = (T)(1.0 - (double)prod);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  __shared__ T s_p[kReduceSlots][kBlock];
+  const int ntl = pb.counters[1];
+  for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) soft_reduce_tile<T>(a, pb, pb.tiles[ti], s_p);
+}
+
+// Flat over the (tile, 256-record chunk) items: each record's distance type and probability
+// (bit-identical to the reference), its backward coefficients (GRAD) and optionally the close
+// lists.  (Reducing a tile in the workgroup that finishes its last chunk needs a device-scope
+// release per item -- an L2 writeback on gfx950 -- and measured 30x slower than kd_soft_reduce.)
 template <typename T, bool GRAD, bool LISTS>
 __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftPairBuf<T> pb) {
   const FaceSet<T> &fs = a.fs;
@@ -274,65 +322,37 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
     const int64_t tile = item.x;
     const int n = pb.ntile[2 * tile];
     const int i = item.y * kBlock + threadIdx.x;
-    if (i >= n) continue;
-    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-    const int tx = tl % pb.ntx, ty = tl / pb.ntx;
-    int64_t lo, hi;
-    view_range(fs, b, lo, hi);
-    SoftPairRec *rp = pb.rec + tile * pb.cap + i;
-    const SoftPairRec r = *rp;
-    int px, py;
-    tile_pixel(tx, ty, r.q, px, py);
-    const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
-    T v[6];
-    load_corners(fs, (int64_t)r.row, v);
-    int et = 0;
-    T prob = (T)0;
-    if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
-    const int64_t gp = ((int64_t)b * H + py) * W + px;
-    pb.sprob[(int64_t)r.slot * pb.npixels + gp] = prob;
-    rp->type = (uint8_t)et;
-    if (LISTS) {
-      const int64_t o = gp * K + r.slot;
-      a.prob[o] = prob;
-      a.cidx[o] = (int64_t)r.row - lo;
-      a.ctype[o] = (uint8_t)(et + 1);
+    if (i < n) {
+      const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+      const int tx = tl % pb.ntx, ty = tl / pb.ntx;
+      int64_t lo, hi;
+      view_range(fs, b, lo, hi);
+      SoftPairRec *rp = pb.rec + tile * pb.cap + i;
+      const SoftPairRec r = *rp;
+      int px, py;
+      tile_pixel(tx, ty, r.q, px, py);
+      const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
+      T v[6];
+      load_corners(fs, (int64_t)r.row, v);
+      int et = 0;
+      T prob = (T)0;
+      if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+      const int64_t gp = ((int64_t)b * H + py) * W + px;
+      pb.sprob[tile * pb.cap + i] = prob;  // record order: coalesced
+      rp->type = (uint8_t)et;
+      if (LISTS) {
+        const int64_t o = gp * K + r.slot;
+        a.prob[o] = prob;
+        a.cidx[o] = (int64_t)r.row - lo;
+        a.ctype[o] = (uint8_t)(et + 1);
+      }
+      if (a.last && r.slot == K - 1) a.last[gp] = (int32_t)((int64_t)r.row - lo);
+      if (GRAD) {
+        SoftCoef<T> c;
+        soft_pair_coef<T>(x0, y0, v, et, prob, M, c.h);
+        pb.coef[tile * pb.cap + i] = c;
+      }
     }
-    if (a.last && r.slot == K - 1) a.last[gp] = (int32_t)((int64_t)r.row - lo);
-    if (GRAD) {
-      SoftCoef<T> c;
-      soft_pair_coef<T>(x0, y0, v, et, prob, M, c.h);
-      pb.coef[tile * pb.cap + i] = c;
-    }
-  }
-}
-
-// soft = 1 - prod(1 - p) over the close faces in slot order, for the pixels that have any (the
-// tiles with records); every other pixel was written by kd_soft_pairs.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPairBuf<T> pb) {
-  const int H = a.fs.H, W = a.fs.W;
-  const int ntl = pb.counters[1];
-  for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) {
-    const int64_t tile = pb.tiles[ti];
-    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-    int px, py;
-    tile_pixel(tl % pb.ntx, tl / pb.ntx, threadIdx.x, px, py);
-    if (px >= W || py >= H) continue;
-    const int64_t p = ((int64_t)b * H + py) * W + px;
-    const int n = pb.npix[p];
-    if (n == 0) continue;
-    T prod = (T)1.0;
-    const T *sp = pb.sprob + p;
-    for (int s0 = 0; s0 < n; s0 += 8) {  // 8 loads in flight, then the ordered product
-      T v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = s0 + j < n ? sp[(int64_t)(s0 + j) * pb.npixels] : (T)0;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)  // dibr_soft_mask_cuda.cu:174-178, slot order
-        if (s0 + j < n) prod = (T)((double)prod * (1.0 - (double)v[j]));
-    }
-    a.soft[p] = (T)(1.0 - (double)prod);  // :181
   }
 }
 
@@ -450,7 +470,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   {
     ProfScope prof(K_SOFT_MATH, stream);
-    const dim3 grid(kPersistentBlocks);
+    const dim3 grid((a.fs.dbg & 2048) ? 512 : (a.fs.dbg & 4096) ? 8192 : kPersistentBlocks);
     const bool lists = a.prob != nullptr;
     if (grad && lists)
       hipLaunchKernelGGL((kd_soft_pair_math<T, true, true>), grid, dim3(kBlock), 0, stream, a, pb);
@@ -462,10 +482,10 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
       hipLaunchKernelGGL((kd_soft_pair_math<T, false, false>), grid, dim3(kBlock), 0, stream, a,
                          pb);
   }
-  if (reduce) {
+  if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
-    const unsigned g = (a.fs.dbg & 2048) ? 256 : (a.fs.dbg & 4096) ? 8192 : kPersistentBlocks;
-    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(g), dim3(kBlock), 0, stream, a, pb);
+    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a,
+                       pb);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
