@@ -225,6 +225,11 @@ template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
   const FaceSet<T> &fs = jobs.fs[blockIdx.z];
   const BinBuffers &bb = jobs.bb[blockIdx.z];
+  if (blockIdx.x == gridDim.x - 1) {  // the extra column: the set's tile dispatch order
+    if (blockIdx.y == 0)
+      tile_order(bb, fs.B, (fs.W + kTile - 1) / kTile, (fs.H + kTile - 1) / kTile);
+    return;
+  }
   // 256-bit membership mask per coarse tile: bit t set <=> face (chunk*256 + t) touches it.
   extern __shared__ uint32_t s_mask[];  // [nct][8]
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
@@ -268,15 +273,15 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
 
 // Dispatch order of the tile kernels: (view, fine tile) by descending bit length of its coarse
 // bin's face count (a proxy for its work), so the heaviest tiles start first and the grid's
-// tail is short.  One 1024-thread workgroup per job, one coarse tile (and its <= (ct/16)^2 fine
-// tiles) per thread and pass; histograms and cursors are kept per wave.  Order within a bucket
-// follows the (view, coarse tile) index; results never depend on the order.
-__global__ __launch_bounds__(1024) void kd_tile_order(BinBuffers bb0, BinBuffers bb1, int B,
-                                                      int ntx, int nty) {
-  constexpr int kNB = 33, kWaves = 16, kPer = 4;
+// tail is short.  Run by one extra 256-thread workgroup of kd_bin_scatter per face set (it only
+// needs the scan's totals, so it overlaps the scatter instead of taking a launch of its own):
+// one coarse tile (and its <= (ct/16)^2 fine tiles) per thread and pass, histograms and cursors
+// per wave.  Order within a bucket follows the (view, coarse tile) index; results never depend
+// on the order.  Each entry also carries the coarse bin's face count.
+__device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty) {
+  constexpr int kNB = 33, kWaves = kBlock / kWave, kPer = 8;
   __shared__ int s_cnt[kWaves][kNB];
   __shared__ int s_base, s_next;
-  const BinBuffers &bb = blockIdx.x ? bb1 : bb0;
   const int tid = threadIdx.x, w = tid >> 6;
   const int nct = bb.g.nct(), n = B * nct;
   const int per = bb.g.ct / kTile;  // fine tiles per coarse tile side
@@ -286,13 +291,13 @@ __global__ __launch_bounds__(1024) void kd_tile_order(BinBuffers bb0, BinBuffers
     return (min(cx * per + per, ntx) - cx * per) * (min(cy * per + per, nty) - cy * per);
   };
   if (tid == 0) s_base = 0;
-  for (int v0 = 0; v0 < n; v0 += 1024 * kPer) {
-    for (int i = tid; i < kWaves * kNB; i += 1024) (&s_cnt[0][0])[i] = 0;
+  for (int v0 = 0; v0 < n; v0 += kBlock * kPer) {
+    for (int i = tid; i < kWaves * kNB; i += kBlock) (&s_cnt[0][0])[i] = 0;
     __syncthreads();
     int bk[kPer], nf[kPer], tot[kPer];
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {  // coalesced: consecutive threads, consecutive bins
-      const int v = v0 + k * 1024 + tid;
+      const int v = v0 + k * kBlock + tid;
       tot[k] = v < n ? bb.totals[v] : 0;
       bk[k] = v < n ? 32 - __clz((unsigned)tot[k]) : -1;
       nf[k] = v < n ? fine_count(v) : 0;
@@ -305,13 +310,13 @@ __global__ __launch_bounds__(1024) void kd_tile_order(BinBuffers bb0, BinBuffers
       const int lane = tid & 63;
       const int kb = kNB - 1 - lane;  // lane 0 = heaviest bucket
       int c[kWaves];
-      int tot = 0;
+      int t = 0;
 #pragma unroll
       for (int ww = 0; ww < kWaves; ++ww) {
         c[ww] = kb >= 0 ? s_cnt[ww][kb] : 0;
-        tot += c[ww];
+        t += c[ww];
       }
-      int run = s_base + wave_incl_scan(tot) - tot;
+      int run = s_base + wave_incl_scan(t) - t;
       if (kb >= 0) {
 #pragma unroll
         for (int ww = 0; ww < kWaves; ++ww) {
@@ -319,14 +324,14 @@ __global__ __launch_bounds__(1024) void kd_tile_order(BinBuffers bb0, BinBuffers
           run += c[ww];
         }
       }
-      const int all = __builtin_amdgcn_readlane(wave_incl_scan(tot), 63);
+      const int all = __builtin_amdgcn_readlane(wave_incl_scan(t), 63);
       if (lane == 0) s_next = s_base + all;
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       if (bk[k] < 0) continue;
-      const int v = v0 + k * 1024 + tid;
+      const int v = v0 + k * kBlock + tid;
       const int b = v / nct, c = v - b * nct;
       const int cx = c % bb.g.nctx, cy = c / bb.g.nctx;
       int pos = atomicAdd(&s_cnt[w][bk[k]], nf[k]);
@@ -367,16 +372,10 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
     hipLaunchKernelGGL(kd_bin_scan, grid_t, dim3(kBlock), 0, stream, jobs.bb[0],
                        jobs.bb[njobs - 1]);
   }
-  {
+  {  // + one column of workgroups for the tile order (kd_bin_scatter, tile_order)
     ProfScope prof(K_BIN_SCATTER, stream);
-    hipLaunchKernelGGL(kd_bin_scatter<T>, grid_c, dim3(kBlock),
+    hipLaunchKernelGGL(kd_bin_scatter<T>, dim3(bb.nchunk + 1, fs.B, njobs), dim3(kBlock),
                        sizeof(uint32_t) * 8 * bb.g.nct(), stream, jobs);
-  }
-  {
-    ProfScope prof(K_TILE_ORDER, stream);
-    hipLaunchKernelGGL(kd_tile_order, dim3(njobs), dim3(1024), 0, stream, jobs.bb[0],
-                       jobs.bb[njobs - 1], fs.B, (fs.W + kTile - 1) / kTile,
-                       (fs.H + kTile - 1) / kTile);
   }
   return hipGetLastError();
 }

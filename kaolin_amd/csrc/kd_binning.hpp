@@ -37,7 +37,7 @@ struct BinBuffers {
   int *clear;      // nullable: n_clear ints zeroed by kd_bin_count (counters of later passes)
   int n_clear;
   int2 *order;     // [B * fine tiles] (view * tiles + tile, its coarse bin's face count),
-                   // heaviest first (kd_tile_order): the tile kernels' dispatch order
+                   // heaviest first (tile_order in kd_bin_scatter): the tile kernels' dispatch order
   int nchunk;
   BinGeom g;
 };

@@ -31,7 +31,7 @@ struct TileGeom {
   int nbin;                // faces in the tile's coarse bin when known (tile order), else -1
 };
 
-// (view, fine tile) of this workgroup: the bins' heaviest-first order (kd_tile_order) when the
+// (view, fine tile) of this workgroup: the bins' heaviest-first order (tile_order) when the
 // bins were built, else (blockIdx.y, blockIdx.x).
 __device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W, int &b,
                                               int &tile, int &nbin) {
