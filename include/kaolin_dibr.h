@@ -213,7 +213,10 @@ int kd_dibr_soft_mask_backward_binned_f64(int batch, int height, int width, int6
  * weights (B, H, W, 3), soft (B, H, W).  With want_grad the workspace keeps what the backward
  * needs; pass the same workspace to the backward.  Workspace: kd_dibr_workspace_size().
  * The backward writes grad_fvi (B, F, 3, 2) = raster + soft-mask gradients (one buffer) and
- * grad_feat (nullable); grad_interp / grad_soft NULL = zero.
+ * grad_feat (nullable); grad_interp / grad_soft NULL = zero.  A forward with want_grad may zero
+ * the backward's gradient buffers (grad_fvi_zero (B, F, 3, 2), grad_feat_zero (B, F, 3, D),
+ * nullable) inside one of its kernels; the backward then takes them with grads_zeroed = 1 and
+ * skips its own fill launch.
  * ------------------------------------------------------------------------------------------- */
 size_t kd_dibr_workspace_size(int batch, int height, int width, int64_t num_faces, int knum,
                               int double_precision);
@@ -228,8 +231,8 @@ int kd_dibr_rasterization_forward_f32(int batch, int height, int width, int64_t 
                                       int64_t normals_z_stride, double multiplier, float eps,
                                       float sigmainv, double boxlen, int knum, float *interp,
                                       int64_t *face_idx, float *weights, float *soft,
-                                      int want_grad, void *workspace, size_t workspace_bytes,
-                                      void *stream);
+                                      int want_grad, float *grad_fvi_zero, float *grad_feat_zero,
+                                      void *workspace, size_t workspace_bytes, void *stream);
 int kd_dibr_rasterization_forward_f64(int batch, int height, int width, int64_t num_faces,
                                       int feat_dim, const double *fvz, int64_t fvz_face_stride,
                                       int64_t fvz_corner_stride, const double *fvi,
@@ -237,15 +240,15 @@ int kd_dibr_rasterization_forward_f64(int batch, int height, int width, int64_t 
                                       int64_t normals_z_stride, double multiplier, float eps,
                                       float sigmainv, double boxlen, int knum, double *interp,
                                       int64_t *face_idx, double *weights, double *soft,
-                                      int want_grad, void *workspace, size_t workspace_bytes,
-                                      void *stream);
+                                      int want_grad, double *grad_fvi_zero, double *grad_feat_zero,
+                                      void *workspace, size_t workspace_bytes, void *stream);
 int kd_dibr_rasterization_backward_f32(int batch, int height, int width, int64_t num_faces,
                                        int feat_dim, const float *grad_interp,
                                        const float *grad_soft, const int64_t *face_idx,
                                        const float *weights, const float *soft, const float *fvi,
                                        const float *feat, float eps, double multiplier,
                                        double boxlen, float sigmainv, int knum, float *grad_fvi,
-                                       float *grad_feat, void *workspace,
+                                       float *grad_feat, int grads_zeroed, void *workspace,
                                        size_t workspace_bytes, void *stream);
 int kd_dibr_rasterization_backward_f64(int batch, int height, int width, int64_t num_faces,
                                        int feat_dim, const double *grad_interp,
@@ -254,7 +257,8 @@ int kd_dibr_rasterization_backward_f64(int batch, int height, int width, int64_t
                                        const double *fvi, const double *feat, float eps,
                                        double multiplier, double boxlen, float sigmainv,
                                        int knum, double *grad_fvi, double *grad_feat,
-                                       void *workspace, size_t workspace_bytes, void *stream);
+                                       int grads_zeroed, void *workspace, size_t workspace_bytes,
+                                       void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * prepare_vertices (kaolin/render/mesh/utils.py:128-175 with camera_transform): camera

@@ -397,9 +397,10 @@ def _rows_view(t, F, inner):
 
 def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertices_image,
                                      face_features, face_normals_z, sigmainv, boxlen, knum,
-                                     multiplier, eps, want_grad=True):
+                                     multiplier, eps, want_grad=True, grad_buffers=None):
     """rasterize(valid = normals_z >= 0) + dibr_soft_mask in one launch sequence.  Returns
-    (interp, face_idx, weights, soft, workspace)."""
+    (interp, face_idx, weights, soft, workspace).  grad_buffers = (grad_fvi, grad_feat or None):
+    buffers of the backward that this forward zeroes (see kd_dibr_rasterization_forward)."""
     fn = 'dibr_rasterization'
     dev = _check_same_gpu(fn, face_vertices_z=face_vertices_z,
                           face_vertices_image=face_vertices_image, face_features=face_features,
@@ -431,27 +432,35 @@ def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertic
     _lib.call(f'kd_dibr_rasterization_forward_{sfx}', B, height, width, F, D, _ptr(fvz), fvz_fs,
               fvz_cs, _ptr(fvi), _ptr(feat), _ptr(nz), nz_s, float(multiplier), float(eps),
               float(sigmainv), float(boxlen), knum, _ptr(interp), _ptr(face_idx), _ptr(weights),
-              _ptr(soft), 1 if want_grad else 0, _ptr(ws), nb, _stream(dev))
+              _ptr(soft), 1 if want_grad else 0,
+              _ptr(grad_buffers[0]) if grad_buffers else None,
+              _ptr(grad_buffers[1]) if grad_buffers else None, _ptr(ws), nb, _stream(dev))
     return interp, face_idx, weights, soft, ws
 
 
 def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights, soft,
                                       face_vertices_image, face_features, eps, multiplier,
-                                      boxlen, sigmainv, knum, workspace, need_feat=True):
-    """Gradients (grad_fvi, grad_feat or None) of the fused forward, from its workspace."""
+                                      boxlen, sigmainv, knum, workspace, need_feat=True,
+                                      grad_buffers=None):
+    """Gradients (grad_fvi, grad_feat or None) of the fused forward, from its workspace;
+    grad_buffers: the (grad_fvi, grad_feat) the forward zeroed, filled in place."""
     dev = face_idx.device
     B, F = face_vertices_image.shape[:2]
     H, W = face_idx.shape[1:3]
     D = face_features.shape[-1]
     sfx = _sfx(face_vertices_image, 'dibr_rasterization_backward')
-    gfvi = torch.empty_like(face_vertices_image)
-    gfeat = torch.empty_like(face_features) if need_feat else None
+    zeroed = grad_buffers is not None and (grad_buffers[1] is not None or not need_feat)
+    if zeroed:
+        gfvi, gfeat = grad_buffers[0], grad_buffers[1] if need_feat else None
+    else:
+        gfvi = torch.empty_like(face_vertices_image)
+        gfeat = torch.empty_like(face_features) if need_feat else None
     c = (lambda t: None if t is None else t.contiguous())  # noqa: E731
     _lib.call(f'kd_dibr_rasterization_backward_{sfx}', B, H, W, F, D, _ptr(c(grad_interp)),
               _ptr(c(grad_soft)), _ptr(face_idx), _ptr(weights), _ptr(soft),
               _ptr(face_vertices_image), _ptr(face_features), float(eps), float(multiplier),
               float(boxlen), float(sigmainv), int(knum), _ptr(gfvi), _ptr(gfeat),
-              _ptr(workspace), workspace.numel(), _stream(dev))
+              1 if zeroed else 0, _ptr(workspace), workspace.numel(), _stream(dev))
     return gfvi, gfeat
 
 

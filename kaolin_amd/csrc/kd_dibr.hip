@@ -60,8 +60,8 @@ template <typename T>
 static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t fvz_fs,
                     int64_t fvz_cs, const T *fvi, const T *feat, const T *nz, int64_t nz_stride,
                     double M, float eps, float sigmainv, double boxlen, int K, T *interp,
-                    int64_t *face_idx, T *weights, T *soft, int want_grad, void *ws,
-                    size_t wsb, void *stream_) {
+                    int64_t *face_idx, T *weights, T *soft, int want_grad, T *gz_fvi,
+                    T *gz_feat, void *ws, size_t wsb, void *stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
   KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
@@ -71,7 +71,10 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   const size_t need = dibr_workspace_bytes(B, H, W, F, K, sizeof(T));
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
-  if (B == 0 || H == 0 || W == 0) return KD_OK;
+  const int64_t nf = (int64_t)B * F;
+  if (!want_grad) gz_fvi = gz_feat = nullptr;
+  if (B == 0 || H == 0 || W == 0)
+    return zero_buffers<T>(gz_fvi, nf * 6, gz_feat, gz_feat ? nf * 3 * D : 0, stream);
   DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
   // raster: valid faces (normals z >= 0, dibr.py:195), tight boxes; soft: all faces, +-boxlen*M
   FaceSet<T> rfs = dibr_faceset<T>(B, H, W, F, fvi, M);
@@ -97,6 +100,12 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   sa.K = K;
   sa.sigmainv = sigmainv;
   sa.soft = soft;
+  // the backward's gradient buffers are zeroed by the soft reduction (latency-bound, so the
+  // fill is nearly free there) instead of a fill launch of the backward
+  sa.zero0 = gz_fvi;
+  sa.nzero0 = gz_fvi ? nf * 6 : 0;
+  sa.zero1 = gz_feat;
+  sa.nzero1 = gz_feat ? nf * 3 * D : 0;
   return soft_pairs_launch<T>(sa, d.pb, want_grad != 0, true, stream);
 }
 
@@ -104,7 +113,7 @@ template <typename T>
 static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
                     const T *grad_soft, const int64_t *face_idx, const T *weights, const T *soft,
                     const T *fvi, const T *feat, float eps, double M, double boxlen,
-                    float sigmainv, int K, T *gfvi, T *gfeat, void *ws, size_t wsb,
+                    float sigmainv, int K, T *gfvi, T *gfeat, int zeroed, void *ws, size_t wsb,
                     void *stream_) {
   hipStream_t stream = (hipStream_t)stream_;
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
@@ -114,7 +123,7 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   const int64_t nf = (int64_t)B * F;
-  int rc = zero_buffers<T>(gfvi, nf * 6, gfeat, gfeat ? nf * 3 * D : 0, stream);
+  int rc = zeroed ? KD_OK : zero_buffers<T>(gfvi, nf * 6, gfeat, gfeat ? nf * 3 * D : 0, stream);
   if (rc != KD_OK || B == 0 || H == 0 || W == 0) return rc;
   if (grad_soft) {
     DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
@@ -173,11 +182,12 @@ int kd_dibr_rasterization_forward_f32(int B, int H, int W, int64_t F, int D, con
                                       const float *normals_z, int64_t normals_z_stride, double M,
                                       float eps, float sigmainv, double boxlen, int knum,
                                       float *interp, int64_t *face_idx, float *weights,
-                                      float *soft, int want_grad, void *ws, size_t wsb,
-                                      void *stream) {
+                                      float *soft, int want_grad, float *grad_fvi_zero,
+                                      float *grad_feat_zero, void *ws, size_t wsb, void *stream) {
   return dibr_fwd<float>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
                          normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
-                         face_idx, weights, soft, want_grad, ws, wsb, stream);
+                         face_idx, weights, soft, want_grad, grad_fvi_zero, grad_feat_zero, ws,
+                         wsb, stream);
 }
 int kd_dibr_rasterization_forward_f64(int B, int H, int W, int64_t F, int D, const double *fvz,
                                       int64_t fvz_face_stride, int64_t fvz_corner_stride,
@@ -185,22 +195,24 @@ int kd_dibr_rasterization_forward_f64(int B, int H, int W, int64_t F, int D, con
                                       const double *normals_z, int64_t normals_z_stride,
                                       double M, float eps, float sigmainv, double boxlen,
                                       int knum, double *interp, int64_t *face_idx,
-                                      double *weights, double *soft, int want_grad, void *ws,
+                                      double *weights, double *soft, int want_grad,
+                                      double *grad_fvi_zero, double *grad_feat_zero, void *ws,
                                       size_t wsb, void *stream) {
   return dibr_fwd<double>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
                           normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
-                          face_idx, weights, soft, want_grad, ws, wsb, stream);
+                          face_idx, weights, soft, want_grad, grad_fvi_zero, grad_feat_zero, ws,
+                          wsb, stream);
 }
 int kd_dibr_rasterization_backward_f32(int B, int H, int W, int64_t F, int D,
                                        const float *grad_interp, const float *grad_soft,
                                        const int64_t *face_idx, const float *weights,
                                        const float *soft, const float *fvi, const float *feat,
                                        float eps, double M, double boxlen, float sigmainv,
-                                       int knum, float *grad_fvi, float *grad_feat, void *ws,
-                                       size_t wsb, void *stream) {
+                                       int knum, float *grad_fvi, float *grad_feat,
+                                       int grads_zeroed, void *ws, size_t wsb, void *stream) {
   return dibr_bwd<float>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
-                         feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat, ws, wsb,
-                         stream);
+                         feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat, grads_zeroed,
+                         ws, wsb, stream);
 }
 int kd_dibr_rasterization_backward_f64(int B, int H, int W, int64_t F, int D,
                                        const double *grad_interp, const double *grad_soft,
@@ -208,10 +220,11 @@ int kd_dibr_rasterization_backward_f64(int B, int H, int W, int64_t F, int D,
                                        const double *soft, const double *fvi,
                                        const double *feat, float eps, double M, double boxlen,
                                        float sigmainv, int knum, double *grad_fvi,
-                                       double *grad_feat, void *ws, size_t wsb, void *stream) {
+                                       double *grad_feat, int grads_zeroed, void *ws,
+                                       size_t wsb, void *stream) {
   return dibr_bwd<double>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
-                          feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat, ws, wsb,
-                          stream);
+                          feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat,
+                          grads_zeroed, ws, wsb, stream);
 }
 
 }  // extern "C"

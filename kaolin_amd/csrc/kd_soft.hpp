@@ -108,6 +108,9 @@ struct SoftArgs {
   const T *grad_soft;
   const T *soft_in;
   T *grad_fvi;
+  // buffers the soft reduction zeroes on the side (the fused backward's gradients), nullable
+  T *zero0, *zero1;
+  int64_t nzero0, nzero1;
 };
 
 // Per-wave pair list of the current batch and its per-pixel bookkeeping.

@@ -303,6 +303,14 @@ __device__ __forceinline__ void soft_reduce_tile(const SoftArgs<T> &a, const Sof
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPairBuf<T> pb) {
   __shared__ T s_p[kReduceSlots][kBlock];
+  const int64_t nz = a.nzero0 + a.nzero1;  // side job: zero fills (grid-stride, coalesced)
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nz;
+       i += (int64_t)gridDim.x * kBlock) {
+    if (i < a.nzero0)
+      a.zero0[i] = (T)0;
+    else
+      a.zero1[i - a.nzero0] = (T)0;
+  }
   const int ntl = pb.counters[1];
   for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) soft_reduce_tile<T>(a, pb, pb.tiles[ti], s_p);
 }

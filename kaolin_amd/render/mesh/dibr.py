@@ -85,11 +85,20 @@ class DibrRasterizationHip(Function):
     def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features,
                 face_normals_z, sigmainv, boxlen, knum, multiplier, eps):
         want_grad = face_vertices_image.requires_grad or face_features.requires_grad
+        # the backward's gradient buffers, zeroed inside the forward's soft reduction
+        bufs = None
+        if want_grad:
+            bufs = (torch.empty(face_vertices_image.shape, device=face_vertices_image.device,
+                                dtype=face_vertices_image.dtype),
+                    torch.empty(face_features.shape, device=face_features.device,
+                                dtype=face_features.dtype) if face_features.requires_grad
+                    else None)
         interp, face_idx, weights, soft, ws = _C.render.mesh.dibr_rasterization_forward_fused(
             height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z,
-            sigmainv, boxlen, knum, multiplier, eps, want_grad=want_grad)
+            sigmainv, boxlen, knum, multiplier, eps, want_grad=want_grad, grad_buffers=bufs)
         ctx.save_for_backward(face_idx, weights, soft, face_vertices_image, face_features)
         ctx.workspace = ws if want_grad else None
+        ctx.grad_buffers = bufs
         ctx.params = (eps, multiplier, boxlen, sigmainv, knum)
         ctx.mark_non_differentiable(face_idx)
         ctx.set_materialize_grads(False)
@@ -104,8 +113,9 @@ class DibrRasterizationHip(Function):
         eps, multiplier, boxlen, sigmainv, knum = ctx.params
         gfvi, gfeat = _C.render.mesh.dibr_rasterization_backward_fused(
             grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier, boxlen,
-            sigmainv, knum, ctx.workspace, need_feat=need_feat)
+            sigmainv, knum, ctx.workspace, need_feat=need_feat, grad_buffers=ctx.grad_buffers)
         ctx.workspace = None
+        ctx.grad_buffers = None
         return (None, None, None, gfvi if need_fvi else None, gfeat, None, None, None, None,
                 None, None)
 
