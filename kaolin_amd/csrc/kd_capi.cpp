@@ -31,7 +31,7 @@ const char *kNames[K_NUM_KERNELS] = {
     "kd_raster_bwd_tile", "kd_soft_bwd_tile", "kd_raster_bwd_atomic", "kd_soft_bwd_atomic",
     "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs",
     "kd_prepare_fwd", "kd_prepare_bwd", "kd_tile_order", "kd_iou_partial", "kd_iou_bwd",
-    "kd_tex_fwd", "kd_tex_bwd", "kd_rast_interp", "kd_dt_chunks",
+    "kd_tex_fwd", "kd_tex_bwd", "kd_rast_interp", "kd_dt_bin",
     "kd_dt_fwd"};
 }  // namespace
 

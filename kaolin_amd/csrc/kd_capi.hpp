@@ -35,7 +35,7 @@ enum KernelId {
   K_TEX_FWD,
   K_TEX_BWD,
   K_RAST_INTERP,
-  K_DT_CHUNKS,
+  K_DT_BIN,
   K_DT_FWD,
   K_NUM_KERNELS
 };

@@ -10,17 +10,17 @@
 // 32 faces per step and scans every face of the mesh.
 //
 // Here:
-//   kd_dt_chunks  the union box of each 64-face chunk of each view (faces whose box has a NaN
-//                 never pass the box test and are left out).
-//   kd_dt_fwd     one wave per pixel.  Lane c tests chunk c's union box (a face box holding the
-//                 pixel implies the union box does), the wave walks the passing chunks in order,
-//                 lane l tests face 64 * chunk + l with the reference arithmetic, and the hits are
-//                 appended in face order (ballot + mbcnt) to the wave's LDS list.  The walk stops
-//                 at knum hits (later faces can no longer enter).  The list is then ranked by
-//                 depth, descending, ties by face order (a stable order; the reference's
-//                 torch.argsort is not stable, so tied depths are the one place it is unpinned),
-//                 and each slot writes its face index, weights (w0, w1, 1 - (w0 + w1)) and
-//                 interpolated features; empty slots get -1 / 0.
+//   kd_dt_bin     conservative per-cell face lists on a uniform grid over [-1, 1]^2 (dt_grid),
+//                 counted per workgroup in LDS and reserved with one global atomic per touched
+//                 cell; the lists are unordered.
+//   kd_dt_fwd     one wave per pixel walks its cell's list (lane = face, the reference test),
+//                 hits go to an LDS list.  The reference keeps the first knum hits by face
+//                 index: with more hits than knum the list is cut by face rank, with more than
+//                 the LDS capacity a bisection on the face index (re-walks) finds the knum-th.
+//                 The kept hits are ranked by depth, descending, ties by face index (a stable
+//                 order; the reference's torch.argsort is not stable, so tied depths are the one
+//                 place it is unpinned), and each slot writes its face index, weights
+//                 (w0, w1, 1 - (w0 + w1)) and interpolated features; empty slots get -1 / 0.
 //   backward      the rasterize backward (kd_raster.hip, the same per-sample math:
 //                 deftet_cuda.cu:238-402 == rasterization_cuda.cu:238-402) over the (pixel, slot)
 //                 samples laid out as a P x knum image.
@@ -33,167 +33,227 @@
 
 namespace kd {
 
-template <typename T>
-struct DtBox {
-  T x0, y0, x1, y1;
-};
+// Uniform grid of G x G cells over [-1, 1]^2 per view (G = 64, or 32 when the worst-case list
+// reservation of G^2 * B * F entries would pass 2^29); coordinates outside are clamped to the
+// border cells.  dt_cell is monotone in x, so a pixel inside a face's box (xmin <= x0 <= xmax)
+// lies in a cell of the face's cell range: the binning is conservative for any coordinates (NaN
+// pixels and NaN boxes never pass the box test and are skipped).
+constexpr int kDtGridMax = 64;
+
+__host__ __device__ inline int dt_grid(int64_t N) {
+  return (int64_t)64 * 64 * N <= (1ll << 29) ? 64 : 32;
+}
 
 template <typename T>
-__global__ __launch_bounds__(kWave) void kd_dt_chunks(int64_t F, int64_t nchunk, const T *fvi,
-                                                      DtBox<T> *box) {
-  const int b = blockIdx.y;
-  const int64_t c = blockIdx.x;
-  const int64_t f = c * kWave + threadIdx.x;
-  const T inf = (T)INFINITY;
-  T x0 = inf, y0 = inf, x1 = -inf, y1 = -inf;
-  if (f < F) {
-    const T *v = fvi + ((int64_t)b * F + f) * 6;
-    const T mx = nmin3(v[0], v[2], v[4]), my = nmin3(v[1], v[3], v[5]);
-    const T Mx = nmax3(v[0], v[2], v[4]), My = nmax3(v[1], v[3], v[5]);
-    if (!(isnan(mx) || isnan(my) || isnan(Mx) || isnan(My))) {
-      x0 = mx;
-      y0 = my;
-      x1 = Mx;
-      y1 = My;
+__device__ __forceinline__ int dt_cell(T x, int G) {
+  T t = (x + (T)1) * (T)(G / 2);
+  t = fmin(fmax(t, (T)0), (T)(G - 1));  // NaN -> 0
+  return (int)t;                        // floor for t >= 0
+}
+
+template <typename T>
+__device__ __forceinline__ bool dt_box(const T *v, T &xmin, T &ymin, T &xmax, T &ymax) {
+  xmin = nmin3(v[0], v[2], v[4]);
+  xmax = nmax3(v[0], v[2], v[4]);
+  ymin = nmin3(v[1], v[3], v[5]);
+  ymax = nmax3(v[1], v[3], v[5]);
+  return !(isnan(xmin) || isnan(xmax) || isnan(ymin) || isnan(ymax));
+}
+
+// (view, face) -> every cell its box touches: unordered lists, cell c of view b at
+// lists[c * N + b * F] with room for all F faces of the view; cursor[b][c] = list length.
+// Neighbouring faces share cells, so a workgroup counts its 256 faces per cell in LDS, reserves
+// one range per touched cell with a single global atomic, and places its faces in it.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_dt_bin(int64_t F, int64_t N, int G, const T *fvi,
+                                                    int *cursor, int *lists) {
+  __shared__ int s_cnt[kDtGridMax * kDtGridMax];
+  const int b = blockIdx.y, cells = G * G;
+  const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  for (int i = threadIdx.x; i < cells; i += kBlock) s_cnt[i] = 0;
+  __syncthreads();
+  T xmin, ymin, xmax, ymax;
+  int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
+  if (f < F && dt_box<T>(fvi + ((int64_t)b * F + f) * 6, xmin, ymin, xmax, ymax)) {
+    cx0 = dt_cell(xmin, G);
+    cx1 = dt_cell(xmax, G);
+    cy0 = dt_cell(ymin, G);
+    cy1 = dt_cell(ymax, G);
+  }
+  for (int cy = cy0; cy <= cy1; ++cy)
+    for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&s_cnt[cy * G + cx], 1);
+  __syncthreads();
+  int *cur = cursor + (int64_t)b * cells;
+  for (int i = threadIdx.x; i < cells; i += kBlock) {
+    const int n = s_cnt[i];
+    s_cnt[i] = n ? atomicAdd(&cur[i], n) : 0;  // this workgroup's range start in cell i
+  }
+  __syncthreads();
+  for (int cy = cy0; cy <= cy1; ++cy)
+    for (int cx = cx0; cx <= cx1; ++cx) {
+      const int c = cy * G + cx;
+      const int pos = atomicAdd(&s_cnt[c], 1);
+      lists[(int64_t)c * N + (int64_t)b * F + pos] = (int)f;
     }
-  }
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) {
-    x0 = fmin(x0, __shfl_xor(x0, s));
-    y0 = fmin(y0, __shfl_xor(y0, s));
-    x1 = fmax(x1, __shfl_xor(x1, s));
-    y1 = fmax(y1, __shfl_xor(y1, s));
-  }
-  if (threadIdx.x == 0) box[(int64_t)b * nchunk + c] = DtBox<T>{x0, y0, x1, y1};
+}
+
+// The reference's per-face test (deftet_cuda.cu:114-160): half-open box of the corner min / max,
+// eps-normalised barycentrics (copysignf of the float eps, also for fp64 data), all >= 0, depth
+// in [min, max).
+template <typename T>
+__device__ __forceinline__ bool dt_face_test(const T *v, const T *z, T x0, T y0, T dmin, T dmax,
+                                             T eps, T &w0, T &w1, T &depth) {
+  const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
+  const T xmin = nmin3(ax, bx, cx), xmax = nmax3(ax, bx, cx);
+  const T ymin = nmin3(ay, by, cy), ymax = nmax3(ay, by, cy);
+  if (!(x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax)) return false;
+  const T aex = ax - x0, aey = ay - y0, bex = bx - x0, bey = by - y0;
+  const T cex = cx - x0, cey = cy - y0;
+  const T _w0 = bex * cey - bey * cex;
+  const T _w1 = cex * aey - cey * aex;
+  const T _w2 = aex * bey - aey * bex;
+  const T norm = _w0 + _w1 + _w2;
+  const T ne = (T)copysignf((float)eps, (float)norm);
+  w0 = _w0 / (norm + ne);
+  w1 = _w1 / (norm + ne);
+  const T w2 = _w2 / (norm + ne);
+  if (!(w0 >= (T)0 && w1 >= (T)0 && w2 >= (T)0)) return false;
+  depth = w0 * z[0] + w1 * z[1] + w2 * z[2];  // :156
+  return depth < dmax && depth >= dmin;       // :158
 }
 
 template <typename T>
 struct DtArgs {
   int B;
-  int64_t P, F, nchunk;
-  int K, D;
+  int64_t P, F, N;
+  int K, D, C;  // C: LDS hit-list capacity per pixel (>= K)
+  int G;        // grid cells per side
   float eps;
   const T *px;      // (B, P, 2)
   const T *range;   // (B, P, 2): min, max depth
   const T *fvz;     // (B, F, 3)
   const T *fvi;     // (B, F, 3, 2)
   const T *feat;    // (B, F, 3, D)
-  const DtBox<T> *box;
-  T *interp;        // (B, P, K, D)
+  const int *cursor, *lists;
+  T *interp;          // (B, P, K, D)
   int64_t *face_idx;  // (B, P, K)
-  T *weights;       // (B, P, K, 3)
+  T *weights;         // (B, P, K, 3)
 };
 
 constexpr int kDtWaves = 4;  // pixels per workgroup
 
-// per-wave LDS list of (depth, face, w0, w1), knum entries
 template <typename T>
-__device__ __forceinline__ void dt_carve(char *base, int K, T *&dep, T *&w0, T *&w1, int *&fid) {
-  dep = (T *)base;
-  w0 = dep + K;
-  w1 = w0 + K;
-  fid = (int *)(w1 + K);
+__host__ __device__ inline size_t dt_wave_lds(int C) {  // depth, w0, w1, face, face rank
+  return (size_t)C * (3 * sizeof(T) + 2 * sizeof(int));
 }
 
-template <typename T>
-__host__ __device__ inline size_t dt_wave_lds(int K) {
-  return (size_t)K * (3 * sizeof(T) + sizeof(int));
-}
-
+// One wave per pixel.  The pixel's cell list is walked 64 faces at a time (lane = face, the
+// reference test), hits go to the wave's LDS list.  The reference keeps the first knum hits by
+// face index: with more hits than knum the list is cut by face rank; with more than the LDS
+// capacity a binary search on the face index (re-walks counting hits below a threshold) finds
+// the knum-th smallest and only hits below it are collected.  The kept hits are then ranked by
+// depth, descending, ties by face index, and each slot writes face index, weights
+// (w0, w1, 1 - (w0 + w1)) and interpolated features; empty slots get -1 / 0.
 template <typename T>
 __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
   extern __shared__ __align__(16) char dt_lds[];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int K = a.K;
-  T *dep, *lw0, *lw1;
-  int *fid;
-  dt_carve<T>(dt_lds + (size_t)w * dt_wave_lds<T>(K), K, dep, lw0, lw1, fid);
+  const int K = a.K, C = a.C;
+  T *dep = (T *)(dt_lds + (size_t)w * dt_wave_lds<T>(C));
+  T *lw0 = dep + C, *lw1 = lw0 + C;
+  int *fid = (int *)(lw1 + C);
   const int b = blockIdx.y;
   const int64_t p = (int64_t)blockIdx.x * kDtWaves + w;
   if (p >= a.P) return;  // whole wave
   const int64_t pp = (int64_t)b * a.P + p;
   const T x0 = a.px[2 * pp], y0 = a.px[2 * pp + 1];
   const T dmin = a.range[2 * pp], dmax = a.range[2 * pp + 1];
-  const DtBox<T> *box = a.box + (int64_t)b * a.nchunk;
   const T *fvi = a.fvi + (int64_t)b * a.F * 6;
   const T *fvz = a.fvz + (int64_t)b * a.F * 3;
   const T eps = (T)a.eps;
-  int num = 0;
-  for (int64_t g0 = 0; g0 < a.nchunk && num < K; g0 += kWave) {
-    bool in = false;
-    if (g0 + lane < a.nchunk) {
-      const DtBox<T> u = box[g0 + lane];
-      in = x0 >= u.x0 && x0 < u.x1 && y0 >= u.y0 && y0 < u.y1;
-    }
-    for (uint64_t cm = __ballot(in); cm && num < K; cm &= cm - 1ull) {
-      const int64_t f = (g0 + __builtin_ctzll(cm)) * kWave + lane;
+  const int G = a.G;
+  const int c = dt_cell(y0, G) * G + dt_cell(x0, G);
+  const int nl = a.cursor[(int64_t)b * G * G + c];
+  const int *list = a.lists + (int64_t)c * a.N + (int64_t)b * a.F;
+  // walk: hits with face < limit are appended (limit = F: all)
+  auto walk = [&](int limit, bool store) {
+    int num = 0;
+    for (int j0 = 0; j0 < nl; j0 += kWave) {
+      const int j = j0 + lane;
       bool hit = false;
       T w0 = 0, w1 = 0, depth = 0;
-      if (f < a.F) {
-        const T *v = fvi + f * 6;
-        const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
-        // deftet_cuda.cu:114-126: half-open box of min / max corners
-        const T xmin = nmin3(ax, bx, cx), xmax = nmax3(ax, bx, cx);
-        const T ymin = nmin3(ay, by, cy), ymax = nmax3(ay, by, cy);
-        if (x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax) {
-          // :128-147, same operation order
-          const T aex = ax - x0, aey = ay - y0, bex = bx - x0, bey = by - y0;
-          const T cex = cx - x0, cey = cy - y0;
-          const T _w0 = bex * cey - bey * cex;
-          const T _w1 = cex * aey - cey * aex;
-          const T _w2 = aex * bey - aey * bex;
-          const T norm = _w0 + _w1 + _w2;
-          const T ne = (T)copysignf((float)eps, (float)norm);
-          w0 = _w0 / (norm + ne);
-          w1 = _w1 / (norm + ne);
-          const T w2 = _w2 / (norm + ne);
-          if (w0 >= (T)0 && w1 >= (T)0 && w2 >= (T)0) {
-            const T *z = fvz + f * 3;
-            depth = w0 * z[0] + w1 * z[1] + w2 * z[2];  // :156
-            hit = depth < dmax && depth >= dmin;        // :158
-          }
-        }
+      int f = 0;
+      if (j < nl) {
+        f = list[j];
+        if (f < limit) hit = dt_face_test<T>(fvi + (int64_t)f * 6, fvz + (int64_t)f * 3, x0, y0,
+                                             dmin, dmax, eps, w0, w1, depth);
       }
       const uint64_t hm = __ballot(hit);
-      if (hit) {
+      if (store && hit) {
         const int at = num + (int)__builtin_amdgcn_mbcnt_hi(
-                                 (uint32_t)(hm >> 32),
-                                 __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-        if (at < K) {
+                                 (uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
+        if (at < C) {
           dep[at] = depth;
           lw0[at] = w0;
           lw1[at] = w1;
-          fid[at] = (int)f;
+          fid[at] = f;
         }
       }
       num += __popcll(hm);
     }
+    return num;
+  };
+  int nh = walk(INT_MAX, true);
+  if (nh > C) {  // more hits than the list holds: the knum smallest face indices, by bisection
+    int lo = 0, hi = (int)a.F;  // count(face < hi) >= K
+    while (lo < hi) {
+      const int mid = lo + (hi - lo) / 2;
+      if (walk(mid + 1, false) >= K)
+        hi = mid;
+      else
+        lo = mid + 1;
+    }
+    wave_lds_sync();
+    nh = walk(lo + 1, true);  // exactly K hits: faces <= the K-th smallest
   }
-  const int n = num < K ? num : K;
   wave_lds_sync();
-  // rank: depth descending, then list (= face) order
+  // the reference keeps the first K hits by face index: mark the others (face rank >= K)
+  int *frank = fid + C;
+  const bool cut = nh > K;
+  for (int i = lane; i < nh; i += kWave) {
+    int r = 0;
+    if (cut) {
+      const int fi = fid[i];
+      for (int j = 0; j < nh; ++j) r += fid[j] < fi ? 1 : 0;
+    }
+    frank[i] = r;
+  }
+  wave_lds_sync();
+  // rank the kept hits: depth descending, then face index (deftet.py:300-303, stable order)
+  const int n = cut ? K : nh;
   const int D = a.D;
   const int64_t row = pp * K;
   const T *feat = a.feat + (int64_t)b * a.F * 3 * D;
-  for (int i = lane; i < n; i += kWave) {
+  for (int i = lane; i < nh; i += kWave) {
+    if (frank[i] >= K) continue;
     const T di = dep[i];
+    const int fi = fid[i];
     int r = 0;
-    for (int j = 0; j < n; ++j) {
+    for (int j = 0; j < nh; ++j) {
       const T dj = dep[j];
-      r += (dj > di || (dj == di && j < i)) ? 1 : 0;
+      r += (frank[j] < K && (dj > di || (dj == di && fid[j] < fi))) ? 1 : 0;
     }
     const T w0 = lw0[i], w1 = lw1[i];
     const T w2 = (T)1 - (w0 + w1);  // deftet.py:304
-    const int f = fid[i];
     const int64_t o = row + r;
-    a.face_idx[o] = f;
+    a.face_idx[o] = fi;
     a.weights[3 * o] = w0;
     a.weights[3 * o + 1] = w1;
     a.weights[3 * o + 2] = w2;
-    const T *c = feat + (int64_t)f * 3 * D;
+    const T *cf = feat + (int64_t)fi * 3 * D;
     T *out = a.interp + o * D;
     for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
-      out[d] = w0 * c[d] + w1 * c[D + d] + w2 * c[2 * D + d];
+      out[d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
   }
   for (int s = n + lane; s < K; s += kWave) {
     const int64_t o = row + s;
@@ -205,10 +265,14 @@ __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
   }
 }
 
-template <typename T>
 static size_t dt_workspace(int B, int64_t F) {
-  return sizeof(DtBox<T>) * (size_t)B * (size_t)((F + kWave - 1) / kWave);
+  const int64_t N = (int64_t)B * F;
+  const int64_t cells = (int64_t)dt_grid(N) * dt_grid(N);
+  return align_up(sizeof(int) * (size_t)B * cells) +
+         align_up(sizeof(int) * (size_t)cells * (size_t)(N > 0 ? N : 1));
 }
+
+static int dt_capacity(int K) { return K < 256 ? 256 : K; }
 
 template <typename T>
 static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, const T *range,
@@ -216,34 +280,39 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
                       int64_t *face_idx, T *weights, void *ws, size_t wsb, hipStream_t stream) {
   KD_CHECK_ARG(B >= 0 && B <= 65535 && P >= 0 && F >= 0 && D >= 0, "deftet: bad sizes");
   KD_CHECK_ARG(K >= 1, "deftet: knum must be >= 1");
-  KD_CHECK_ARG(F < (1ll << 31), "deftet: too many faces");
-  const size_t lds = dt_wave_lds<T>(K) * kDtWaves;
-  KD_CHECK_ARG(lds <= 160 * 1024, "deftet: knum too large for the LDS list (fp32 <= 2560, "
-                                  "fp64 <= 1462)");
-  const size_t need = dt_workspace<T>(B, F);
+  KD_CHECK_ARG(F < (1ll << 31) && (int64_t)B * F < (1ll << 40), "deftet: too many faces");
+  const int C = dt_capacity(K);
+  const size_t lds = dt_wave_lds<T>(C) * kDtWaves;
+  KD_CHECK_ARG(lds <= 160 * 1024, "deftet: knum too large for the LDS list (fp32 <= 2048, "
+                                  "fp64 <= 1280)");
+  const size_t need = dt_workspace(B, F);
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   if (B == 0 || P == 0) return KD_OK;
-  const int64_t nchunk = (F + kWave - 1) / kWave;
-  DtBox<T> *box = (DtBox<T> *)ws;
-  if (nchunk > 0) {
-    ProfScope prof(K_DT_CHUNKS, stream);
-    hipLaunchKernelGGL(kd_dt_chunks<T>, dim3((unsigned)nchunk, B), dim3(kWave), 0, stream, F,
-                       nchunk, fvi, box);
+  const int64_t N = (int64_t)B * F;
+  const int G = dt_grid(N);
+  int *cursor = (int *)ws;
+  int *lists = (int *)((char *)ws + align_up(sizeof(int) * (size_t)B * G * G));
+  hipError_t e = hipMemsetAsync(cursor, 0, sizeof(int) * (size_t)B * G * G, stream);
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "deftet: %s", hipGetErrorString(e));
+  if (F > 0) {
+    ProfScope prof(K_DT_BIN, stream);
+    hipLaunchKernelGGL(kd_dt_bin<T>, dim3((unsigned)((F + kBlock - 1) / kBlock), B),
+                       dim3(kBlock), 0, stream, F, N, G, fvi, cursor, lists);
   }
-  DtArgs<T> a{B, P, F, nchunk, K, D, eps, px, range, fvz, fvi, feat, box, interp, face_idx,
-              weights};
+  DtArgs<T> a{B, P, F, N, K, D, C, G, eps, px, range, fvz, fvi, feat, cursor, lists, interp,
+              face_idx, weights};
   const int64_t gx = (P + kDtWaves - 1) / kDtWaves;
   KD_CHECK_ARG(gx < (1ll << 31), "deftet: too many pixels");
   {
     ProfScope prof(K_DT_FWD, stream);
     if (lds > 64 * 1024)
       (void)hipFuncSetAttribute((const void *)kd_dt_fwd<T>,
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL(kd_dt_fwd<T>, dim3((unsigned)gx, B), dim3(kWave * kDtWaves), lds, stream,
                        a);
   }
-  const hipError_t e = hipGetLastError();
+  e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "deftet fwd: %s", hipGetErrorString(e));
   return KD_OK;
 }
@@ -271,7 +340,8 @@ extern "C" {
 
 size_t kd_deftet_workspace_size(int B, int64_t F, int double_precision) {
   if (B < 0 || F < 0) return 0;
-  return double_precision ? dt_workspace<double>(B, F) : dt_workspace<float>(B, F);
+  (void)double_precision;
+  return dt_workspace(B, F);
 }
 
 int kd_deftet_sparse_render_forward_f32(int B, int64_t P, int64_t F, int knum, int D,
