@@ -478,7 +478,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   {
     ProfScope prof(K_SOFT_MATH, stream);
-    const dim3 grid((a.fs.dbg & 2048) ? 512 : (a.fs.dbg & 4096) ? 8192 : kPersistentBlocks);
+    const dim3 grid((a.fs.dbg & 2048) ? 512 : (a.fs.dbg & 4096) ? kPersistentBlocks : 8192);
     const bool lists = a.prob != nullptr;
     if (grad && lists)
       hipLaunchKernelGGL((kd_soft_pair_math<T, true, true>), grid, dim3(kBlock), 0, stream, a, pb);
@@ -492,8 +492,8 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
-    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a,
-                       pb);
+    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3((a.fs.dbg & 2048) ? kPersistentBlocks : 8192),
+                       dim3(kBlock), 0, stream, a, pb);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
