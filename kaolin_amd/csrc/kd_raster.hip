@@ -169,14 +169,14 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
 //   meets a NaN depth replays the reference's sequential loop over its coarse bin instead.
 //   The winner's weights are recomputed with the identical expression for the outputs.
 // ------------------------------------------------------------------------------------------
-constexpr int kRasterPairCap = 512;
+constexpr int kRasterPairCap = 256;
 
 __device__ __forceinline__ uint32_t ordered_f32(float z) {
   const uint32_t u = __float_as_uint(z + 0.0f);  // -0 -> +0
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-__global__ __launch_bounds__(kBlock) void kd_raster_fwd_pairs(RasterFwdArgs<float> a) {
+__global__ __launch_bounds__(kBlock, 6) void kd_raster_fwd_pairs(RasterFwdArgs<float> a) {
   TileClock clk(a.fs.tbuf, 0);
   __shared__ TileLists L;
   __shared__ float s_geo[9][kCap];   // ax ay bx by cx cy (scaled), az bz cz

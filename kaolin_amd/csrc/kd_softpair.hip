@@ -160,7 +160,7 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
+__global__ __launch_bounds__(kBlock, 8) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
   TileClock clk(a.fs.tbuf, 1);
   __shared__ TileLists L;
   __shared__ uint64_t s_pm[4][kWave];
