@@ -287,10 +287,21 @@ __device__ __forceinline__ void soft_reduce_tile(const SoftArgs<T> &a, const Sof
   T prod = (T)1.0;
   for (int s0 = 0; s0 < K; s0 += kReduceSlots) {
     __syncthreads();  // the previous pass is done with s_p
-    for (int i = tid; i < n; i += kBlock) {
-      const uint32_t sq = __builtin_nontemporal_load((const uint32_t *)(rec + i) + 2);
-      const int s = (int)(sq & 0xffffu) - s0;  // slot | q << 16 | type << 24
-      if (s >= 0 && s < kReduceSlots) s_p[s][(sq >> 16) & 0xffu] = pr[i];
+    constexpr int U = 4;  // record loads in flight per thread
+    for (int i0 = tid; i0 < n; i0 += U * kBlock) {
+      uint32_t sq[U];
+      T pv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * kBlock;
+        sq[u] = i < n ? __builtin_nontemporal_load((const uint32_t *)(rec + i) + 2) : 0xffffu;
+        pv[u] = i < n ? pr[i] : (T)0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int s = (int)(sq[u] & 0xffffu) - s0;  // slot | q << 16 | type << 24
+        if (s >= 0 && s < kReduceSlots) s_p[s][(sq[u] >> 16) & 0xffu] = pv[u];
+      }
     }
     __syncthreads();
     const int e = min(np - s0, kReduceSlots);
