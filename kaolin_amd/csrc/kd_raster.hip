@@ -496,7 +496,12 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   int h = -1;
   if (px < W && py < H) {
     const int64_t p = ((int64_t)b * H + py) * W + px;
+    // the pixel's weights and incoming gradient do not depend on its face: issued with it
     const int64_t f = face_idx[p];
+    const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
+    T gd[DMAX];
+#pragma unroll
+    for (int d = 0; d < DMAX; ++d) gd[d] = d < D ? grad[p * D + d] : (T)0;
     if (f >= 0 && f < F) {
       unsigned u = ((unsigned)f * 2654435761u) >> 24;
       for (;;) {  // <= 256 keys in 256 slots: terminates
@@ -507,9 +512,8 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
       h = (int)u;
       atomicOr(&s_mask[h][tid >> 5], 1u << (tid & 31));
       const int64_t tf = (int64_t)b * F + f;
-      const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
       T c[SMAX];
-      raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, grad + p * D, feat + tf * 3 * D, D, eps, c);
+      raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, gd, feat + tf * 3 * D, D, eps, c);
 #pragma unroll
       for (int j = 0; j < 6; ++j) s_con[tid][j] = c[j];
 #pragma unroll
