@@ -5,7 +5,7 @@ import subprocess
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'kaolin_amd',
                     'csrc')
-for f in ('kd_binning', 'kd_raster', 'kd_softmask', 'kd_softpair'):
+for f in sorted(x[:-4] for x in os.listdir(CSRC) if x.endswith('.hip')):
     out = subprocess.run(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off',
                           '--offload-arch=gfx950', '-c', f'{f}.hip', '-o', '/tmp/kd_ru.o',
                           '-Rpass-analysis=kernel-resource-usage'], cwd=CSRC,
@@ -22,7 +22,7 @@ for f in ('kd_binning', 'kd_raster', 'kd_softmask', 'kd_softpair'):
             m = re.search(pat, line)
             if m and cur is not None:
                 cur[key] = m.group(1)
-        if cur and 'occ' in cur:
+        if cur and 'lds' in cur:  # the last field of a kernel's remark block
             print(f"{cur['name'][:64]:64s} vgpr={cur.get('vgpr')} scratch={cur.get('scratch')} "
                   f"lds={cur.get('lds')} occ={cur.get('occ')}")
             cur = None
