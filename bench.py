@@ -30,12 +30,17 @@ from kaolin_amd.render.mesh import dibr, dibr_rasterization, prepare_vertices  #
 METRIC = 'Mpixels/s DIB-R fwd+bwd, 50k-face mesh @512² bs=8, 1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
-# name -> (n_lon, n_lat, H, W, views per GPU, elevation)
+# name -> (n_lon, n_lat, H, W, views per GPU, elevation); SURVEY.md §8(d) configs C2-C5
 CONFIGS = {
     'c2': (100, 51, 256, 256, 4, 0.3),
     'c3': (250, 101, 512, 512, 8, 0.3),
     'c4': (250, 101, 1024, 1024, 8, 0.3),
     'c5': (500, 201, 512, 512, 16, 0.6),
+}
+# name -> (faces, H, W, views per GPU): the C5 stress soup (workloads.soup, seed 3); a step is
+# dibr_rasterization fwd + bwd on per-view face soups (no shared mesh: no all-reduce)
+SOUP_CONFIGS = {
+    'c5soup': (200000, 512, 512, 16),
 }
 
 
@@ -86,7 +91,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
-    ap.add_argument('--config', default='c3', choices=sorted(CONFIGS))
+    ap.add_argument('--config', default='c3', choices=sorted(CONFIGS) + sorted(SOUP_CONFIGS))
     ap.add_argument('--views-per-gpu', type=int, default=None)
     ap.add_argument('--knum', type=int, default=30)
     ap.add_argument('--sigmainv', type=float, default=7000.)
@@ -111,34 +116,59 @@ def main():
     _lib.load()
     dibr.SAVE_CLOSE_LISTS = args.lists
 
-    n_lon, n_lat, H, W, B_def, elev = CONFIGS[args.config]
-    Bl = args.views_per_gpu or B_def
-    first, _ = distributed.shard_views(Bl * world, rank, world)
-    verts, faces, face_uvs = workloads.uv_sphere(n_lon, n_lat, seed=0)
-    F = faces.shape[0]
-    vertices = verts.to(dev).requires_grad_(True)
-    faces = faces.to(dev)
-    cam = workloads.orbit_cameras(Bl, elev, first_view=first, total_views=Bl * world).to(dev)
-    proj = workloads.generate_perspective_projection(math.pi / 4).to(dev)
-    uvs = face_uvs.to(dev).unsqueeze(0).repeat(Bl, 1, 1, 1)
-    feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
-    feats.requires_grad_(True)  # learnable per-face-vertex features: grad_feat is computed too
+    soup = args.config in SOUP_CONFIGS
+    kw = dict(sigmainv=args.sigmainv, boxlen=args.boxlen, knum=args.knum)
+    if soup:
+        F, H, W, B_def = SOUP_CONFIGS[args.config]
+        Bl = args.views_per_gpu or B_def
+        first, _ = distributed.shard_views(Bl * world, rank, world)
+        sz, si, sn = workloads.soup(F, seed=3, batch=Bl * world)
+        sfvz = sz[first:first + Bl].to(dev).contiguous()
+        sfvi = si[first:first + Bl].to(dev).contiguous().requires_grad_(True)
+        snz = sn[first:first + Bl].to(dev).contiguous()
+        g = torch.Generator().manual_seed(4)
+        uvs = torch.rand((Bl, F, 3, 2), generator=g).to(dev)
+        feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
+        feats.requires_grad_(True)
+        n_lon = n_lat = None
+        verts = None
+    else:
+        n_lon, n_lat, H, W, B_def, elev = CONFIGS[args.config]
+        Bl = args.views_per_gpu or B_def
+        first, _ = distributed.shard_views(Bl * world, rank, world)
+        verts, faces, face_uvs = workloads.uv_sphere(n_lon, n_lat, seed=0)
+        F = faces.shape[0]
+        vertices = verts.to(dev).requires_grad_(True)
+        faces = faces.to(dev)
+        cam = workloads.orbit_cameras(Bl, elev, first_view=first,
+                                      total_views=Bl * world).to(dev)
+        proj = workloads.generate_perspective_projection(math.pi / 4).to(dev)
+        uvs = face_uvs.to(dev).unsqueeze(0).repeat(Bl, 1, 1, 1)
+        feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
+        feats.requires_grad_(True)  # learnable per-face-vertex features: grad_feat is computed
     D = feats.shape[-1]
     g = torch.Generator().manual_seed(1)
     g_feat = torch.rand((Bl, H, W, D), generator=g).to(dev)
     g = torch.Generator().manual_seed(2)
     g_soft = torch.rand((Bl, H, W), generator=g).to(dev)
-    kw = dict(sigmainv=args.sigmainv, boxlen=args.boxlen, knum=args.knum)
 
-    def step():
+    def inputs():
+        if soup:
+            return sfvz, sfvi, snz
         # one mesh, Bl cameras: vertices batch 1 broadcast over the views (utils.py:128-175)
         fvc, fvi, nrm = prepare_vertices(vertices.unsqueeze(0), faces, proj,
                                          camera_transform=cam)
-        interp, soft, face_idx = dibr_rasterization(H, W, fvc[..., 2], fvi, feats, nrm[..., 2],
-                                                    **kw)
+        return fvc[..., 2], fvi, nrm[..., 2]
+
+    def step():
+        fvz, fvi, nz = inputs()
+        interp, soft, face_idx = dibr_rasterization(H, W, fvz, fvi, feats, nz, **kw)
         torch.autograd.backward([interp, soft], [g_feat, g_soft])
-        distributed.allreduce_grads_([vertices.grad])
-        vertices.grad = None
+        if soup:
+            sfvi.grad = None
+        else:
+            distributed.allreduce_grads_([vertices.grad])
+            vertices.grad = None
         feats.grad = None
         return face_idx
 
@@ -178,17 +208,17 @@ def main():
     fv = int((face_idx >= 0).sum().item())  # covered pixels (for the record)
 
     with torch.no_grad():
-        fvc, fvi, nrm = prepare_vertices(vertices.unsqueeze(0), faces, proj,
-                                         camera_transform=cam)
-        Fv = int((nrm[..., 2] >= 0).sum().item())
+        fvz, fvi, nz = inputs()
+        fvi = fvi.detach()
+        Fv = int((nz >= 0).sum().item())
     P = Bl * H * W
     Ftot = Bl * F
-    V = vertices.shape[0]
+    V = 0 if soup else vertices.shape[0]
     pairs = None
     if not args.lists:
         with torch.no_grad():
             _, _, _, _, ws = _C.render.mesh.dibr_rasterization_forward_fused(
-                H, W, fvc[..., 2], fvi, feats, nrm[..., 2], args.sigmainv, args.boxlen,
+                H, W, fvz, fvi, feats, nz, args.sigmainv, args.boxlen,
                 args.knum, 1000., 1e-8, want_grad=True)
             pairs = int(_lib.load().kd_dibr_pair_count(ws.data_ptr(), Bl, H, W, F, args.knum, 0,
                                                        torch.cuda.current_stream(dev).cuda_stream))
@@ -237,20 +267,23 @@ def main():
     # ---- CPU baseline: the oracle (C port of the reference kernels), rank 0, N == 1 -------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, fvc, fvi, nrm, feats, g_feat, g_soft, H, W, kw)
+        cpu = cpu_baseline(args, fvz, fvi, nz, feats, g_feat, g_soft, H, W, kw)
 
     out = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
         'data': 'synthetic (seeded uv-sphere, orbit cameras; no dataset)',
-        'config': {'workload': f'{args.config.upper()}: uv_sphere({n_lon},{n_lat}) {F} faces, '
+        'config': {'workload': f'{args.config.upper()}: ' +
+                               (f'soup({F}, seed=3) per view' if soup else
+                                f'uv_sphere({n_lon},{n_lat}) {F} faces') + ', '
                                f'{H}x{W}, {Bl} views/GPU, D={D}, knum={args.knum}, '
                                f'sigmainv={args.sigmainv:g}, boxlen={args.boxlen:g}',
                    'faces': F, 'height': H, 'width': W, 'views_per_gpu': Bl,
                    'global_batch': Bl * world,
                    'parallelism': f'view-sharded x{world}' +
-                                  (' + RCCL vertex-grad all-reduce' if world > 1 else ''),
+                                  (' + RCCL vertex-grad all-reduce'
+                                   if world > 1 and not soup else ''),
                    'close_lists': 'materialised' if args.lists else 'not materialised',
                    'covered_px_per_step': fv, 'front_faces': Fv},
         'roofline': roofline,
@@ -265,7 +298,7 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, fvc, fvi, nrm, feats, g_feat, g_soft, H, W, kw):
+def cpu_baseline(args, fvz, fvi, nz, feats, g_feat, g_soft, H, W, kw):
     """The CPU oracle (oracle/dibr_oracle.c, OpenMP) doing the same fwd+bwd on a bounded sample
     (the first `--cpu-sample-views` views of the workload)."""
     import numpy as np
@@ -274,7 +307,7 @@ def cpu_baseline(args, fvc, fvi, nrm, feats, g_feat, g_soft, H, W, kw):
     oracle.set_num_threads(threads)
     nb = max(1, min(args.cpu_sample_views, fvi.shape[0]))
     n = lambda t: t[:nb].detach().cpu().numpy()  # noqa: E731
-    fvz_, fvi_, nz_, ft_ = n(fvc[..., 2]), n(fvi), n(nrm[..., 2]), n(feats)
+    fvz_, fvi_, nz_, ft_ = n(fvz), n(fvi), n(nz), n(feats)
     gf_, gs_ = n(g_feat), n(g_soft)
     reps = 0
     t0 = time.perf_counter()

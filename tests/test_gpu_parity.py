@@ -314,6 +314,97 @@ def test_uv_sphere_rows_vs_oracle(cfg):
         np.testing.assert_allclose(N(soft)[:, r], osoft[:, r], rtol=1e-6, atol=1e-7)
 
 
+def test_c3_view_full_fwd_bwd_vs_oracle():
+    """One whole C3 view (50k-face uv-sphere, 512x512, knum 30): every output and both
+    gradients of the fused dibr_rasterization against the oracle's brute-force loops."""
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import dibr_rasterization
+    h = w = 512
+    v = workloads.sphere_views(250, 101, h, w, 1, DEV, first_view=3, total_views=8)
+    fvz, feats, nz = v['fvz'], v['feats'].contiguous(), v['normals_z']
+    fvi = v['fvi'].detach().clone().requires_grad_(True)
+    feats.requires_grad_(True)
+    interp, soft, face_idx = dibr_rasterization(h, w, fvz, fvi, feats, nz)
+    g = torch.Generator().manual_seed(1)
+    g_feat = torch.rand(interp.shape, generator=g).to(DEV)
+    g_soft = torch.rand(soft.shape, generator=g).to(DEV)
+    torch.autograd.backward([interp, soft], [g_feat, g_soft])
+    valid = N(nz) >= 0
+    ri, rf, rw = oracle.rasterize(h, w, N(fvz), N(fvi), N(feats), valid)
+    np.testing.assert_array_equal(N(face_idx), rf)
+    np.testing.assert_array_equal(N(interp), ri)
+    osoft, oprob, ocidx, octype, sfvi = oracle.soft_mask_forward(N(fvi), rf)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+    gr, gfeat = oracle.rasterize_backward(N(g_feat), rf, rw, N(fvi), N(feats), 1e-8)
+    gs = oracle.soft_mask_backward(N(g_soft), osoft, rf, oprob, ocidx, octype, sfvi, 7000, 1000.)
+    np.testing.assert_allclose(N(fvi.grad), gr + gs, rtol=1e-4, atol=1e-5 * np.abs(gr + gs).max())
+    np.testing.assert_allclose(N(feats.grad), gfeat, rtol=1e-4, atol=1e-5 * np.abs(gfeat).max())
+
+
+@pytest.mark.parametrize('sweep', [(3000., 0.05), (7000., 0.02), (17000., 0.02), (30000., 0.01)])
+def test_c4_rows_sigma_sweep(sweep):
+    """C4 shapes (50k faces at 1024x1024) across SURVEY §8(d)'s (sigmainv, boxlen) sweep: rows
+    through the silhouette band bit-exact / 1e-6 vs the oracle; the fused path equals the
+    reference composition with materialised close-face lists (op-form kernels) everywhere."""
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import dibr_rasterization, dibr_soft_mask
+    sig, box = sweep
+    h = w = 1024
+    v = workloads.sphere_views(250, 101, h, w, 1, DEV, first_view=1, total_views=8)
+    fvz, fvi, feats, nz = v['fvz'], v['fvi'], v['feats'], v['normals_z']
+    interp, soft, face_idx = dibr_rasterization(h, w, fvz, fvi, feats, nz, sig, box)
+    soft_op = dibr_soft_mask(fvi, face_idx, sig, box)
+    assert torch.equal(soft, soft_op)
+    valid = N(nz) >= 0
+    for r in (int(h * 0.1), int(h * 0.12), h // 2, int(h * 0.88)):
+        ri, rf, _ = oracle.rasterize(h, w, N(fvz), N(fvi), N(feats), valid, rows=(r, r + 1))
+        np.testing.assert_array_equal(N(face_idx)[:, r], rf[:, r])
+        np.testing.assert_array_equal(N(interp)[:, r], ri[:, r])
+        osoft, _, _, _, _ = oracle.soft_mask_forward(N(fvi), N(face_idx), sig, box,
+                                                     rows=(r, r + 1))
+        np.testing.assert_allclose(N(soft)[:, r], osoft[:, r], rtol=1e-6, atol=1e-7)
+
+
+def test_c5_soup_rows_and_grad_consistency():
+    """C5 stress soup (200k clustered faces, 512x512): dense central tiles far past the LDS list
+    capacity.  Rows vs the oracle; gradients of the fused pair pipeline vs the op-form
+    (materialised K-lists, atomic) kernels on the whole image."""
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import dibr, dibr_rasterization
+    h = w = 512
+    sz, si, sn = workloads.soup(200000, seed=3, batch=1)
+    fvz, fvi0, nz = T(sz), T(si), T(sn)
+    gen = torch.Generator().manual_seed(4)
+    feats = torch.rand((1, 200000, 3, 3), generator=gen).to(DEV)
+    g = torch.Generator().manual_seed(1)
+    g_feat = torch.rand((1, h, w, 3), generator=g).to(DEV)
+    g_soft = torch.rand((1, h, w), generator=g).to(DEV)
+    grads = []
+    for lists in (False, True):
+        fvi = fvi0.clone().requires_grad_(True)
+        old = dibr.SAVE_CLOSE_LISTS
+        dibr.SAVE_CLOSE_LISTS = lists
+        try:
+            interp, soft, face_idx = dibr_rasterization(h, w, fvz, fvi, feats, nz)
+            torch.autograd.backward([interp, soft], [g_feat, g_soft])
+        finally:
+            dibr.SAVE_CLOSE_LISTS = old
+        grads.append(fvi.grad)
+        if not lists:
+            out = (interp, soft, face_idx)
+    interp, soft, face_idx = out
+    scale = grads[1].abs().max().item()
+    torch.testing.assert_close(grads[0], grads[1], rtol=1e-4, atol=1e-5 * scale)
+    valid = N(nz) >= 0
+    for r in (h // 2, h // 2 + 7, int(h * 0.3), int(h * 0.05)):
+        ri, rf, _ = oracle.rasterize(h, w, sz.numpy(), si.numpy(), N(feats), valid,
+                                     rows=(r, r + 1))
+        np.testing.assert_array_equal(N(face_idx)[:, r], rf[:, r])
+        np.testing.assert_array_equal(N(interp)[:, r], ri[:, r])
+        osoft, _, _, _, _ = oracle.soft_mask_forward(si.numpy(), N(face_idx), rows=(r, r + 1))
+        np.testing.assert_allclose(N(soft)[:, r], osoft[:, r], rtol=1e-6, atol=1e-7)
+
+
 def test_dense_tile_overflow():
     """More faces on one tile than the LDS list holds (the CAP overflow path): 3000 large
     overlapping triangles on a 48x40 image."""
@@ -514,6 +605,45 @@ def test_prepare_vertices_vs_torch(dname, shared, which):
         err = (v1.grad.double() - v2.grad).abs().max().item()
         err_ref = (v3.grad.double() - v2.grad).abs().max().item()
         assert err <= 4 * err_ref + 1e-5 * v2.grad.abs().max().item(), (err, err_ref)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('shared', [True, False])
+def test_prepare_vertices_high_degree_and_isolated(dname, shared):
+    """Owner-workgroup vertex sums: a hub vertex in 900 faces (its CSR run spans four 256-entry
+    workgroups), runs crossing workgroup boundaries, and vertices without faces (zero)."""
+    import math
+
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import prepare_vertices
+    dt = TORCH_DTYPES[dname]
+    gen = torch.Generator().manual_seed(11)
+    n_rim, B = 900, 2
+    ang = torch.arange(n_rim, dtype=torch.float64) * (2 * math.pi / n_rim)
+    rim = torch.stack([torch.cos(ang), torch.sin(ang), 0.1 * torch.sin(3 * ang)], -1)
+    # vertex 0 hub, 1..900 rim, 901..909 isolated
+    verts = torch.cat([torch.tensor([[0., 0., 0.3]], dtype=torch.float64), rim,
+                       torch.randn((9, 3), generator=gen, dtype=torch.float64)])
+    i = torch.arange(n_rim)
+    faces = torch.stack([torch.zeros_like(i), 1 + i, 1 + (i + 1) % n_rim], -1)
+    # a second strip so runs of other vertices cross workgroup boundaries too
+    faces = torch.cat([faces, torch.stack([1 + i, 1 + (i + 2) % n_rim, 1 + (i + 1) % n_rim], -1)])
+    faces = faces[torch.randperm(faces.shape[0], generator=gen)].to(DEV)
+    cam = workloads.orbit_cameras(B, 0.5).to(DEV, torch.float64)
+    proj = workloads.generate_perspective_projection(math.pi / 4).to(DEV, torch.float64)
+    v = verts.unsqueeze(0).to(DEV)
+    if not shared:
+        v = v + 0.01 * torch.randn((B,) + verts.shape, generator=gen, dtype=torch.float64).to(DEV)
+    v1 = v.to(dt).clone().requires_grad_(True)
+    v2 = v.to(dt).double().clone().requires_grad_(True)
+    out1 = prepare_vertices(v1, faces, proj.to(dt), camera_transform=cam.to(dt))
+    out2 = _torch_prepare(v2, faces, proj, cam)
+    g = [torch.randn(o.shape, generator=gen, dtype=torch.float64).to(DEV) for o in out2]
+    torch.autograd.backward(out1[1], g[1].to(dt))
+    torch.autograd.backward(out2[1], g[1])
+    assert torch.all(v1.grad[:, 901:] == 0)
+    tol = 1e-9 if dname == 'f64' else 2e-4 * v2.grad.abs().max().item()
+    torch.testing.assert_close(v1.grad.double(), v2.grad, rtol=tol, atol=tol)
 
 
 def test_prepare_vertices_rot_trans_and_camera_grad():
