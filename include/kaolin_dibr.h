@@ -269,8 +269,9 @@ int kd_dibr_rasterization_backward_f64(int batch, int height, int width, int64_t
  * normals (B, F, 3).
  * The backward walks each vertex's incident (face, corner) list -- CSR adjacency: adj_offsets
  * (V + 1) int64, adj (3F) int32 entries f * 3 + corner, grouped by vertex -- and writes
- * grad_vertices (Bv, V, 3) (summed over the views when Bv == 1; LDS sums per vertex, one float
- * atomic per workgroup and vertex coordinate).  Any of the three incoming gradients may be NULL
+ * grad_vertices (Bv, V, 3) (summed over the views when Bv == 1).  adj_ranges (num_ranges + 1)
+ * int32 are the workgroups' entry ranges from kd_prepare_vertices_ranges (once per topology):
+ * each vertex is summed in LDS and stored once -- no pre-fill, no global atomics.  Any of the three incoming gradients may be NULL
  * (zero).  fvc is the forward's output.
  * ------------------------------------------------------------------------------------------- */
 int kd_prepare_vertices_forward_f32(int batch, int vertex_batch, int64_t num_vertices,
@@ -289,6 +290,7 @@ int kd_prepare_vertices_backward_f32(int batch, int vertex_batch, int64_t num_ve
                                      const float *fvc, const float *grad_fvc,
                                      const float *grad_fvi, const float *grad_normals,
                                      const int64_t *adj_offsets, const int32_t *adj,
+                                     const int32_t *adj_ranges, int64_t num_ranges,
                                      float *grad_vertices, void *stream);
 int kd_prepare_vertices_backward_f64(int batch, int vertex_batch, int64_t num_vertices,
                                      int64_t num_faces, const int64_t *faces,
@@ -296,7 +298,13 @@ int kd_prepare_vertices_backward_f64(int batch, int vertex_batch, int64_t num_ve
                                      const double *fvc, const double *grad_fvc,
                                      const double *grad_fvi, const double *grad_normals,
                                      const int64_t *adj_offsets, const int32_t *adj,
+                                     const int32_t *adj_ranges, int64_t num_ranges,
                                      double *grad_vertices, void *stream);
+/* Host function (host memory): workgroup entry ranges of the prepare_vertices backward from the
+ * CSR offsets (V + 1): greedy, whole vertices, at most `cap` (<= 256) entries per range unless one
+ * vertex alone has more.  ranges_out holds at least V + 2 values; returns the range count. */
+int64_t kd_prepare_vertices_ranges(const int64_t *adj_offsets, int64_t num_vertices, int32_t cap,
+                                   int32_t *ranges_out);
 
 /* ---------------------------------------------------------------------------------------------
  * mask_iou (kaolin/metrics/render.py:18-40): loss = 1 - mean_b(U_b / (D_b + 1e-10)) with

@@ -326,13 +326,23 @@ def dibr_soft_mask_backward_binned(grad_soft, soft, selected_face_idx, face_vert
 # -------------------------------------------------------------------------------------------
 def vertex_face_adjacency(faces, num_vertices):
     """CSR of each vertex's incident (face, corner) entries f * 3 + corner, grouped by vertex
-    (stable order).  Returns (offsets (V+1) int64, adj (3F) int32) on the faces' device."""
+    (stable order), and the backward's workgroup entry ranges (whole vertices, <= 256 entries;
+    kd_prepare_vertices_ranges).  Returns (offsets (V+1) int64, adj (3F) int32, ranges (R+1)
+    int32) on the faces' device.  Built once per topology (one device->host copy of offsets)."""
+    import numpy as np
     flat = faces.reshape(-1)
     order = torch.argsort(flat, stable=True)
     counts = torch.bincount(flat, minlength=num_vertices)
     offsets = torch.zeros(num_vertices + 1, dtype=torch.long, device=faces.device)
     torch.cumsum(counts, 0, out=offsets[1:])
-    return offsets, order.to(torch.int32)
+    off_h = np.ascontiguousarray(offsets.cpu().numpy())
+    rng = np.empty(num_vertices + 2, np.int32)
+    n = int(_lib.load().kd_prepare_vertices_ranges(off_h.ctypes.data, num_vertices, 256,
+                                                   rng.ctypes.data))
+    if n < 0:
+        raise RuntimeError('vertex_face_adjacency: kd_prepare_vertices_ranges failed')
+    ranges = torch.from_numpy(rng[:n + 1].copy()).to(faces.device)
+    return offsets, order.to(torch.int32), ranges
 
 
 def prepare_vertices_forward(vertices, faces, camera_proj, camera_transform):
@@ -368,12 +378,12 @@ def prepare_vertices_backward(faces, camera_proj, camera_transform, fvc, grad_fv
     dev = fvc.device
     B, F = fvc.shape[:2]
     sfx = _sfx(fvc, 'prepare_vertices_backward')
-    offsets, adj = adjacency
+    offsets, adj, ranges = adjacency
     g = torch.empty((vertex_batch, num_vertices, 3), device=dev, dtype=fvc.dtype)
     _lib.call(f'kd_prepare_vertices_backward_{sfx}', B, vertex_batch, num_vertices, F,
               _ptr(faces), _ptr(camera_proj), _ptr(camera_transform), _ptr(fvc),
-              _ptr(grad_fvc), _ptr(grad_fvi), _ptr(grad_nrm), _ptr(offsets), _ptr(adj), _ptr(g),
-              _stream(dev))
+              _ptr(grad_fvc), _ptr(grad_fvi), _ptr(grad_nrm), _ptr(offsets), _ptr(adj),
+              _ptr(ranges), ranges.numel() - 1, _ptr(g), _stream(dev))
     return g
 
 

@@ -48,7 +48,7 @@ _SIGS = {
     'kd_prepare_vertices_forward': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p,
                                     c_p, c_p],
     'kd_prepare_vertices_backward': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p,
-                                     c_p, c_p, c_p, c_p, c_p],
+                                     c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
     'kd_dibr_soft_mask_backward_binned': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,
                                           c_double, c_double, c_float, c_p, c_p, c_size, c_int,
                                           c_p],
@@ -103,6 +103,8 @@ def load():
             lib.kd_debug_set.restype = c_int
             lib.kd_debug_buffer.argtypes = [c_p]
             lib.kd_debug_buffer.restype = c_int
+            lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
+            lib.kd_prepare_vertices_ranges.restype = c_i64
             for base, sig in _SIGS.items():
                 for sfx in ('f32', 'f64'):
                     fn = getattr(lib, f'{base}_{sfx}')

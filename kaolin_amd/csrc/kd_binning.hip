@@ -170,39 +170,42 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   for (int c = tid; c < nct; c += kBlock) out[c] = s_cnt[c];
 }
 
-// One workgroup per (coarse tile, view): exclusive scan of counts[b][*][c] over the chunks.
-// Each thread owns a contiguous run of chunks; the run sums are scanned with DPP inside each
-// wave and across the 4 waves through LDS (kd_tile.hpp wg_exclusive_scan, one barrier pair).
+// One wave per (coarse tile, view, set), four per workgroup: exclusive scan of counts[b][*][c]
+// over the chunks.  Lane l owns the contiguous run of chunks [l*per, l*per + per), held in
+// registers; the run sums are scanned with DPP (wave_incl_scan).  No LDS, no barriers: every
+// wave's loads are in flight at once and the grid is one round on the chip.
 __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers bb1) {
-  __shared__ int s_w[4];
   const BinBuffers &bb = blockIdx.z ? bb1 : bb0;
-  const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
   const int nct = bb.g.nct();
+  const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int b = blockIdx.y, lane = threadIdx.x & (kWave - 1);
+  if (c >= nct) return;
   const int n = bb.nchunk;
-  const int per = (n + kBlock - 1) / kBlock;
+  const int per = (n + kWave - 1) / kWave;
   int *base = bb.counts + (int64_t)b * n * nct + c;
-  constexpr int kMaxPer = 8;  // register-held run (n <= 2048 chunks = 524k faces per view)
+  constexpr int kMaxPer = 16;  // register-held run (n <= 1024 chunks = 262k faces per view)
   int v[kMaxPer];
   int local = 0;
   if (per <= kMaxPer) {
 #pragma unroll
     for (int k = 0; k < kMaxPer; ++k) {
-      const int j = tid * per + k;
+      const int j = lane * per + k;
       v[k] = (k < per && j < n) ? base[(int64_t)j * nct] : 0;
       local += v[k];
     }
   } else {
     for (int k = 0; k < per; ++k) {
-      const int j = tid * per + k;
+      const int j = lane * per + k;
       if (j < n) local += base[(int64_t)j * nct];
     }
   }
-  int total;
-  int run = wg_exclusive_scan(local, s_w, total);  // exclusive prefix of this thread's run
+  const int incl = wave_incl_scan(local);
+  int run = incl - local;  // exclusive prefix of this lane's run
+  const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
   if (per <= kMaxPer) {
 #pragma unroll
     for (int k = 0; k < kMaxPer; ++k) {
-      const int j = tid * per + k;
+      const int j = lane * per + k;
       if (k < per && j < n) {
         base[(int64_t)j * nct] = run;
         run += v[k];
@@ -210,7 +213,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers
     }
   } else {
     for (int k = 0; k < per; ++k) {
-      const int j = tid * per + k;
+      const int j = lane * per + k;
       if (j < n) {
         const int x = base[(int64_t)j * nct];
         base[(int64_t)j * nct] = run;
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers
       }
     }
   }
-  if (tid == 0) bb.totals[(int64_t)b * nct + c] = total;
+  if (lane == 0) bb.totals[(int64_t)b * nct + c] = total;
 }
 
 template <typename T>
@@ -362,7 +365,8 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
     }
     return hipSuccess;
   }
-  const dim3 grid_c(bb.nchunk, fs.B, njobs), grid_t(bb.g.nct(), fs.B, njobs);
+  const dim3 grid_c(bb.nchunk, fs.B, njobs);
+  const dim3 grid_t((bb.g.nct() + kBlock / kWave - 1) / (kBlock / kWave), fs.B, njobs);
   {
     ProfScope prof(K_BIN_COUNT, stream);
     hipLaunchKernelGGL(kd_bin_count<T>, grid_c, dim3(kBlock), 0, stream, jobs);

@@ -7,7 +7,7 @@
 // order, produced without sorting by a three-pass counting scatter:
 //   1. kd_bin_count   one workgroup per (256-face chunk, view): each face computes its exact
 //                     pixel span (kd::make_span), stores it, and counts per coarse tile in LDS.
-//   2. kd_bin_scan    one workgroup per (coarse tile, view): exclusive scan over the chunks.
+//   2. kd_bin_scan    one wave per (coarse tile, view): exclusive scan over the chunks.
 //   3. kd_bin_scatter one workgroup per (chunk, view): the rank of a face inside its chunk for a
 //                     tile is a popcount over an LDS bitmask of the chunk's faces touching that
 //                     tile, so the global position is scan offset + rank: ascending by face.

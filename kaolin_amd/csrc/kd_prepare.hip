@@ -14,8 +14,8 @@
 //   kd_prepare_bwd  one thread per incident (face, corner) entry of the vertex -> corner CSR
 //                   (built once per topology): projection / normal / gather backward and the
 //                   transposed camera transform, summed over the views when the vertices are
-//                   shared; a vertex's entries are summed in LDS and added with one float
-//                   atomic per (workgroup, vertex, coordinate) instead of one per corner.
+//                   shared; workgroups take whole vertices (ranges computed once per
+//                   topology), sum each vertex's entries in LDS and store it once.
 #include "../../include/kaolin_dibr.h"
 #include "kd_capi.hpp"
 #include "kd_common.hpp"
@@ -114,27 +114,41 @@ __device__ __forceinline__ void corner_grad(const T c[3][3], int k, const T proj
 
 // One thread per incident (face, corner) entry of the CSR (entries grouped by vertex) and vertex
 // batch: the corner's gradient, transformed back to world space, summed over the views it
-// covers; the entries of one vertex are then summed in LDS (segments of the workgroup's 256
-// entries) and added to the vertex with one float atomic per (workgroup, vertex, coordinate).
+// covers.  Workgroup k takes the entries [blocks[k], blocks[k+1]): whole vertices, at most 256
+// entries, or one vertex alone when it has more (then its entries are walked in 256-entry
+// rounds, each thread summing its own).  A vertex's entries are summed in LDS and stored once --
+// no memset, no global atomics.  The workgroups past the last range (blockIdx.x >= nblk) write
+// the zero gradient of vertices without incident faces.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T *fvc,
                                                          const T *gfvc, const T *gfvi,
-                                                         const T *gnrm, const int32_t *adj,
+                                                         const T *gnrm, const int64_t *adj_off,
+                                                         const int32_t *adj,
+                                                         const int32_t *blocks, int nblk,
                                                          T *gvert) {
   __shared__ T s_acc[kBlock][3];
   __shared__ int64_t s_vid[kBlock];
   __shared__ int s_scan[4];
-  const int64_t ne = a.F * 3;
   const int bv = blockIdx.y;
-  const int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool valid = e < ne;
+  T *gv = gvert + (int64_t)bv * a.V * 3;
+  if ((int)blockIdx.x >= nblk) {  // isolated vertices
+    const int64_t v = (int64_t)(blockIdx.x - nblk) * kBlock + threadIdx.x;
+    if (v < a.V && adj_off[v] == adj_off[v + 1]) {
+      gv[v * 3 + 0] = (T)0;
+      gv[v * 3 + 1] = (T)0;
+      gv[v * 3 + 2] = (T)0;
+    }
+    return;
+  }
+  const int64_t e0 = blocks[blockIdx.x], e1 = blocks[blockIdx.x + 1];
+  const bool valid = e0 + threadIdx.x < e1;
   int64_t v = -1;
   T g3[3] = {0, 0, 0};
-  if (valid) {
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
     const int32_t fc = adj[e];
     const int64_t f = fc / 3;
     const int k = fc - (int)f * 3;
-    v = a.faces[f * 3 + k];
+    v = a.faces[fc];  // (F, 3) row-major: entry fc = 3 f + k (one vertex per multi-round range)
     const int b0 = a.Bv == 1 ? 0 : bv, b1 = a.Bv == 1 ? a.B : bv + 1;
     for (int b = b0; b < b1; ++b) {
       const int64_t row = (int64_t)b * a.F + f;
@@ -173,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T 
   __syncthreads();
   for (int i = threadIdx.x; i < nseg * 3; i += kBlock) {
     const int sg = i / 3, q = i - sg * 3;
-    atomicAdd(gvert + ((int64_t)bv * a.V + s_vid[kBlock - 1 - sg]) * 3 + q, s_acc[sg][q]);
+    gv[s_vid[kBlock - 1 - sg] * 3 + q] = s_acc[sg][q];
   }
 }
 
@@ -199,23 +213,27 @@ static int prep_fwd(int B, int Bv, int64_t V, int64_t F, const T *vert, const in
 template <typename T>
 static int prep_bwd(int B, int Bv, int64_t V, int64_t F, const int64_t *faces, const T *proj,
                     const T *tf, const T *fvc, const T *gfvc, const T *gfvi, const T *gnrm,
-                    const int64_t *adj_off, const int32_t *adj, T *gvert, void *stream) {
+                    const int64_t *adj_off, const int32_t *adj, const int32_t *blocks,
+                    int64_t nblk, T *gvert, void *stream) {
   KD_CHECK_ARG(B >= 0 && V >= 0 && F >= 0, "negative size");
   KD_CHECK_ARG(Bv == 1 || Bv == B, "vertex batch must be 1 or the view count");
   KD_CHECK_ARG(F * 3 < (1ll << 31), "too many faces");
-  (void)adj_off;  // the entries carry their vertex through `faces`
   const int64_t total = (int64_t)Bv * V;
   if (total == 0) return KD_OK;
-  hipError_t e0 = hipMemsetAsync(gvert, 0, sizeof(T) * total * 3, (hipStream_t)stream);
-  if (e0 != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e0));
-  if (F == 0 || B == 0) return KD_OK;
+  if (F == 0 || B == 0) {
+    hipError_t e0 = hipMemsetAsync(gvert, 0, sizeof(T) * total * 3, (hipStream_t)stream);
+    if (e0 != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e0));
+    return KD_OK;
+  }
+  KD_CHECK_ARG(adj_off && adj && blocks && nblk >= 1, "vertex adjacency and its ranges required");
+  const int64_t nz = (V + kBlock - 1) / kBlock;
+  KD_CHECK_ARG(nblk + nz < (1ll << 31), "too many faces");
   PrepArgs<T> a{B, Bv, V, F, nullptr, faces, proj, tf};
-  const int64_t nb = (F * 3 + kBlock - 1) / kBlock;
-  KD_CHECK_ARG(nb < (1ll << 31), "too many faces");
   {
     ProfScope prof(K_PREPARE_BWD, (hipStream_t)stream);
-    hipLaunchKernelGGL(kd_prepare_bwd<T>, dim3((unsigned)nb, Bv), dim3(kBlock), 0,
-                       (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj, gvert);
+    hipLaunchKernelGGL(kd_prepare_bwd<T>, dim3((unsigned)(nblk + nz), Bv), dim3(kBlock), 0,
+                       (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj_off, adj, blocks,
+                       (int)nblk, gvert);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "prepare bwd: %s", hipGetErrorString(e));
@@ -247,18 +265,41 @@ int kd_prepare_vertices_backward_f32(int B, int Bv, int64_t V, int64_t F, const 
                                      const float *fvc, const float *grad_fvc,
                                      const float *grad_fvi, const float *grad_normals,
                                      const int64_t *adj_offsets, const int32_t *adj,
+                                     const int32_t *adj_ranges, int64_t num_ranges,
                                      float *grad_vertices, void *stream) {
   return prep_bwd<float>(B, Bv, V, F, faces, camera_proj, camera_transform, fvc, grad_fvc,
-                         grad_fvi, grad_normals, adj_offsets, adj, grad_vertices, stream);
+                         grad_fvi, grad_normals, adj_offsets, adj, adj_ranges, num_ranges,
+                         grad_vertices, stream);
 }
 int kd_prepare_vertices_backward_f64(int B, int Bv, int64_t V, int64_t F, const int64_t *faces,
                                      const double *camera_proj, const double *camera_transform,
                                      const double *fvc, const double *grad_fvc,
                                      const double *grad_fvi, const double *grad_normals,
                                      const int64_t *adj_offsets, const int32_t *adj,
+                                     const int32_t *adj_ranges, int64_t num_ranges,
                                      double *grad_vertices, void *stream) {
   return prep_bwd<double>(B, Bv, V, F, faces, camera_proj, camera_transform, fvc, grad_fvc,
-                          grad_fvi, grad_normals, adj_offsets, adj, grad_vertices, stream);
+                          grad_fvi, grad_normals, adj_offsets, adj, adj_ranges, num_ranges,
+                          grad_vertices, stream);
+}
+
+// Host: workgroup entry ranges of the backward from the CSR offsets (host memory, V + 1 values):
+// greedy, whole vertices per range, at most `cap` entries unless one vertex alone has more.
+// Writes up to V + 1 range starts plus the end into ranges_out; returns the number of ranges.
+int64_t kd_prepare_vertices_ranges(const int64_t *adj_offsets, int64_t V, int32_t cap,
+                                   int32_t *ranges_out) {
+  if (!adj_offsets || !ranges_out || V < 0 || cap < 1) return -1;
+  int64_t n = 0, start = adj_offsets[0];
+  for (int64_t v = 0; v < V; ++v) {
+    const int64_t end = adj_offsets[v + 1];
+    if (end - start > cap && adj_offsets[v] > start) {  // close the range before vertex v
+      ranges_out[n++] = (int32_t)start;
+      start = adj_offsets[v];
+    }
+  }
+  if (adj_offsets[V] > start) ranges_out[n++] = (int32_t)start;
+  ranges_out[n] = (int32_t)adj_offsets[V];
+  return n;
 }
 
 }  // extern "C"

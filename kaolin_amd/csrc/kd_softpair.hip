@@ -29,6 +29,8 @@
 namespace kd {
 
 constexpr unsigned kPersistentBlocks = 2048;  // 8 workgroups per CU for the item loops
+constexpr int kMathItems = 1;                 // items per pair-math workgroup pass (4: slower)
+constexpr unsigned kMathBlocks = 8192;        // pair-math grid
 
 size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize) {
   const int64_t ntiles = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
@@ -185,7 +187,41 @@ __global__ __launch_bounds__(kBlock, 8) void kd_soft_pairs(SoftArgs<T> a, SoftPa
   int my_kid = 0, lbase = 0;
   if (tid == 0) s_nrec = 0;
 
+  // faces matter only where they reach an uncovered pixel: the filter boxes of tile_rounds
+  // shrink to the uncovered pixels' bounding boxes (exact: a record needs the pixel centre
+  // inside the face's enlarged span)
+  __shared__ int s_box[4];
+  if (tid == 0) {
+    s_box[0] = s_box[2] = 1 << 30;
+    s_box[1] = s_box[3] = -1;
+  }
+  if (!(fs.dbg & 512)) {
+    const uint64_t um = __ballot(unc);
+    t.wave_live = t.wave_live && um != 0ull;
+    if (um) {
+      uint32_t cols = 0u;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) cols |= (uint32_t)(um >> (8 * r)) & 0xffu;
+      t.SX0 = t.WX0 + __builtin_ctz(cols);
+      t.SX1 = t.WX0 + 31 - __builtin_clz(cols);
+      t.SY0 = t.WY0 + __builtin_ctzll(um) / 8;
+      t.SY1 = t.WY0 + (63 - __builtin_clzll(um)) / 8;
+    }
+  }
+  __syncthreads();
+  if (!(fs.dbg & 512) && t.wave_live && (tid & 63) == 0) {
+    atomicMin(&s_box[0], t.SX0);
+    atomicMax(&s_box[1], t.SX1);
+    atomicMin(&s_box[2], t.SY0);
+    atomicMax(&s_box[3], t.SY1);
+  }
   if (__syncthreads_or(unc)) {
+    if (!(fs.dbg & 512)) {
+      t.FX0 = s_box[0];
+      t.FX1 = s_box[1];
+      t.FY0 = s_box[2];
+      t.FY1 = s_box[3];
+    }
     auto stage = [&](int, int64_t) {};  // pass A needs the spans only
     auto round = [&](int nsub, int cnt) {
       if (wave_unc && !(fs.dbg & 1024))
@@ -225,7 +261,9 @@ __global__ __launch_bounds__(kBlock, 8) void kd_soft_pairs(SoftArgs<T> a, SoftPa
       pb.tiles[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
     }
     __syncthreads();
-    for (int c = tid; c < nch; c += kBlock) pb.items[s_base + c] = make_int2((int)tile, c);
+    // item = (tile, chunk | records in the chunk << 16): the math pass needs no tile lookup
+    for (int c = tid; c < nch; c += kBlock)
+      pb.items[s_base + c] = make_int2((int)tile, c | (min(kBlock, n - c * kBlock) << 16));
   }
 }
 
@@ -330,45 +368,61 @@ __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPair
 // (bit-identical to the reference), its backward coefficients (GRAD) and optionally the close
 // lists.  (Reducing a tile in the workgroup that finishes its last chunk needs a device-scope
 // release per item -- an L2 writeback on gfx950 -- and measured 30x slower than kd_soft_reduce.)
-template <typename T, bool GRAD, bool LISTS>
+template <typename T, bool GRAD, bool LISTS, int R>
 __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftPairBuf<T> pb) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
   const int nitems = pb.counters[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {  // (tile, 256-record chunk) items
-    const int2 item = pb.items[it];
-    const int64_t tile = item.x;
-    const int n = pb.ntile[2 * tile];
-    const int i = item.y * kBlock + threadIdx.x;
-    if (i < n) {
+  // R items per workgroup pass, their loads issued together: each thread has R independent
+  // item -> record -> corner load chains in flight (the kernel is latency-bound, not ALU-bound)
+  for (int it0 = blockIdx.x * R; it0 < nitems; it0 += gridDim.x * R) {
+    int2 item[R];
+    bool ok[R];
+    SoftPairRec r[R];
+    T v[R][6];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      item[u] = it0 + u < nitems ? pb.items[it0 + u] : make_int2(0, 0);
+      ok[u] = (int)threadIdx.x < (item[u].y >> 16);
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (ok[u]) r[u] = pb.rec[(int64_t)item[u].x * pb.cap + (item[u].y & 0xffff) * kBlock +
+                               threadIdx.x];
+#pragma unroll
+    for (int u = 0; u < R; ++u)
+      if (ok[u]) load_corners(fs, (int64_t)r[u].row, v[u]);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (!ok[u]) continue;
+      const int64_t tile = item[u].x;
+      const int i = (item[u].y & 0xffff) * kBlock + threadIdx.x;
       const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
       const int tx = tl % pb.ntx, ty = tl / pb.ntx;
-      int64_t lo, hi;
-      view_range(fs, b, lo, hi);
-      SoftPairRec *rp = pb.rec + tile * pb.cap + i;
-      const SoftPairRec r = *rp;
       int px, py;
-      tile_pixel(tx, ty, r.q, px, py);
+      tile_pixel(tx, ty, r[u].q, px, py);
       const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
-      T v[6];
-      load_corners(fs, (int64_t)r.row, v);
       int et = 0;
       T prob = (T)0;
-      if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+      if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v[u], M, a.sigmainv, et, prob);
       const int64_t gp = ((int64_t)b * H + py) * W + px;
       pb.sprob[tile * pb.cap + i] = prob;  // record order: coalesced
-      rp->type = (uint8_t)et;
-      if (LISTS) {
-        const int64_t o = gp * K + r.slot;
-        a.prob[o] = prob;
-        a.cidx[o] = (int64_t)r.row - lo;
-        a.ctype[o] = (uint8_t)(et + 1);
+      pb.rec[tile * pb.cap + i].type = (uint8_t)et;
+      if (LISTS || a.last) {
+        int64_t lo, hi;
+        view_range(fs, b, lo, hi);
+        if (LISTS) {
+          const int64_t o = gp * K + r[u].slot;
+          a.prob[o] = prob;
+          a.cidx[o] = (int64_t)r[u].row - lo;
+          a.ctype[o] = (uint8_t)(et + 1);
+        }
+        if (a.last && r[u].slot == K - 1) a.last[gp] = (int32_t)((int64_t)r[u].row - lo);
       }
-      if (a.last && r.slot == K - 1) a.last[gp] = (int32_t)((int64_t)r.row - lo);
       if (GRAD) {
         SoftCoef<T> c;
-        soft_pair_coef<T>(x0, y0, v, et, prob, M, c.h);
+        soft_pair_coef<T>(x0, y0, v[u], et, prob, M, c.h);
         pb.coef[tile * pb.cap + i] = c;
       }
     }
@@ -473,6 +527,67 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_pairs(SoftArgs<T> a, SoftP
   }
 }
 
+// Flat over the (tile, 256-record chunk) items, one record per thread: s_p * h_j expanded to
+// the face's 6 corner coordinates, summed over the record's run of equal faces inside its wave
+// by a segmented inclusive scan (records are face-major runs; no LDS), and the run's last lane
+// adds the nonzero sums with float atomics.  Every
+// record costs the same, so the grid is balanced however the records fall on the tiles.
+template <typename T>
+__device__ __forceinline__ T shfl_up_t(T v, int d) {
+  return __shfl_up(v, d);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  const FaceSet<T> &fs = a.fs;
+  const int H = fs.H, W = fs.W;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int nitems = pb.counters[0];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const int2 item = pb.items[it];
+    const int64_t tile = item.x;
+    const bool ok = (int)threadIdx.x < (item.y >> 16);
+    const int64_t ri = tile * pb.cap + (item.y & 0xffff) * kBlock + threadIdx.x;
+    int key = -1;
+    T g[6] = {0, 0, 0, 0, 0, 0};
+    if (ok) {
+      const SoftPairRec r = pb.rec[ri];
+      const SoftCoef<T> c = pb.coef[ri];
+      const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+      int px, py;
+      tile_pixel(tl % pb.ntx, tl / pb.ntx, r.q, px, py);
+      const int64_t gp = ((int64_t)b * H + py) * W + px;
+      const double sp = -(double)a.sigmainv * (double)a.grad_soft[gp] *
+                        (1.0 - (double)a.soft_in[gp]);
+      soft_add_pair<T>(g, r.type, sp, c);
+      key = r.row;
+    }
+    // segmented inclusive scan over the wave's lanes; segments are the runs of equal key (a
+    // face may have several runs in a tile: one per wave sub-list chunk), numbered by the count
+    // of run heads up to the lane
+    const int prev_key = __shfl_up(key, 1);
+    const uint64_t heads = __ballot(lane == 0 || prev_key != key);
+    const int seg = __popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+      const int o_seg = __shfl_up(seg, d);
+      const bool take = lane >= d && o_seg == seg;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        const T o = shfl_up_t<T>(g[q], d);
+        g[q] += take ? o : (T)0;
+      }
+    }
+    const int next_key = __shfl_down(key, 1);
+    const bool tail = key >= 0 && (lane == kWave - 1 || next_key != key);
+    if (tail && !(fs.dbg & 128)) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q)
+        if (g[q] != (T)0) atomicAdd(a.grad_fvi + (int64_t)key * 6 + q, g[q]);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
@@ -489,17 +604,20 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   {
     ProfScope prof(K_SOFT_MATH, stream);
-    const dim3 grid((a.fs.dbg & 2048) ? 512 : (a.fs.dbg & 4096) ? kPersistentBlocks : 8192);
     const bool lists = a.prob != nullptr;
+    const dim3 grid(kMathBlocks);
+#define KD_MATH_LAUNCH(G, L)                                                                  \
+  hipLaunchKernelGGL((kd_soft_pair_math<T, G, L, kMathItems>), grid, dim3(kBlock), 0, stream, a, \
+                     pb)
     if (grad && lists)
-      hipLaunchKernelGGL((kd_soft_pair_math<T, true, true>), grid, dim3(kBlock), 0, stream, a, pb);
+      KD_MATH_LAUNCH(true, true);
     else if (grad)
-      hipLaunchKernelGGL((kd_soft_pair_math<T, true, false>), grid, dim3(kBlock), 0, stream, a, pb);
+      KD_MATH_LAUNCH(true, false);
     else if (lists)
-      hipLaunchKernelGGL((kd_soft_pair_math<T, false, true>), grid, dim3(kBlock), 0, stream, a, pb);
+      KD_MATH_LAUNCH(false, true);
     else
-      hipLaunchKernelGGL((kd_soft_pair_math<T, false, false>), grid, dim3(kBlock), 0, stream, a,
-                         pb);
+      KD_MATH_LAUNCH(false, false);
+#undef KD_MATH_LAUNCH
   }
   if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
@@ -536,8 +654,11 @@ int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t s
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_SOFT_BWD_PAIRS, stream);
-    hipLaunchKernelGGL(kd_soft_bwd_pairs<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream, a,
-                       pb);
+    if (a.fs.dbg & 4096)  // the per-tile LDS form, for A/B runs
+      hipLaunchKernelGGL(kd_soft_bwd_pairs<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream,
+                         a, pb);
+    else
+      hipLaunchKernelGGL(kd_soft_bwd_items<T>, dim3(kMathBlocks), dim3(kBlock), 0, stream, a, pb);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));

@@ -29,6 +29,11 @@ struct TileGeom {
   int px, py;              // this lane's pixel
   bool inimg, wave_live;
   int nbin;                // faces in the tile's coarse bin when known (tile order), else -1
+  // face filter boxes of tile_rounds (default: the tile and the wave's sub-tile); a caller whose
+  // pixels do not all need faces may shrink them to the pixels that do (wave_live = false when
+  // the wave has none)
+  int FX0, FX1, FY0, FY1;      // tile filter
+  int SX0, SX1, SY0, SY1;      // this wave's sub-list filter
 };
 
 // (view, fine tile) of this workgroup: the bins' heaviest-first order (tile_order) when the
@@ -66,6 +71,14 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
   t.inimg = t.px < W && t.py < H;
   t.wave_live = t.WX0 < W && t.WY0 < H;
   t.nbin = -1;
+  t.FX0 = t.X0;
+  t.FX1 = t.X1;
+  t.FY0 = t.Y0;
+  t.FY1 = t.Y1;
+  t.SX0 = t.WX0;
+  t.SX1 = t.WX1;
+  t.SY0 = t.WY0;
+  t.SY1 = t.WY1;
   return t;
 }
 __device__ __forceinline__ TileGeom tile_geom(int H, int W) { return tile_geom(H, W, blockIdx.x); }
@@ -153,7 +166,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
       const int e = base0 + u * kBlock + tid;
       const int f = fr[u];
       const Span sp = spr[u];
-      const bool ov = e < n && span_overlaps(sp, t.X0, t.X1, t.Y0, t.Y1);
+      const bool ov = e < n && span_overlaps(sp, t.FX0, t.FX1, t.FY0, t.FY1);
       int tot;
       const int pos = wg_compact(ov, L.cnt, tot);
       // a batch holds at most kCap faces: flush first if this chunk would overflow it
@@ -165,7 +178,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
         for (int k0 = 0; k0 < cnt; k0 += kWave) {
           const int k = k0 + lane;
           const bool ok =
-              t.wave_live && k < cnt && span_overlaps(L.span[k], t.WX0, t.WX1, t.WY0, t.WY1);
+              t.wave_live && k < cnt && span_overlaps(L.span[k], t.SX0, t.SX1, t.SY0, t.SY1);
           const uint64_t m = __ballot(ok);
           if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
           nsub += __popcll(m);
@@ -191,7 +204,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
     for (int k0 = 0; k0 < cnt; k0 += kWave) {
       const int k = k0 + lane;
       const bool ok =
-          t.wave_live && k < cnt && span_overlaps(L.span[k], t.WX0, t.WX1, t.WY0, t.WY1);
+          t.wave_live && k < cnt && span_overlaps(L.span[k], t.SX0, t.SX1, t.SY0, t.SY1);
       const uint64_t m = __ballot(ok);
       if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
       nsub += __popcll(m);

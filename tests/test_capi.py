@@ -43,3 +43,28 @@ def test_shim_rejects_bad_dtype_and_sizes():
         _C._sfx(torch.zeros(1, dtype=torch.float16), 'x')
     with pytest.raises(RuntimeError):
         _C._check_size('f', 'a', torch.zeros(2, 3), (2, 4))
+
+
+def test_prepare_vertices_ranges_partition():
+    """kd_prepare_vertices_ranges (host): ranges tile all entries, never split a vertex, hold at
+    most `cap` entries unless a single vertex has more."""
+    import numpy as np
+    from kaolin_amd import _lib
+    rng = np.random.default_rng(0)
+    for cap in (1, 7, 256):
+        deg = rng.integers(0, 12, 3000)
+        deg[[5, 900, 2999]] = [0, 700, 300]  # isolated, hubs past the cap
+        off = np.zeros(deg.size + 1, np.int64)
+        np.cumsum(deg, out=off[1:])
+        out = np.empty(deg.size + 2, np.int32)
+        n = int(_lib.load().kd_prepare_vertices_ranges(off.ctypes.data, deg.size, cap,
+                                                       out.ctypes.data))
+        r = out[:n + 1].astype(np.int64)
+        assert r[0] == 0 and r[-1] == off[-1] and np.all(np.diff(r) > 0)
+        assert np.all(np.isin(r, off))  # boundaries fall between vertices
+        for a, b in zip(r[:-1], r[1:]):
+            if b - a > cap:  # only a single vertex may exceed the cap
+                assert np.count_nonzero((off[:-1] >= a) & (off[:-1] < b) & (deg > 0)) == 1
+    empty = np.zeros(4, np.int64)
+    out = np.empty(5, np.int32)
+    assert _lib.load().kd_prepare_vertices_ranges(empty.ctypes.data, 3, 256, out.ctypes.data) == 0

@@ -11,10 +11,16 @@ code = ("import sys, runpy; sys.argv=['bench.py','--no-cpu-baseline','--steps','
         "from kaolin_amd import _lib; _lib.load().kd_debug_set(%d); "
         "runpy.run_path('bench.py', run_name='__main__')")
 res = {a: [], b: []}
+kern = {a: {}, b: {}}
 for r in range(reps):
     for f in (a, b):
         out = subprocess.run([sys.executable, '-c', code % f], cwd=root, capture_output=True,
                              text=True, timeout=600).stdout.strip().splitlines()[-1]
-        res[f].append(json.loads(out)['ms_per_step'])
+        d = json.loads(out)
+        res[f].append(d['ms_per_step'])
+        for k, v in d['kernels'].items():
+            kern[f].setdefault(k, []).append(v['avg_us'])
 for f in (a, b):
     print(f'flags={f}: ms/step {sorted(res[f])}  best {min(res[f]):.4f}')
+for k in kern[a]:
+    print(f'  {k:22s} ' + '  '.join(f'{f}: {min(kern[f].get(k, [0])):7.2f}' for f in (a, b)))
