@@ -111,6 +111,7 @@ struct SoftArgs {
   // buffers the soft reduction zeroes on the side (the fused backward's gradients), nullable
   T *zero0, *zero1;
   int64_t nzero0, nzero1;
+  int want_coef;  // fused soft-mask kernel: store the backward's coefficients
 };
 
 // Per-wave pair list of the current batch and its per-pixel bookkeeping.

@@ -29,6 +29,7 @@
 namespace kd {
 
 constexpr unsigned kPersistentBlocks = 2048;  // 8 workgroups per CU for the item loops
+constexpr int kFuseSlots = 32;               // knum bound of the fused soft-mask kernel
 constexpr int kMathItems = 1;                 // items per pair-math workgroup pass (4: slower)
 constexpr unsigned kMathBlocks = 8192;        // pair-math grid
 
@@ -82,6 +83,37 @@ __device__ __forceinline__ void tile_pixel(int tx, int ty, int q, int &px, int &
   py = ty * kTile + (w >> 1) * 8 + (l >> 3);
 }
 
+// Backward coefficients h_j of one pair (see the file comment); the geometric factors are the
+// reference's expressions (dibr_soft_mask_cuda.cu:288-343) in T.
+template <typename T>
+__device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et, T prob, float M,
+                                               T h[4]) {
+  // the backward's coefficients need gradient accuracy, not bit-exactness: reciprocals
+  const double s = (double)prob * (1.0 / ((1.0 - (double)prob + KD_SOFT_EPS) * (double)M));
+  if (et >= 3) {
+    const int ps = (et - 3) * 2;
+    h[0] = (T)(s * (double)((T)2 * (v[ps] - x0)));
+    h[1] = (T)(s * (double)((T)2 * (v[ps + 1] - y0)));
+    h[2] = (T)0;
+    h[3] = (T)0;
+  } else {
+    const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
+    const T x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
+    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+    const T up = A * x0 + Bc * y0 + C;
+    const T down = A * A + Bc * Bc;
+    const double rd = 1.0 / ((double)down + KD_SOFT_EPS);
+    const T dissquare = (T)((double)(up * up) * rd);
+    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) * rd);
+    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) * rd);
+    const T dzdC = (T)((double)((T)2 * up) * rd);
+    h[0] = (T)(s * (double)(dzdB - y2 * dzdC));
+    h[1] = (T)(s * (double)(x2 * dzdC - dzdA));
+    h[2] = (T)(s * (double)(y1 * dzdC - dzdB));
+    h[3] = (T)(s * (double)(dzdA - x1 * dzdC));
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // pass A: (pixel, slot, face) records per tile
 // ------------------------------------------------------------------------------------------
@@ -112,7 +144,8 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
                                                    int K, const TileGeom &t, int64_t lo,
                                                    int lbase, int &my_kid, uint64_t *s_pm,
                                                    unsigned short *s_off, int *s_nrec,
-                                                   SoftPairRec *rec) {
+                                                   SoftPairRec *rec,
+                                                   unsigned short (*s_ridx)[kBlock] = nullptr) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qx = lane & 7, qy = lane >> 3;
   const int j = c * kWave + lane;
@@ -155,14 +188,21 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
     r.slot = (uint16_t)slot++;
     r.q = (uint8_t)tile_q;
     r.type = 0;
-    rec[base + s_off[jj] + __popcll(s_pm[jj] & below)] = r;
+    const int ri = base + s_off[jj] + __popcll(s_pm[jj] & below);
+    rec[ri] = r;
+    if (s_ridx) s_ridx[r.slot][tile_q] = (unsigned short)ri;  // (slot, pixel) -> record
   }
   my_kid = slot;
   wave_lds_sync();
 }
 
-template <typename T>
-__global__ __launch_bounds__(kBlock, 8) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
+// Records of one tile's pixel set (pass A).  FUSED (knum <= kFuseSlots, no close-face lists):
+// the same workgroup then runs the pair math over its own records and the ordered product of
+// each pixel's slots -- the whole soft mask in one launch.  Pass A notes each (slot, pixel)'s
+// record index in LDS, so the product reads the probabilities in slot order.
+template <typename T, bool FUSED, int OCC = 8>
+__global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  __shared__ unsigned short s_ridx[FUSED ? kFuseSlots : 1][kBlock];
   TileClock clk(a.fs.tbuf, 1);
   __shared__ TileLists L;
   __shared__ uint64_t s_pm[4][kWave];
@@ -227,7 +267,7 @@ __global__ __launch_bounds__(kBlock, 8) void kd_soft_pairs(SoftArgs<T> a, SoftPa
       if (wave_unc && !(fs.dbg & 1024))
         for (int c = 0; c * kWave < nsub; ++c)
           soft_chunk_records(L, nsub, c, unc, K, t, lo, lbase, my_kid, s_pm[w], s_off[w],
-                             &s_nrec, rec);
+                             &s_nrec, rec, FUSED ? s_ridx : nullptr);
       lbase += cnt;
     };
     // once every uncovered pixel holds K close faces, later faces cannot enter
@@ -265,42 +305,61 @@ __global__ __launch_bounds__(kBlock, 8) void kd_soft_pairs(SoftArgs<T> a, SoftPa
     for (int c = tid; c < nch; c += kBlock)
       pb.items[s_base + c] = make_int2((int)tile, c | (min(kBlock, n - c * kBlock) << 16));
   }
+  if constexpr (FUSED) {
+    // side job of the launch: the backward's gradient buffers (grid-stride, coalesced)
+    const int64_t nz = a.nzero0 + a.nzero1;
+    const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
+    for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + tid; i < nz;
+         i += nblk * kBlock) {
+      if (i < a.nzero0)
+        a.zero0[i] = (T)0;
+      else
+        a.zero1[i - a.nzero0] = (T)0;
+    }
+    if (n == 0) return;
+    // pair math over this tile's records (record order: coalesced reads)
+    const float M = fs.M;
+    const int tx = tl % pb.ntx, ty = tl / pb.ntx;
+    T *sp = pb.sprob + tile * pb.cap;  // record order
+    for (int i = tid; i < n; i += kBlock) {
+      const SoftPairRec r = rec[i];
+      T v[6];
+      load_corners(fs, (int64_t)r.row, v);
+      int px, py;
+      tile_pixel(tx, ty, r.q, px, py);
+      const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
+      int et = 0;
+      T prob = (T)0;
+      soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+      sp[i] = prob;
+      rec[i].type = (uint8_t)et;
+      if (a.want_coef) {  // gradients wanted: the backward's coefficients
+        SoftCoef<T> c;
+        soft_pair_coef<T>(x0, y0, v, et, prob, M, c.h);
+        pb.coef[tile * pb.cap + i] = c;
+      }
+    }
+    __syncthreads();  // the workgroup's probabilities are visible to it
+    // soft = 1 - prod(1 - p) in slot order (dibr_soft_mask_cuda.cu:174-181, double-promoted)
+    if (unc && my_kid > 0) {
+      constexpr int U = 8;
+      T prod = (T)1.0;
+      for (int s0 = 0; s0 < my_kid; s0 += U) {
+        T pv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pv[u] = s0 + u < my_kid ? sp[s_ridx[s0 + u][tid]] : (T)0;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (s0 + u < my_kid) prod = (T)((double)prod * (1.0 - (double)pv[u]));
+      }
+      a.soft[p] = (T)(1.0 - (double)prod);
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------------
 // per-pair math
 // ------------------------------------------------------------------------------------------
-// Backward coefficients h_j of one pair (see the file comment); the geometric factors are the
-// reference's expressions (dibr_soft_mask_cuda.cu:288-343) in T.
-template <typename T>
-__device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et, T prob, float M,
-                                               T h[4]) {
-  // the backward's coefficients need gradient accuracy, not bit-exactness: reciprocals
-  const double s = (double)prob * (1.0 / ((1.0 - (double)prob + KD_SOFT_EPS) * (double)M));
-  if (et >= 3) {
-    const int ps = (et - 3) * 2;
-    h[0] = (T)(s * (double)((T)2 * (v[ps] - x0)));
-    h[1] = (T)(s * (double)((T)2 * (v[ps + 1] - y0)));
-    h[2] = (T)0;
-    h[3] = (T)0;
-  } else {
-    const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
-    const T x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
-    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-    const T up = A * x0 + Bc * y0 + C;
-    const T down = A * A + Bc * Bc;
-    const double rd = 1.0 / ((double)down + KD_SOFT_EPS);
-    const T dissquare = (T)((double)(up * up) * rd);
-    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) * rd);
-    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) * rd);
-    const T dzdC = (T)((double)((T)2 * up) * rd);
-    h[0] = (T)(s * (double)(dzdB - y2 * dzdC));
-    h[1] = (T)(s * (double)(x2 * dzdC - dzdA));
-    h[2] = (T)(s * (double)(y1 * dzdC - dzdB));
-    h[3] = (T)(s * (double)(dzdA - x1 * dzdC));
-  }
-}
-
 // soft = 1 - prod(1 - p) over the close faces of the 256 pixels of one tile, in slot order
 // (dibr_soft_mask_cuda.cu:174-181, double-promoted product).  The probabilities are stored in
 // record order; kReduceSlots slots at a time are placed into an LDS table by (slot, pixel) and
@@ -532,58 +591,104 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_pairs(SoftArgs<T> a, SoftP
 // by a segmented inclusive scan (records are face-major runs; no LDS), and the run's last lane
 // adds the nonzero sums with float atomics.  Every
 // record costs the same, so the grid is balanced however the records fall on the tiles.
-template <typename T>
-__device__ __forceinline__ T shfl_up_t(T v, int d) {
-  return __shfl_up(v, d);
+// One step of a segmented inclusive wave scan with DPP (no LDS): lanes add the DPP source lane's
+// six sums when it belongs to the same segment (invalid sources read segment -1).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_scan_dpp(int seg, float g[6]) {
+  const int os = __builtin_amdgcn_update_dpp(-1, seg, CTRL, ROWS, 0xf, false);
+  const bool take = os == seg;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const float o = __int_as_float(
+        __builtin_amdgcn_update_dpp(0, __float_as_int(g[q]), CTRL, ROWS, 0xf, false));
+    g[q] += take ? o : 0.f;
+  }
 }
 
 template <typename T>
+__device__ __forceinline__ void seg_scan_shfl(int seg, int lane, T g[6]) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int o_seg = __shfl_up(seg, d);
+    const bool take = lane >= d && o_seg == seg;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+      const T o = __shfl_up(g[q], d);
+      g[q] += take ? o : (T)0;
+    }
+  }
+}
+
+template <typename T, int R>
 __global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftPairBuf<T> pb) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const int lane = threadIdx.x & (kWave - 1);
   const int nitems = pb.counters[0];
-  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-    const int2 item = pb.items[it];
-    const int64_t tile = item.x;
-    const bool ok = (int)threadIdx.x < (item.y >> 16);
-    const int64_t ri = tile * pb.cap + (item.y & 0xffff) * kBlock + threadIdx.x;
-    int key = -1;
-    T g[6] = {0, 0, 0, 0, 0, 0};
-    if (ok) {
-      const SoftPairRec r = pb.rec[ri];
-      const SoftCoef<T> c = pb.coef[ri];
-      const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-      int px, py;
-      tile_pixel(tl % pb.ntx, tl / pb.ntx, r.q, px, py);
-      const int64_t gp = ((int64_t)b * H + py) * W + px;
-      const double sp = -(double)a.sigmainv * (double)a.grad_soft[gp] *
-                        (1.0 - (double)a.soft_in[gp]);
-      soft_add_pair<T>(g, r.type, sp, c);
-      key = r.row;
+  // R items per workgroup pass; their load chains (item -> record and coefficients -> the
+  // pixel's gradient and soft value) are issued together
+  for (int it0 = blockIdx.x * R; it0 < nitems; it0 += gridDim.x * R) {
+    int2 item[R];
+    bool ok[R];
+    SoftPairRec r[R];
+    SoftCoef<T> c[R];
+    T gs[R], so[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      item[u] = it0 + u < nitems ? pb.items[it0 + u] : make_int2(0, 0);
+      ok[u] = (int)threadIdx.x < (item[u].y >> 16);
     }
-    // segmented inclusive scan over the wave's lanes; segments are the runs of equal key (a
-    // face may have several runs in a tile: one per wave sub-list chunk), numbered by the count
-    // of run heads up to the lane
-    const int prev_key = __shfl_up(key, 1);
-    const uint64_t heads = __ballot(lane == 0 || prev_key != key);
-    const int seg = __popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
 #pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-      const int o_seg = __shfl_up(seg, d);
-      const bool take = lane >= d && o_seg == seg;
-#pragma unroll
-      for (int q = 0; q < 6; ++q) {
-        const T o = shfl_up_t<T>(g[q], d);
-        g[q] += take ? o : (T)0;
+    for (int u = 0; u < R; ++u)
+      if (ok[u]) {
+        const int64_t ri =
+            (int64_t)item[u].x * pb.cap + (item[u].y & 0xffff) * kBlock + threadIdx.x;
+        r[u] = pb.rec[ri];
+        c[u] = pb.coef[ri];
       }
-    }
-    const int next_key = __shfl_down(key, 1);
-    const bool tail = key >= 0 && (lane == kWave - 1 || next_key != key);
-    if (tail && !(fs.dbg & 128)) {
 #pragma unroll
-      for (int q = 0; q < 6; ++q)
-        if (g[q] != (T)0) atomicAdd(a.grad_fvi + (int64_t)key * 6 + q, g[q]);
+    for (int u = 0; u < R; ++u)
+      if (ok[u]) {
+        const int64_t tile = item[u].x;
+        const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+        int px, py;
+        tile_pixel(tl % pb.ntx, tl / pb.ntx, r[u].q, px, py);
+        const int64_t gp = ((int64_t)b * H + py) * W + px;
+        gs[u] = a.grad_soft[gp];
+        so[u] = a.soft_in[gp];
+      }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      int key = -1;
+      T g[6] = {0, 0, 0, 0, 0, 0};
+      if (ok[u]) {
+        const double sp = -(double)a.sigmainv * (double)gs[u] * (1.0 - (double)so[u]);
+        soft_add_pair<T>(g, r[u].type, sp, c[u]);
+        key = r[u].row;
+      }
+      // segmented inclusive scan over the wave's lanes; segments are the runs of equal key (a
+      // face may have several runs in a tile: one per wave sub-list chunk), numbered by the
+      // count of run heads up to the lane
+      const int prev_key = __shfl_up(key, 1);
+      const uint64_t heads = __ballot(lane == 0 || prev_key != key);
+      const int seg = __popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
+      if constexpr (std::is_same<T, float>::value) {
+        seg_scan_dpp<0x111, 0xf>(seg, g);  // row_shr:1
+        seg_scan_dpp<0x112, 0xf>(seg, g);  // row_shr:2
+        seg_scan_dpp<0x114, 0xf>(seg, g);  // row_shr:4
+        seg_scan_dpp<0x118, 0xf>(seg, g);  // row_shr:8
+        seg_scan_dpp<0x142, 0xa>(seg, g);  // row_bcast:15 -> rows 1, 3
+        seg_scan_dpp<0x143, 0xc>(seg, g);  // row_bcast:31 -> rows 2, 3
+      } else {
+        seg_scan_shfl<T>(seg, lane, g);
+      }
+      const int next_key = __shfl_down(key, 1);
+      const bool tail = key >= 0 && (lane == kWave - 1 || next_key != key);
+      if (tail && !(fs.dbg & 128)) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q)
+          if (g[q] != (T)0) atomicAdd(a.grad_fvi + (int64_t)key * 6 + q, g[q]);
+      }
     }
   }
 }
@@ -597,10 +702,23 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   const FaceSet<T> &fs = a.fs;
   a.fs.dbg = debug_flags();
   a.fs.tbuf = debug_tile_buffer();
+  // one launch for the whole soft mask (the autograd path: no close-face lists)
+  const bool fused =
+      reduce && a.soft && !a.prob && !a.last && a.K <= kFuseSlots && !(a.fs.dbg & 4096);
+  if (fused) {
+    a.want_coef = grad ? 1 : 0;
+    ProfScope prof(K_SOFT_PAIRS, stream);
+    // 6 workgroups per CU (the 16 KB record-index table); 4 and 8 measured no faster
+    hipLaunchKernelGGL((kd_soft_pairs<T, true, 6>), dim3((unsigned)pb.ntiles, fs.B),
+                       dim3(kBlock), 0, stream, a, pb);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
+    return KD_OK;
+  }
   {
     ProfScope prof(K_SOFT_PAIRS, stream);
-    hipLaunchKernelGGL(kd_soft_pairs<T>, dim3((unsigned)pb.ntiles, fs.B), dim3(kBlock), 0, stream,
-                       a, pb);
+    hipLaunchKernelGGL((kd_soft_pairs<T, false>), dim3((unsigned)pb.ntiles, fs.B), dim3(kBlock),
+                       0, stream, a, pb);
   }
   {
     ProfScope prof(K_SOFT_MATH, stream);
@@ -657,8 +775,12 @@ int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t s
     if (a.fs.dbg & 4096)  // the per-tile LDS form, for A/B runs
       hipLaunchKernelGGL(kd_soft_bwd_pairs<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream,
                          a, pb);
+    else if (a.fs.dbg & 256)  // four items per pass (measured slower), for A/B runs
+      hipLaunchKernelGGL((kd_soft_bwd_items<T, 4>), dim3(kPersistentBlocks), dim3(kBlock), 0,
+                         stream, a, pb);
     else
-      hipLaunchKernelGGL(kd_soft_bwd_items<T>, dim3(kMathBlocks), dim3(kBlock), 0, stream, a, pb);
+      hipLaunchKernelGGL((kd_soft_bwd_items<T, 1>), dim3(kMathBlocks), dim3(kBlock), 0, stream,
+                         a, pb);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
