@@ -473,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
     int B, int H, int W, int64_t F, int D, const T *__restrict__ grad,
     const int64_t *__restrict__ face_idx, const T *__restrict__ weights,
     const T *__restrict__ fvi, const T *__restrict__ feat, float eps, T *grad_fvi,
-    T *grad_feat) {
+    T *grad_feat, int dbg) {
   constexpr int SMAX = 6 + 3 * DMAX;
   constexpr int HT = kBlock;  // slots >= distinct faces of a tile
   __shared__ int s_key[HT];
@@ -552,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
     const int o = s_off[slot];
     T v = (T)0;
     for (int r = 0; r < n; ++r) v += s_con[s_ord[o + r]][j];
-    if (v == (T)0) continue;
+    if (v == (T)0 || (dbg & 128)) continue;
     const int64_t row = (int64_t)b * F + s_key[slot];
     if (j < 6)
       atomicAdd(grad_fvi + row * 6 + j, v);
@@ -621,11 +621,13 @@ int raster_backward_launch(int B, int H, int W, int64_t F, int D, const T *grad,
     if (D <= 4) {
       ProfScope prof(K_RASTER_BWD_TILE, stream);
       hipLaunchKernelGGL((kd_raster_bwd_tile<T, 4>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
-                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat);
+                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
+                         debug_flags());
     } else if (D <= 8) {
       ProfScope prof(K_RASTER_BWD_TILE, stream);
       hipLaunchKernelGGL((kd_raster_bwd_tile<T, 8>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
-                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat);
+                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
+                         debug_flags());
     } else {
       const int64_t blocks = (total + kBlock - 1) / kBlock;
       ProfScope prof(K_RASTER_BWD_ATOMIC, stream);

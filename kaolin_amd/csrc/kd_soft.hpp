@@ -7,6 +7,8 @@
 #include "kd_capi.hpp"
 #include "kd_tile.hpp"
 
+#include <type_traits>
+
 namespace kd {
 
 #define KD_SOFT_EPS 1e-7  // dibr_soft_mask_cuda.cu:23 (a double literal)
