@@ -461,13 +461,13 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_atomic(
   }
 }
 
-// One workgroup per 16x16 tile.  Every pixel writes its terms to LDS; pixels are grouped by face
-// without any contended atomics: an LDS hash table gives each face a slot, a 256-bit pixel mask
-// per slot gives each pixel its rank among the slot's pixels (popcount), a prefix sum over the
-// slots turns (slot, rank) into a position, and the tile sum of each (face, term) is then
-// added in ascending pixel order by one lane -- deterministic within the tile -- and flushed with
-// one float atomic per (tile, face, term), a face's terms on adjacent lanes (its 6 corner terms
-// and its 3*D feature terms are contiguous in memory).
+// One workgroup per 16x16 tile.  Every pixel writes its terms to LDS; pixels are grouped by face:
+// an LDS hash table gives each face a slot, the slot's LDS counter gives each pixel its rank
+// among the slot's pixels, a prefix sum over the slots turns (slot, rank) into a position, and
+// the tile sum of each (face, term) is then added by one lane and flushed with one float atomic
+// per (tile, face, term), a face's terms on adjacent lanes (its 6 corner terms and its 3*D
+// feature terms are contiguous in memory).  (Summation order varies with the LDS counters, as it
+// does across tiles with the float atomics.)
 template <typename T, int DMAX>
 __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
     int B, int H, int W, int64_t F, int D, const T *__restrict__ grad,
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   constexpr int SMAX = 6 + 3 * DMAX;
   constexpr int HT = kBlock;  // slots >= distinct faces of a tile
   __shared__ int s_key[HT];
-  __shared__ uint32_t s_mask[HT][8];
+  __shared__ int s_n[HT];  // pixels per slot (their ranks come from the counter)
   __shared__ T s_con[kBlock][SMAX + 1];
   __shared__ short s_off[HT];
   __shared__ unsigned char s_ord[kBlock];
@@ -490,10 +490,9 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   const int px = (blockIdx.x % ntx) * kTile + (tid & 15);
   const int py = (blockIdx.x / ntx) * kTile + (tid >> 4);
   s_key[tid] = -1;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) s_mask[tid][k] = 0u;
+  s_n[tid] = 0;
   __syncthreads();
-  int h = -1;
+  int h = -1, rank = 0;
   if (px < W && py < H) {
     const int64_t p = ((int64_t)b * H + py) * W + px;
     // the pixel's weights and incoming gradient do not depend on its face: issued with it
@@ -510,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
         u = (u + 1) & (HT - 1);
       }
       h = (int)u;
-      atomicOr(&s_mask[h][tid >> 5], 1u << (tid & 31));
+      rank = atomicAdd(&s_n[h], 1);
       const int64_t tf = (int64_t)b * F + f;
       T c[SMAX];
       raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, gd, feat + tf * 3 * D, D, eps, c);
@@ -525,9 +524,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   }
   __syncthreads();
   // slot sizes -> positions (prefix sum over slots), and the list of occupied slots
-  int sz = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) sz += __popc(s_mask[tid][k]);
+  const int sz = s_n[tid];
   int total;
   const int off = wg_exclusive_scan(sz, s_cnt, total);
   s_off[tid] = (short)off;
@@ -535,20 +532,13 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   const bool occ = sz > 0;
   const int pos = wg_compact(occ, s_cnt, nocc);
   if (occ) s_list[pos] = tid;
-  int rank = 0;
-  if (h >= 0) {
-    rank = __popc(s_mask[h][tid >> 5] & ((1u << (tid & 31)) - 1u));
-    for (int k = 0; k < (tid >> 5); ++k) rank += __popc(s_mask[h][k]);
-  }
   __syncthreads();
   if (h >= 0) s_ord[s_off[h] + rank] = (unsigned char)tid;
   __syncthreads();
   for (int idx = tid; idx < nocc * S; idx += kBlock) {
     const int i = idx / S, j = idx - i * S;
     const int slot = s_list[i];
-    int n = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) n += __popc(s_mask[slot][k]);
+    const int n = s_n[slot];
     const int o = s_off[slot];
     T v = (T)0;
     for (int r = 0; r < n; ++r) v += s_con[s_ord[o + r]][j];
@@ -618,7 +608,12 @@ int raster_backward_launch(int B, int H, int W, int64_t F, int D, const T *grad,
   const int64_t total = (int64_t)B * H * W;
   if (total > 0 && nf > 0) {
     const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    if (D <= 4) {
+    if (D <= 3) {  // 6 + 3 D <= 15 terms: 16 KB of LDS terms, 8 workgroups per CU
+      ProfScope prof(K_RASTER_BWD_TILE, stream);
+      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 3>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
+                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
+                         debug_flags());
+    } else if (D <= 4) {
       ProfScope prof(K_RASTER_BWD_TILE, stream);
       hipLaunchKernelGGL((kd_raster_bwd_tile<T, 4>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
                          H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
