@@ -44,7 +44,7 @@ SOUP_CONFIGS = {
 }
 
 
-def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4):
+def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4, fused=True):
     """Bytes each kernel must move at minimum per launch: every tensor of its contract read or
     written once (SURVEY.md §8(d) decomposed per kernel).  P pixels, F faces
     (all views), Fv valid (front) faces, D features, K knum, pairs = (pixel, close face) pairs of
@@ -66,6 +66,9 @@ def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4):
         return F * (9 + 6) * e + V * 3 * e
     if pairs is None:
         return None
+    if kernel == 'kd_soft_pairs' and fused:  # whole soft mask: face_idx + corners in; records,
+        # coefficients, types, counts, soft out
+        return P * (8 + 4 + e) + F * 6 * e + pairs * (12 + 4 * e + 1)
     if kernel == 'kd_soft_pairs':      # face_idx in; records, counts, soft out
         return P * (8 + 4 + e) + pairs * 12
     if kernel == 'kd_soft_pair_math':  # records in; probabilities, types, coefficients out
@@ -223,10 +226,12 @@ def main():
             pairs = int(_lib.load().kd_dibr_pair_count(ws.data_ptr(), Bl, H, W, F, args.knum, 0,
                                                        torch.cuda.current_stream(dev).cuda_stream))
             del ws
+    fused = 'kd_soft_pair_math' not in prof  # the one-launch soft mask (kd_softpair.hip)
     kernels = {}
     for name, (ms, n) in prof.items():
         avg_us = ms * 1e3 / n
-        ab = algorithmic_bytes(name, P, Ftot, Fv, D, args.knum, args.lists, pairs, V)
+        ab = algorithmic_bytes(name, P, Ftot, Fv, D, args.knum, args.lists, pairs, V,
+                               fused=fused)
         kernels[name] = {'avg_us': round(avg_us, 2), 'launches': n,
                          'share': round(ms / max(sum(v[0] for v in prof.values()), 1e-9), 3)}
         if ab is not None:
@@ -237,7 +242,8 @@ def main():
     if dom is not None:
         ms, n = prof[dom]
         avg_s = ms / n / 1e3
-        ab = algorithmic_bytes(dom, P, Ftot, Fv, D, args.knum, args.lists, pairs, V)
+        ab = algorithmic_bytes(dom, P, Ftot, Fv, D, args.knum, args.lists, pairs, V,
+                               fused=fused)
         achieved = ab / avg_s / 1e9 if ab else None
         traffic = None
         if os.path.exists(args.pmc):

@@ -12,6 +12,10 @@ SLOT = {
     'kd::kd_raster_fwd_pairs': 'kd_raster_fwd', 'kd::kd_raster_fwd<float>': 'kd_raster_fwd',
     'kd::kd_soft_fwd<float, false>': 'kd_soft_fwd', 'kd::kd_soft_fwd<float, true>': 'kd_soft_fwd',
     'kd::kd_soft_pairs<float>': 'kd_soft_pairs',
+    'kd::kd_soft_pairs<float, true, 6>': 'kd_soft_pairs',
+    'kd::kd_soft_pairs<float, false, 8>': 'kd_soft_pairs',
+    'kd::kd_soft_bwd_items<float, 1>': 'kd_soft_bwd_pairs',
+    'kd::kd_raster_bwd_tile<float, 3>': 'kd_raster_bwd_tile',
     'kd::kd_soft_pair_math<float, true, false>': 'kd_soft_pair_math',
     'kd::kd_soft_reduce<float>': 'kd_soft_reduce',
     'kd::kd_soft_bwd_pairs<float>': 'kd_soft_bwd_pairs',
