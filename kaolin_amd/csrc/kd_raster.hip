@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   int b, tl, nbin;
-  tile_of_block(a.bb, H, W, b, tl, nbin);
+  tile_of_block(a.bb, H, W, b, tl, nbin, fs.dbg);
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   TileGeom t = tile_geom(H, W, tl);
@@ -190,7 +190,7 @@ __global__ __launch_bounds__(kBlock, 6) void kd_raster_fwd_pairs(RasterFwdArgs<f
   const float M = fs.M;
   if (a.fs.dbg & 16384) return;  // diagnostics: dispatch cost only
   int b, tl, nbin;
-  tile_of_block(a.bb, H, W, b, tl, nbin);
+  tile_of_block(a.bb, H, W, b, tl, nbin, fs.dbg);
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
   const int H = fs.H, W = fs.W, K = a.K;
   if (fs.dbg & 16384) return;  // diagnostics: dispatch cost only
   int b, tl, nbin;
-  tile_of_block(a.bb, H, W, b, tl, nbin);
+  tile_of_block(a.bb, H, W, b, tl, nbin, fs.dbg);
   const int tid = threadIdx.x, w = tid >> 6;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);

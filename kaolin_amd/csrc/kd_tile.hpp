@@ -39,10 +39,16 @@ struct TileGeom {
 // (view, fine tile) of this workgroup: the bins' heaviest-first order (tile_order) when the
 // bins were built, else (blockIdx.y, blockIdx.x).
 __device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W, int &b,
-                                              int &tile, int &nbin) {
+                                              int &tile, int &nbin, int dbg = 0) {
   if (bb.order && bb.nchunk > 0) {
     const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    const int2 v = bb.order[blockIdx.y * gridDim.x + blockIdx.x];
+    const int n = gridDim.x * gridDim.y;
+    int d = blockIdx.y * gridDim.x + blockIdx.x;
+    // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (d % 8), and the order holds a
+    // coarse tile's fine tiles consecutively; within each group of 32 workgroups fine tile j of
+    // coarse tile g runs at d = 8 j + g, so the tiles sharing a coarse bin share one L2.
+    if ((d | 31) < n && !(dbg & (1 << 17))) d = (d & ~31) | ((d & 7) << 2) | ((d >> 3) & 3);
+    const int2 v = bb.order[d];
     b = v.x / ntiles;
     tile = v.x - b * ntiles;
     nbin = v.y;
