@@ -485,10 +485,15 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   __shared__ int s_cnt[4];
   const int S = 6 + 3 * D;
   const int tid = threadIdx.x;
-  const int b = blockIdx.y;
   const int ntx = (W + kTile - 1) / kTile;
-  const int px = (blockIdx.x % ntx) * kTile + (tid & 15);
-  const int py = (blockIdx.x / ntx) * kTile + (tid >> 4);
+  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so XCD x gets the contiguous
+  // band of tiles [x n/8, (x+1) n/8): neighbouring tiles (which share faces) share one L2
+  const int n = gridDim.x * gridDim.y;
+  int d = blockIdx.y * gridDim.x + blockIdx.x;
+  if ((n & 7) == 0 && !(dbg & (1 << 17))) d = (d & 7) * (n >> 3) + (d >> 3);
+  const int b = d / gridDim.x, tl = d - b * gridDim.x;
+  const int px = (tl % ntx) * kTile + (tid & 15);
+  const int py = (tl / ntx) * kTile + (tid >> 4);
   s_key[tid] = -1;
   s_n[tid] = 0;
   __syncthreads();
