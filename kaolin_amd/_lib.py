@@ -105,6 +105,9 @@ def load():
             lib.kd_debug_buffer.restype = c_int
             lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
             lib.kd_prepare_vertices_ranges.restype = c_i64
+            # diagnostics only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
+            if os.environ.get('KD_DEBUG_FLAGS'):
+                lib.kd_debug_set(int(os.environ['KD_DEBUG_FLAGS'], 0))
             for base, sig in _SIGS.items():
                 for sfx in ('f32', 'f64'):
                     fn = getattr(lib, f'{base}_{sfx}')
