@@ -37,6 +37,12 @@ struct TileClock {
   __device__ ~TileClock() {
     if (buf && threadIdx.x == 0) buf[idx] = wall_clock64() - t0;
   }
+  // diagnostics: also the start time, in `slot` (dispatch slot order)
+  __device__ void start_to(int slot) const {
+    if (buf && threadIdx.x == 0)
+      buf[(int64_t)slot * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
+          t0;
+  }
 };
 
 constexpr int kWave = 64;

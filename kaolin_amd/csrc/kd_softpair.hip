@@ -204,6 +204,7 @@ template <typename T, bool FUSED, int OCC = 8>
 __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
   __shared__ unsigned short s_ridx[FUSED ? kFuseSlots : 1][kBlock];
   TileClock clk(a.fs.tbuf, 1);
+  clk.start_to(2);
   __shared__ TileLists L;
   __shared__ uint64_t s_pm[4][kWave];
   __shared__ unsigned short s_off[4][kWave];

@@ -1,0 +1,44 @@
+"""Dispatch-slot timeline of the fused soft-mask kernel (kd_debug_set flag 64): when do the
+heavy tiles start and end?  python tools/soft_timeline.py [config]"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from kaolin_amd import _lib, workloads  # noqa: E402
+from kaolin_amd.render.mesh import dibr_rasterization  # noqa: E402
+
+cfg = sys.argv[1] if len(sys.argv) > 1 else 'c3'
+n_lon, n_lat, H, W, B, elev = bench.CONFIGS[cfg]
+dev = torch.device('cuda')
+v = workloads.sphere_views(n_lon, n_lat, H, W, B, dev, elevation=elev)
+fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['normals_z']
+ntx, nty = (W + 15) // 16, (H + 15) // 16
+n = B * ntx * nty
+buf = torch.zeros(3 * n, dtype=torch.int64, device=dev)
+lib = _lib.load()
+lib.kd_debug_buffer(buf.data_ptr())
+for _ in range(3):
+    dibr_rasterization(H, W, fvz, fvi, feats, nz)
+torch.cuda.synchronize()
+lib.kd_debug_set(64)
+dibr_rasterization(H, W, fvz, fvi, feats, nz)
+torch.cuda.synchronize()
+lib.kd_debug_set(0)
+lib.kd_debug_buffer(None)
+t = buf.view(3, n).cpu().numpy()
+dur = t[1] / 100.0          # us (100 MHz wall clock)
+start = (t[2] - t[2].min()) / 100.0
+end = start + dur
+print(f'kernel span {end.max():.1f} us, tiles {n}, sum {dur.sum() / 1e3:.2f} ms')
+for q in range(10):
+    sl = slice(q * n // 10, (q + 1) * n // 10)
+    print(f'  slots {sl.start:5d}-{sl.stop:5d}: mean dur {dur[sl].mean():6.1f}  max dur '
+          f'{dur[sl].max():6.1f}  start [{start[sl].min():6.1f}, {start[sl].max():6.1f}]  '
+          f'max end {end[sl].max():6.1f}')
+late = np.argsort(end)[::-1][:10]
+print('latest ending (slot, start, dur):', [(int(i), round(float(start[i]), 1),
+                                            round(float(dur[i]), 1)) for i in late])
