@@ -45,6 +45,9 @@ def allreduce_grads_(tensors, group=None):
     tensors = [t for t in tensors if t is not None]
     if not tensors or not dist.is_initialized() or dist.get_world_size(group) == 1:
         return tensors
+    if len(tensors) == 1 and tensors[0].is_contiguous():  # in place: no pack / unpack kernels
+        dist.all_reduce(tensors[0], op=dist.ReduceOp.SUM, group=group)
+        return tensors
     flat = torch.cat([t.reshape(-1) for t in tensors])
     dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=group)
     off = 0
