@@ -39,41 +39,67 @@ __device__ __forceinline__ void cam_point(const T *tf, const T *p, T c[3]) {
   for (int j = 0; j < 3; ++j) c[j] = p[0] * tf[j] + p[1] * tf[3 + j] + p[2] * tf[6 + j] + tf[9 + j];
 }
 
+// Copies n elements of T from LDS to global memory with the workgroup, 16-byte vectors when
+// both sides allow (the rows of a workgroup are contiguous in every output).
+template <typename T>
+__device__ __forceinline__ void lds_to_global(T *dst, const T *src, int n) {
+  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0 && (n * sizeof(T)) % 16 == 0) {
+    const int nv = n * (int)sizeof(T) / 16;
+    for (int k = threadIdx.x; k < nv; k += kBlock)
+      reinterpret_cast<float4 *>(dst)[k] = reinterpret_cast<const float4 *>(src)[k];
+  } else {
+    for (int k = threadIdx.x; k < n; k += kBlock) dst[k] = src[k];
+  }
+}
+
+// One thread per (view, face) row; the rows' outputs (9 + 6 + 3 values each) are assembled in
+// LDS and written by the workgroup as contiguous, coalesced runs.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_prepare_fwd(PrepArgs<T> a, T *fvc, T *fvi, T *nrm) {
+  __shared__ __align__(16) T s_c[kBlock * 9];
+  __shared__ __align__(16) T s_i[kBlock * 6];
+  __shared__ __align__(16) T s_n[kBlock * 3];
   const int64_t total = (int64_t)a.B * a.F;
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * kBlock) {
-    const int b = (int)(i / a.F);
-    const int64_t f = i - (int64_t)b * a.F;
-    const T *vb = a.vertices + (a.Bv == 1 ? 0 : (int64_t)b * a.V * 3);
-    const T *tf = a.tf + (int64_t)b * 12;
-    T c[3][3];
+  for (int64_t i0 = (int64_t)blockIdx.x * kBlock; i0 < total; i0 += (int64_t)gridDim.x * kBlock) {
+    const int64_t i = i0 + threadIdx.x;
+    const int rows = (int)min((int64_t)kBlock, total - i0);
+    if (i < total) {
+      const int b = (int)(i / a.F);
+      const int64_t f = i - (int64_t)b * a.F;
+      const T *vb = a.vertices + (a.Bv == 1 ? 0 : (int64_t)b * a.V * 3);
+      const T *tf = a.tf + (int64_t)b * 12;
+      T c[3][3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const int64_t v = a.faces[f * 3 + k];
-      cam_point<T>(tf, vb + v * 3, c[k]);
-    }
-    T *oc = fvc + i * 9;
-    T *oi = fvi + i * 6;
+      for (int k = 0; k < 3; ++k) {
+        const int64_t v = a.faces[f * 3 + k];
+        cam_point<T>(tf, vb + v * 3, c[k]);
+      }
+      T *oc = s_c + threadIdx.x * 9;
+      T *oi = s_i + threadIdx.x * 6;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      oc[k * 3 + 0] = c[k][0];
-      oc[k * 3 + 1] = c[k][1];
-      oc[k * 3 + 2] = c[k][2];
-      const T pz = c[k][2] * a.proj[2];
-      oi[k * 2 + 0] = c[k][0] * a.proj[0] / pz;
-      oi[k * 2 + 1] = c[k][1] * a.proj[1] / pz;
+      for (int k = 0; k < 3; ++k) {
+        oc[k * 3 + 0] = c[k][0];
+        oc[k * 3 + 1] = c[k][1];
+        oc[k * 3 + 2] = c[k][2];
+        const T pz = c[k][2] * a.proj[2];
+        oi[k * 2 + 0] = c[k][0] * a.proj[0] / pz;
+        oi[k * 2 + 1] = c[k][1] * a.proj[1] / pz;
+      }
+      const T e1[3] = {c[1][0] - c[0][0], c[1][1] - c[0][1], c[1][2] - c[0][2]};
+      const T e2[3] = {c[2][0] - c[0][0], c[2][1] - c[0][1], c[2][2] - c[0][2]};
+      const T n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                      e1[0] * e2[1] - e1[1] * e2[0]};
+      const T len = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]) + (T)1e-10;
+      T *on = s_n + threadIdx.x * 3;
+      on[0] = n[0] / len;
+      on[1] = n[1] / len;
+      on[2] = n[2] / len;
     }
-    const T e1[3] = {c[1][0] - c[0][0], c[1][1] - c[0][1], c[1][2] - c[0][2]};
-    const T e2[3] = {c[2][0] - c[0][0], c[2][1] - c[0][1], c[2][2] - c[0][2]};
-    const T n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
-                    e1[0] * e2[1] - e1[1] * e2[0]};
-    const T len = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]) + (T)1e-10;
-    T *on = nrm + i * 3;
-    on[0] = n[0] / len;
-    on[1] = n[1] / len;
-    on[2] = n[2] / len;
+    __syncthreads();
+    lds_to_global<T>(fvc + i0 * 9, s_c, rows * 9);
+    lds_to_global<T>(fvi + i0 * 6, s_i, rows * 6);
+    lds_to_global<T>(nrm + i0 * 3, s_n, rows * 3);
+    __syncthreads();
   }
 }
 
