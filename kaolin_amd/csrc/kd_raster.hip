@@ -480,7 +480,6 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   __shared__ int s_n[HT];  // pixels per slot (their ranks come from the counter)
   __shared__ T s_con[kBlock][SMAX + 1];
   __shared__ short s_off[HT];
-  __shared__ unsigned char s_ord[kBlock];
   __shared__ int s_list[HT];
   __shared__ int s_cnt[4];
   const int S = 6 + 3 * D;
@@ -498,6 +497,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   s_n[tid] = 0;
   __syncthreads();
   int h = -1, rank = 0;
+  T c[SMAX];
   if (px < W && py < H) {
     const int64_t p = ((int64_t)b * H + py) * W + px;
     // the pixel's weights and incoming gradient do not depend on its face: issued with it
@@ -516,15 +516,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
       h = (int)u;
       rank = atomicAdd(&s_n[h], 1);
       const int64_t tf = (int64_t)b * F + f;
-      T c[SMAX];
       raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, gd, feat + tf * 3 * D, D, eps, c);
-#pragma unroll
-      for (int j = 0; j < 6; ++j) s_con[tid][j] = c[j];
-#pragma unroll
-      for (int ii = 0; ii < 3; ++ii)
-#pragma unroll
-        for (int d = 0; d < DMAX; ++d)
-          if (d < D) s_con[tid][6 + ii * D + d] = c[6 + ii * DMAX + d];
     }
   }
   __syncthreads();
@@ -538,7 +530,17 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
   const int pos = wg_compact(occ, s_cnt, nocc);
   if (occ) s_list[pos] = tid;
   __syncthreads();
-  if (h >= 0) s_ord[s_off[h] + rank] = (unsigned char)tid;
+  // the pixel's terms go to its position in slot order, so a slot's terms are contiguous rows
+  if (h >= 0) {
+    const int ps = s_off[h] + rank;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s_con[ps][j] = c[j];
+#pragma unroll
+    for (int ii = 0; ii < 3; ++ii)
+#pragma unroll
+      for (int d = 0; d < DMAX; ++d)
+        if (d < D) s_con[ps][6 + ii * D + d] = c[6 + ii * DMAX + d];
+  }
   __syncthreads();
   for (int idx = tid; idx < nocc * S; idx += kBlock) {
     const int i = idx / S, j = idx - i * S;
@@ -546,7 +548,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
     const int n = s_n[slot];
     const int o = s_off[slot];
     T v = (T)0;
-    for (int r = 0; r < n; ++r) v += s_con[s_ord[o + r]][j];
+    for (int r = 0; r < n; ++r) v += s_con[o + r][j];  // independent reads: pipelined
     if (v == (T)0 || (dbg & 128)) continue;
     const int64_t row = (int64_t)b * F + s_key[slot];
     if (j < 6)
