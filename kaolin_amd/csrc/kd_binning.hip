@@ -133,36 +133,39 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   if (bb.clear && b == 0 && chunk == 0 && tid < bb.n_clear) bb.clear[tid] = 0;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const int64_t i = lo + (int64_t)chunk * kChunk + tid;
   __syncthreads();
-  if (i < hi) {
-    Span s;
-    const bool ok = (!fs.valid || fs.valid[i]) && (!fs.nz || fs.nz[i * fs.nz_stride] >= (T)0);
-    if (ok) {
-      T v[6], box[4];
-      load_corners(fs, i, v);
-      face_box(fs, i, v, box);
-      s = make_span<T>(box[0], box[1], box[2], box[3], fs.M, fs.H, fs.W);
-      if constexpr (std::is_same<T, float>::value) {
-        if (bb.cull && !span_empty(s)) {
-          float cc[8];
-          raster_cull_coefs(v, fs.M, fs.H, fs.W, s, bb.cull_eps, cc);
-          bb.cull[2 * i] = make_float4(cc[0], cc[1], cc[2], cc[3]);
-          bb.cull[2 * i + 1] = make_float4(cc[4], cc[5], cc[6], cc[7]);
+#pragma unroll
+  for (int u = 0; u < kChunk / kBlock; ++u) {
+    const int64_t i = lo + (int64_t)chunk * kChunk + u * kBlock + tid;
+    if (i < hi) {
+      Span s;
+      const bool ok = (!fs.valid || fs.valid[i]) && (!fs.nz || fs.nz[i * fs.nz_stride] >= (T)0);
+      if (ok) {
+        T v[6], box[4];
+        load_corners(fs, i, v);
+        face_box(fs, i, v, box);
+        s = make_span<T>(box[0], box[1], box[2], box[3], fs.M, fs.H, fs.W);
+        if constexpr (std::is_same<T, float>::value) {
+          if (bb.cull && !span_empty(s)) {
+            float cc[8];
+            raster_cull_coefs(v, fs.M, fs.H, fs.W, s, bb.cull_eps, cc);
+            bb.cull[2 * i] = make_float4(cc[0], cc[1], cc[2], cc[3]);
+            bb.cull[2 * i + 1] = make_float4(cc[4], cc[5], cc[6], cc[7]);
+          }
         }
+      } else {
+        s.x0 = 1;
+        s.x1 = 0;
+        s.y0 = 1;
+        s.y1 = 0;
       }
-    } else {
-      s.x0 = 1;
-      s.x1 = 0;
-      s.y0 = 1;
-      s.y1 = 0;
-    }
-    bb.spans[i] = s;
-    if (!span_empty(s)) {
-      const int cx0 = s.x0 / bb.g.ct, cx1 = s.x1 / bb.g.ct;
-      const int cy0 = s.y0 / bb.g.ct, cy1 = s.y1 / bb.g.ct;
-      for (int cy = cy0; cy <= cy1; ++cy)
-        for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&s_cnt[cy * bb.g.nctx + cx], 1);
+      bb.spans[i] = s;
+      if (!span_empty(s)) {
+        const int cx0 = s.x0 / bb.g.ct, cx1 = s.x1 / bb.g.ct;
+        const int cy0 = s.y0 / bb.g.ct, cy1 = s.y1 / bb.g.ct;
+        for (int cy = cy0; cy <= cy1; ++cy)
+          for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&s_cnt[cy * bb.g.nctx + cx], 1);
+      }
     }
   }
   __syncthreads();
@@ -233,45 +236,51 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
       tile_order(bb, fs.B, (fs.W + kTile - 1) / kTile, (fs.H + kTile - 1) / kTile);
     return;
   }
-  // 256-bit membership mask per coarse tile: bit t set <=> face (chunk*256 + t) touches it.
-  extern __shared__ uint32_t s_mask[];  // [nct][8]
+  // kChunk-bit membership mask per coarse tile: bit t set <=> face (chunk*kChunk + t) touches it;
+  // each thread holds faces tid and tid + 256.
+  constexpr int kWords = kChunk / 32, kPerT = kChunk / kBlock;
+  extern __shared__ uint32_t s_mask[];  // [nct][kWords]
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
-  for (int k = tid; k < nct * 8; k += kBlock) s_mask[k] = 0u;
+  for (int k = tid; k < nct * kWords; k += kBlock) s_mask[k] = 0u;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  const int64_t i = lo + (int64_t)chunk * kChunk + tid;
-  Span s;
-  s.x0 = 1;
-  s.x1 = 0;
-  s.y0 = 1;
-  s.y1 = 0;
-  if (i < hi) s = bb.spans[i];
-  const bool has = !span_empty(s);
-  int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
-  if (has) {
-    cx0 = s.x0 / bb.g.ct;
-    cx1 = s.x1 / bb.g.ct;
-    cy0 = s.y0 / bb.g.ct;
-    cy1 = s.y1 / bb.g.ct;
+  Span sp[kPerT];
+#pragma unroll
+  for (int u = 0; u < kPerT; ++u) {
+    const int64_t i = lo + (int64_t)chunk * kChunk + u * kBlock + tid;
+    sp[u] = Span{1, 0, 1, 0};
+    if (i < hi) sp[u] = bb.spans[i];
   }
   __syncthreads();
-  const uint32_t bit = 1u << (tid & 31);
-  const int word = tid >> 5;
-  for (int cy = cy0; cy <= cy1; ++cy)
-    for (int cx = cx0; cx <= cx1; ++cx) atomicOr(&s_mask[(cy * bb.g.nctx + cx) * 8 + word], bit);
+#pragma unroll
+  for (int u = 0; u < kPerT; ++u) {
+    if (span_empty(sp[u])) continue;
+    const int t = u * kBlock + tid;
+    const uint32_t bit = 1u << (t & 31);
+    const int word = t >> 5;
+    for (int cy = sp[u].y0 / bb.g.ct; cy <= sp[u].y1 / bb.g.ct; ++cy)
+      for (int cx = sp[u].x0 / bb.g.ct; cx <= sp[u].x1 / bb.g.ct; ++cx)
+        atomicOr(&s_mask[(cy * bb.g.nctx + cx) * kWords + word], bit);
+  }
   __syncthreads();
-  if (!has) return;
   const int *offs = bb.counts + ((int64_t)b * bb.nchunk + chunk) * nct;
-  const int local = (int)(i - lo);
-  for (int cy = cy0; cy <= cy1; ++cy)
-    for (int cx = cx0; cx <= cx1; ++cx) {
-      const int c = cy * bb.g.nctx + cx;
-      const uint32_t *m = s_mask + c * 8;
-      int rank = __popc(m[word] & (bit - 1u));
-      for (int k = 0; k < word; ++k) rank += __popc(m[k]);
-      bb.bins[(int64_t)c * fs.N + lo + offs[c] + rank] = local;
-    }
+#pragma unroll
+  for (int u = 0; u < kPerT; ++u) {
+    if (span_empty(sp[u])) continue;
+    const int t = u * kBlock + tid;
+    const uint32_t bit = 1u << (t & 31);
+    const int word = t >> 5;
+    const int local = chunk * kChunk + t;
+    for (int cy = sp[u].y0 / bb.g.ct; cy <= sp[u].y1 / bb.g.ct; ++cy)
+      for (int cx = sp[u].x0 / bb.g.ct; cx <= sp[u].x1 / bb.g.ct; ++cx) {
+        const int c = cy * bb.g.nctx + cx;
+        const uint32_t *m = s_mask + c * kWords;
+        int rank = __popc(m[word] & (bit - 1u));
+        for (int k = 0; k < word; ++k) rank += __popc(m[k]);
+        bb.bins[(int64_t)c * fs.N + lo + offs[c] + rank] = local;
+      }
+  }
 }
 
 // Dispatch order of the tile kernels: (view, fine tile) by descending bit length of its coarse
@@ -377,9 +386,18 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
                        jobs.bb[njobs - 1]);
   }
   {  // + one column of workgroups for the tile order (kd_bin_scatter, tile_order)
+    // kChunk-bit masks per coarse tile: up to 64 KB of dynamic LDS at 1024 coarse tiles (a
+    // gfx950 workgroup may hold up to 160 KB; past 64 KB it has to be asked for)
+    const size_t dyn = sizeof(uint32_t) * (kChunk / 32) * (size_t)bb.g.nct();
+    if (dyn > 48 * 1024) {
+      const hipError_t ea = hipFuncSetAttribute((const void *)kd_bin_scatter<T>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)dyn);
+      if (ea != hipSuccess) return ea;
+    }
     ProfScope prof(K_BIN_SCATTER, stream);
     hipLaunchKernelGGL(kd_bin_scatter<T>, dim3(bb.nchunk + 1, fs.B, njobs), dim3(kBlock),
-                       sizeof(uint32_t) * 8 * bb.g.nct(), stream, jobs);
+                       sizeof(uint32_t) * (kChunk / 32) * bb.g.nct(), stream, jobs);
   }
   return hipGetLastError();
 }

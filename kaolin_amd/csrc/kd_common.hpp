@@ -48,7 +48,7 @@ struct TileClock {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;      // 4 waves
 constexpr int kTile = 16;        // fine tile: 16x16 pixels per workgroup, 8x8 per wave
-constexpr int kChunk = 256;      // faces per binning workgroup
+constexpr int kChunk = 512;      // faces per binning workgroup (two per thread)
 constexpr int kMaxCtiles = 1024; // coarse tiles per view (LDS bound of the binning kernels)
 
 // ------------------------------------------------------------------------------------------
