@@ -67,16 +67,17 @@ def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4, f
     if pairs is None:
         return None
     if kernel == 'kd_soft_pairs' and fused:  # whole soft mask: face_idx + corners in; records,
-        # coefficients, types, counts, soft out
-        return P * (8 + 4 + e) + F * 6 * e + pairs * (12 + 4 * e + 1)
+        # probabilities, types, counts, soft out
+        return P * (8 + 4 + e) + F * 6 * e + pairs * (12 + e + 1)
     if kernel == 'kd_soft_pairs':      # face_idx in; records, counts, soft out
         return P * (8 + 4 + e) + pairs * 12
-    if kernel == 'kd_soft_pair_math':  # records in; probabilities, types, coefficients out
-        return pairs * (12 + e + 1 + 4 * e)
+    if kernel == 'kd_soft_pair_math':  # records in; probabilities, types out
+        return pairs * (12 + e + 1)
     if kernel == 'kd_soft_reduce':     # probabilities in, soft out
         return pairs * e
-    if kernel == 'kd_soft_bwd_pairs':  # records + coefficients, grad/soft in; face grads added
-        return pairs * (12 + 4 * e) + P * 2 * e + F * 6 * e * 2
+    if kernel == 'kd_soft_bwd_pairs':  # records + probabilities, grad/soft, corners in; face
+        # grads added
+        return pairs * (12 + e) + P * 2 * e + F * 6 * e * 3
     return None
 
 

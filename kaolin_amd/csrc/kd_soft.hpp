@@ -113,7 +113,6 @@ struct SoftArgs {
   // buffers the soft reduction zeroes on the side (the fused backward's gradients), nullable
   T *zero0, *zero1;
   int64_t nzero0, nzero1;
-  int want_coef;  // fused soft-mask kernel: store the backward's coefficients
 };
 
 // Per-wave pair list of the current batch and its per-pixel bookkeeping.
@@ -201,7 +200,6 @@ struct SoftCoef {
 template <typename T>
 struct SoftPairBuf {
   SoftPairRec *rec;   // [B * ntiles][cap]
-  SoftCoef<T> *coef;  // [B * ntiles][cap] backward coefficients
   T *sprob;           // [B * ntiles][cap] probability of each record
   int32_t *npix;      // [B * H * W] close faces of each uncovered pixel
   int32_t *ntile;     // [B * ntiles][2]: records, faces in the tile list

@@ -3,27 +3,26 @@
 // The reference's per-pixel loop (dibr_soft_mask_cuda.cu:27-184) spends its time in two places:
 // finding each uncovered pixel's first K close faces, and the distance / probability math of
 // those (pixel, face) pairs.  Only pixels near the silhouette have pairs (~8 % of the pixels,
-// ~16 pairs each at C3), so a tile kernel that also does the math is badly unbalanced: a
-// handful of silhouette tiles carry all of it.  Here the two parts are separate launches:
-//   kd_soft_pairs      one workgroup per 16x16 tile: walks the tile's ordered bin (kd_tile.hpp),
-//                      pass A (kd_soft.hpp) picks each uncovered pixel's first K close faces by
-//                      face index, and the (pixel, slot, face) records go to the tile's region.
-//                      It stops as soon as every uncovered pixel of the tile holds K faces.
-//   kd_soft_pair_math  flat over the records (several workgroups per tile): distance type and
-//                      probability with the reference arithmetic (bit-identical), stored by
-//                      (pixel, slot); with gradients requested also the pair's backward
-//                      coefficients (below); optionally the reference's close-face lists.
-//   kd_soft_reduce     per pixel: soft = 1 - prod(1 - p) in slot order with the reference's
-//                      double promotion (dibr_soft_mask_cuda.cu:174-181); 1 on covered pixels.
-//   kd_soft_bwd_pairs  the backward: per tile, every record adds s_p * h_j to its face's corner
-//                      sums in LDS, one float atomic per (tile, face, coordinate) flushes them.
+// ~16 pairs each at C3).
+//   kd_soft_pairs<FUSED>  one workgroup per 16x16 tile: walks the tile's ordered bin
+//                      (kd_tile.hpp); pass A picks each uncovered pixel's first K close faces by
+//                      face index and writes (pixel, slot, face) records to the tile's region,
+//                      stopping once every uncovered pixel holds K.  FUSED (knum <= 32, no close
+//                      lists): the same workgroup then does the pair math over its records
+//                      (distance type and probability, bit-identical to the reference) and the
+//                      ordered product soft = 1 - prod(1 - p) (dibr_soft_mask_cuda.cu:174-181,
+//                      double-promoted) -- the whole soft mask in one launch.
+//   kd_soft_pair_math, kd_soft_reduce   the same math and product as separate launches, for
+//                      the op form with the reference's close-face lists (and knum > 32).
+//   kd_soft_bwd_items  the backward, flat over (tile, 256-record) items.
 // Backward factorisation: the reference's per-pair gradient (dibr_soft_mask_cuda.cu:281-348) is
 //   dLdz * f_j / M  with  dLdz = -sigmainv * dLdp * (1 - soft) / (1 - p + 1e-7) * p
 // and f_j the geometric factors of the distance type (2(x1 - x0) ... for a vertex, the four
 // dzdA / dzdB / dzdC combinations for an edge).  Only s_p = -sigmainv * dLdp * (1 - soft)
-// depends on the incoming gradient, so the forward stores h_j = p / (1 - p + 1e-7) * f_j / M per
-// pair and the backward is a multiply-add per coordinate (same value up to rounding order, like
-// the reference's own atomics).  Nothing is recomputed and the close lists are never needed.
+// depends on the incoming gradient: the backward computes h_j = p / (1 - p + 1e-7) * f_j / M from
+// the record (face corners, distance type, the forward's probability) and adds s_p * h_j per
+// coordinate (same value up to rounding order, like the reference's own atomics).  The close
+// lists are never needed.
 #include "kd_soft.hpp"
 
 namespace kd {
@@ -38,7 +37,6 @@ size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int 
   const int64_t tiles = (int64_t)B * ntiles, cap = (int64_t)kBlock * K, P = (int64_t)B * H * W;
   size_t s = bin_workspace_bytes(B, H, W, N, F);
   s += align_up(sizeof(SoftPairRec) * (size_t)(tiles * cap));
-  s += align_up((size_t)esize * 4 * (size_t)(tiles * cap));
   s += align_up((size_t)esize * (size_t)(tiles * cap));
   s += align_up(sizeof(int32_t) * (size_t)P);
   s += align_up(sizeof(int32_t) * 2 * (size_t)tiles);
@@ -59,8 +57,6 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   char *base = (char *)ws;
   pb.rec = (SoftPairRec *)(base + off);
   off += align_up(sizeof(SoftPairRec) * (size_t)(tiles * pb.cap));
-  pb.coef = (SoftCoef<T> *)(base + off);
-  off += align_up(sizeof(T) * 4 * (size_t)(tiles * pb.cap));
   pb.sprob = (T *)(base + off);
   off += align_up(sizeof(T) * (size_t)(tiles * pb.cap));
   pb.npix = (int32_t *)(base + off);
@@ -334,11 +330,7 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
       soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
       sp[i] = prob;
       rec[i].type = (uint8_t)et;
-      if (a.want_coef) {  // gradients wanted: the backward's coefficients
-        SoftCoef<T> c;
-        soft_pair_coef<T>(x0, y0, v, et, prob, M, c.h);
-        pb.coef[tile * pb.cap + i] = c;
-      }
+      // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
     }
     __syncthreads();  // the workgroup's probabilities are visible to it
     // soft = 1 - prod(1 - p) in slot order (dibr_soft_mask_cuda.cu:174-181, double-promoted)
@@ -425,10 +417,9 @@ __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPair
 }
 
 // Flat over the (tile, 256-record chunk) items: each record's distance type and probability
-// (bit-identical to the reference), its backward coefficients (GRAD) and optionally the close
-// lists.  (Reducing a tile in the workgroup that finishes its last chunk needs a device-scope
+// (bit-identical to the reference) and optionally the close lists.  (Reducing a tile in the workgroup that finishes its last chunk needs a device-scope
 // release per item -- an L2 writeback on gfx950 -- and measured 30x slower than kd_soft_reduce.)
-template <typename T, bool GRAD, bool LISTS, int R>
+template <typename T, bool LISTS, int R>
 __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftPairBuf<T> pb) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
@@ -480,11 +471,6 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
         }
         if (a.last && r[u].slot == K - 1) a.last[gp] = (int32_t)((int64_t)r[u].row - lo);
       }
-      if (GRAD) {
-        SoftCoef<T> c;
-        soft_pair_coef<T>(x0, y0, v[u], et, prob, M, c.h);
-        pb.coef[tile * pb.cap + i] = c;
-      }
     }
   }
 }
@@ -502,89 +488,6 @@ __device__ __forceinline__ void soft_add_pair(T g[6], int et, double sp, const S
 #pragma unroll
   for (int i = 0; i < 6; ++i)
     g[i] += i == ps ? v0 : i == ps + 1 ? v1 : i == ps2 ? v2 : i == ps2 + 1 ? v3 : (T)0;
-}
-
-// The records of a tile are face-major runs (kd_soft_pairs), so a thread walking U consecutive
-// records sums most of them in registers and touches LDS once per run.
-template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_soft_bwd_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
-  constexpr int R = 1024 * 4 / sizeof(T);  // faces per LDS pass
-  constexpr int U = 8;                     // consecutive records per thread
-  __shared__ T s_acc[6][R];
-  __shared__ int s_row[R];
-  __shared__ double s_sp[kBlock];  // -sigmainv * grad * (1 - soft) of the tile's pixels
-  const int ntl = pb.counters[1];
-  for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) {  // tiles with records
-  const int64_t tile = pb.tiles[ti];
-  const int n = pb.ntile[2 * tile], nf = pb.ntile[2 * tile + 1];
-  const FaceSet<T> &fs = a.fs;
-  const int H = fs.H, W = fs.W;
-  const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-  const int tx = tl % pb.ntx, ty = tl / pb.ntx;
-  const int tid = threadIdx.x;
-  __syncthreads();  // the previous tile's LDS is done
-  {
-    int px, py;
-    tile_pixel(tx, ty, tid, px, py);
-    double sp = 0.0;
-    if (px < W && py < H) {
-      const int64_t gp = ((int64_t)b * H + py) * W + px;
-      sp = -(double)a.sigmainv * (double)a.grad_soft[gp] * (1.0 - (double)a.soft_in[gp]);
-    }
-    s_sp[tid] = sp;
-  }
-  const SoftPairRec *rec = pb.rec + tile * pb.cap;
-  const SoftCoef<T> *coef = pb.coef + tile * pb.cap;
-  for (int r0 = 0; r0 < nf; r0 += R) {
-    const int nr = min(R, nf - r0);
-    for (int k = tid; k < nr; k += kBlock) {
-#pragma unroll
-      for (int c = 0; c < 6; ++c) s_acc[c][k] = (T)0;
-      s_row[k] = -1;
-    }
-    __syncthreads();
-    auto flush_run = [&](int li, const T g[6]) {
-#pragma unroll
-      for (int c = 0; c < 6; ++c)
-        if (g[c] != (T)0) atomicAdd(&s_acc[c][li], g[c]);
-    };
-    for (int s0 = tid * U; s0 < n && !(fs.dbg & 256); s0 += kBlock * U) {
-      SoftPairRec r[U];
-      SoftCoef<T> c[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)  // issue all loads first
-        if (s0 + u < n) {
-          r[u] = rec[s0 + u];
-          c[u] = coef[s0 + u];
-        }
-      T g[6] = {0, 0, 0, 0, 0, 0};
-      int cur = -1;
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (s0 + u >= n) break;
-        const int li = (int)r[u].lid - r0;
-        if (li < 0 || li >= nr) continue;
-        if (li != cur) {
-          if (cur >= 0) flush_run(cur, g);
-#pragma unroll
-          for (int q = 0; q < 6; ++q) g[q] = (T)0;
-          cur = li;
-          s_row[li] = r[u].row;
-        }
-        soft_add_pair<T>(g, r[u].type, s_sp[r[u].q], c[u]);
-      }
-      if (cur >= 0) flush_run(cur, g);
-    }
-    __syncthreads();
-    // one atomic per (face, coordinate); a face's 6 coordinates on adjacent lanes (24 B)
-    for (int idx = tid; idx < nr * 6 && !(fs.dbg & 128); idx += kBlock) {
-      const int k = idx / 6, cc = idx - k * 6;
-      const T v = s_acc[cc][k];
-      if (v != (T)0 && s_row[k] >= 0) atomicAdd(a.grad_fvi + (int64_t)s_row[k] * 6 + cc, v);
-    }
-    __syncthreads();
-  }
-  }
 }
 
 // Flat over the (tile, 256-record chunk) items, one record per thread: s_p * h_j expanded to
@@ -620,14 +523,17 @@ __device__ __forceinline__ void seg_scan_shfl(int seg, int lane, T g[6]) {
   }
 }
 
+// The coefficients are recomputed here from the record's face corners, distance type and forward
+// probability (soft_pair_coef): the forward's critical path skips them, and this kernel, bound by
+// its load chains and atomics, absorbs the arithmetic (measured free).
 template <typename T, int R>
 __global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftPairBuf<T> pb) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const int lane = threadIdx.x & (kWave - 1);
   const int nitems = pb.counters[0];
-  // R items per workgroup pass; their load chains (item -> record and coefficients -> the
-  // pixel's gradient and soft value) are issued together
+  // R items per workgroup pass; their load chains (item -> record -> the pixel's gradient and
+  // soft value, the face's corners) are issued together
   for (int it0 = blockIdx.x * R; it0 < nitems; it0 += gridDim.x * R) {
     int2 item[R];
     bool ok[R];
@@ -645,7 +551,6 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftP
         const int64_t ri =
             (int64_t)item[u].x * pb.cap + (item[u].y & 0xffff) * kBlock + threadIdx.x;
         r[u] = pb.rec[ri];
-        c[u] = pb.coef[ri];
       }
 #pragma unroll
     for (int u = 0; u < R; ++u)
@@ -657,6 +562,13 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftP
         const int64_t gp = ((int64_t)b * H + py) * W + px;
         gs[u] = a.grad_soft[gp];
         so[u] = a.soft_in[gp];
+        const int64_t ri =
+            (int64_t)item[u].x * pb.cap + (item[u].y & 0xffff) * kBlock + threadIdx.x;
+        T v[6];
+        load_corners(fs, (int64_t)r[u].row, v);
+        const float M = fs.M;
+        soft_pair_coef<T>((T)px_cx(M, W, px), (T)px_cy(M, H, py), v, r[u].type, pb.sprob[ri], M,
+                          c[u].h);
       }
 #pragma unroll
     for (int u = 0; u < R; ++u) {
@@ -707,7 +619,6 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   const bool fused =
       reduce && a.soft && !a.prob && !a.last && a.K <= kFuseSlots && !(a.fs.dbg & 4096);
   if (fused) {
-    a.want_coef = grad ? 1 : 0;
     ProfScope prof(K_SOFT_PAIRS, stream);
     // 6 workgroups per CU (the 16 KB record-index table); 4 and 8 measured no faster
     hipLaunchKernelGGL((kd_soft_pairs<T, true, 6>), dim3((unsigned)pb.ntiles, fs.B),
@@ -725,18 +636,12 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
     ProfScope prof(K_SOFT_MATH, stream);
     const bool lists = a.prob != nullptr;
     const dim3 grid(kMathBlocks);
-#define KD_MATH_LAUNCH(G, L)                                                                  \
-  hipLaunchKernelGGL((kd_soft_pair_math<T, G, L, kMathItems>), grid, dim3(kBlock), 0, stream, a, \
-                     pb)
-    if (grad && lists)
-      KD_MATH_LAUNCH(true, true);
-    else if (grad)
-      KD_MATH_LAUNCH(true, false);
-    else if (lists)
-      KD_MATH_LAUNCH(false, true);
+    if (lists)
+      hipLaunchKernelGGL((kd_soft_pair_math<T, true, kMathItems>), grid, dim3(kBlock), 0, stream,
+                         a, pb);
     else
-      KD_MATH_LAUNCH(false, false);
-#undef KD_MATH_LAUNCH
+      hipLaunchKernelGGL((kd_soft_pair_math<T, false, kMathItems>), grid, dim3(kBlock), 0,
+                         stream, a, pb);
   }
   if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
@@ -773,15 +678,8 @@ int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t s
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_SOFT_BWD_PAIRS, stream);
-    if (a.fs.dbg & 4096)  // the per-tile LDS form, for A/B runs
-      hipLaunchKernelGGL(kd_soft_bwd_pairs<T>, dim3(kPersistentBlocks), dim3(kBlock), 0, stream,
-                         a, pb);
-    else if (a.fs.dbg & 256)  // four items per pass (measured slower), for A/B runs
-      hipLaunchKernelGGL((kd_soft_bwd_items<T, 4>), dim3(kPersistentBlocks), dim3(kBlock), 0,
-                         stream, a, pb);
-    else
-      hipLaunchKernelGGL((kd_soft_bwd_items<T, 1>), dim3(kMathBlocks), dim3(kBlock), 0, stream,
-                         a, pb);
+    hipLaunchKernelGGL((kd_soft_bwd_items<T, 1>), dim3(kMathBlocks), dim3(kBlock), 0, stream, a,
+                       pb);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
