@@ -216,6 +216,9 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
   view_range(fs, b, lo, hi);
   TileGeom t = tile_geom(H, W, tl);
   t.nbin = nbin;
+  if (fs.tbuf && tid == 0)  // diagnostics: (view, tile, coarse count) of this dispatch slot
+    fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
+        ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const bool unc = t.inimg && a.face_idx[p] < 0;
   const bool wave_unc = __ballot(unc) != 0ull;

@@ -39,6 +39,18 @@ for q in range(10):
     print(f'  slots {sl.start:5d}-{sl.stop:5d}: mean dur {dur[sl].mean():6.1f}  max dur '
           f'{dur[sl].max():6.1f}  start [{start[sl].min():6.1f}, {start[sl].max():6.1f}]  '
           f'max end {end[sl].max():6.1f}')
+tile = t[0] & 0xffffffff
+nbin = t[0] >> 32
+_, _, fidx = dibr_rasterization(H, W, fvz, fvi, feats, nz)
+unc = (fidx < 0).reshape(B, nty, 16, ntx, 16).sum(dim=(2, 4)).reshape(-1).cpu().numpy()
+u_slot = unc[tile]
+print('slot deciles: mean uncovered px / mean coarse count (soft bins)')
+for q in range(10):
+    sl = slice(q * n // 10, (q + 1) * n // 10)
+    heavy = dur[sl] > 30
+    print(f'  {sl.start:5d}: unc {u_slot[sl].mean():6.1f}  nbin {nbin[sl].mean():7.1f}  heavy '
+          f'{heavy.sum():4d}  heavy unc {u_slot[sl][heavy].mean() if heavy.any() else 0:6.1f} '
+          f'heavy nbin {nbin[sl][heavy].mean() if heavy.any() else 0:7.1f}')
 late = np.argsort(end)[::-1][:10]
 print('latest ending (slot, start, dur):', [(int(i), round(float(start[i]), 1),
                                             round(float(dur[i]), 1)) for i in late])
