@@ -37,6 +37,7 @@ enum KernelId {
   K_RAST_INTERP,
   K_DT_BIN,
   K_DT_FWD,
+  K_DIBR_BWD,
   K_NUM_KERNELS
 };
 

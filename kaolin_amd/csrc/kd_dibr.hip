@@ -13,6 +13,7 @@
 // Results are exactly those of rasterize + dibr_soft_mask.
 #include "../../include/kaolin_dibr.h"
 #include "kd_raster.hpp"
+#include "kd_raster_bwd.hpp"
 #include "kd_soft.hpp"
 
 #include <vector>
@@ -138,6 +139,12 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
     sa.grad_soft = grad_soft;
     sa.soft_in = soft;
     sa.grad_fvi = gfvi;
+    if (grad_interp && D <= 3 && !(debug_flags() & (1 << 24))) {
+      // both backwards in one launch (kd_dibr_bwd)
+      const RasterBwdArgs<T> ra{B,   H,    W,   F,    D,     grad_interp, face_idx,
+                                weights, fvi, feat, eps, gfvi, gfeat, debug_flags()};
+      return dibr_backward_merged_launch<T>(sa, d.pb, ra, stream);
+    }
     rc = soft_pairs_backward_launch<T>(sa, d.pb, stream);
     if (rc != KD_OK) return rc;
   }

@@ -19,6 +19,7 @@
 #include "kd_binning.hpp"
 #include "kd_capi.hpp"
 #include "kd_raster.hpp"
+#include "kd_raster_bwd.hpp"
 #include "kd_tile.hpp"
 
 #include <type_traits>
@@ -356,59 +357,6 @@ __global__ __launch_bounds__(kBlock, 6) void kd_raster_fwd_pairs(RasterFwdArgs<f
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Backward terms of one covered pixel (rasterization_cuda.cu:271-399) into out[]: out[0..5]
-// the 6 corner terms summed over the D features, out[6 + ii*DMAX + d] the feature terms
-// (register array, static indices only).
-// ------------------------------------------------------------------------------------------
-template <typename T, int DMAX>
-__device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], const T *g,
-                                                 const T *c, int D, float eps,
-                                                 T out[6 + 3 * DMAX]) {
-  T gd[DMAX];
-#pragma unroll
-  for (int d = 0; d < DMAX; ++d) gd[d] = d < D ? g[d] : (T)0;
-#pragma unroll
-  for (int ii = 0; ii < 3; ++ii)
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) out[6 + ii * DMAX + d] = gd[d] * wts[ii];
-  const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
-  const T aw = wts[0], bw = wts[1], cw = wts[2];
-  const T x0 = aw * ax + bw * bx + cw * cx;
-  const T y0 = aw * ay + bw * by + cw * cy;
-  const T m = bx - ax, p = by - ay, n = cx - ax, q = cy - ay, s = x0 - ax, t = y0 - ay;
-  const T k1 = s * q - n * t;
-  const T k2 = m * t - s * p;
-  T k3 = m * q - n * p;
-  k3 = (T)((double)k3 + copysign((double)eps, (double)k3));
-  const T zero = (T)0;
-  const T dk1dm = zero, dk1dn = -t, dk1dp = zero, dk1dq = s, dk1ds = q, dk1dt = -n;
-  const T dk2dm = t, dk2dn = zero, dk2dp = -s, dk2dq = zero, dk2ds = -p, dk2dt = m;
-  const T dk3dm = q, dk3dn = -p, dk3dp = -n, dk3dq = m, dk3ds = zero, dk3dt = zero;
-  const T dw1dm = dk1dm * k3 - dk3dm * k1, dw1dn = dk1dn * k3 - dk3dn * k1;
-  const T dw1dp = dk1dp * k3 - dk3dp * k1, dw1dq = dk1dq * k3 - dk3dq * k1;
-  const T dw1ds = dk1ds * k3 - dk3ds * k1, dw1dt = dk1dt * k3 - dk3dt * k1;
-  const T dw2dm = dk2dm * k3 - dk3dm * k2, dw2dn = dk2dn * k3 - dk3dn * k2;
-  const T dw2dp = dk2dp * k3 - dk3dp * k2, dw2dq = dk2dq * k3 - dk3dq * k2;
-  const T dw2ds = dk2ds * k3 - dk3ds * k2, dw2dt = dk2dt * k3 - dk3dt * k2;
-  const T dw1[6] = {-(dw1dm + dw1dn + dw1ds), -(dw1dp + dw1dq + dw1dt), dw1dm, dw1dp, dw1dn,
-                    dw1dq};
-  const T dw2[6] = {-(dw2dm + dw2dn + dw2ds), -(dw2dp + dw2dq + dw2dt), dw2dm, dw2dp, dw2dn,
-                    dw2dq};
-  const T kk = k3 * k3;
-#pragma unroll
-  for (int j = 0; j < 6; ++j) out[j] = (T)0;
-#pragma unroll
-  for (int d = 0; d < DMAX; ++d) {
-    if (d < D) {
-      const T c0 = c[d], c1 = c[D + d], c2 = c[2 * D + d];
-      const T dldI = gd[d] / kk;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) out[j] += dldI * ((c1 - c0) * dw1[j] + (c2 - c0) * dw2[j]);
-    }
-  }
-}
-
 // General per-pixel form for wide features (D > 8): one thread per pixel, float atomics.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_raster_bwd_atomic(
@@ -461,101 +409,10 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_atomic(
   }
 }
 
-// One workgroup per 16x16 tile.  Every pixel writes its terms to LDS; pixels are grouped by face:
-// an LDS hash table gives each face a slot, the slot's LDS counter gives each pixel its rank
-// among the slot's pixels, a prefix sum over the slots turns (slot, rank) into a position, and
-// the tile sum of each (face, term) is then added by one lane and flushed with one float atomic
-// per (tile, face, term), a face's terms on adjacent lanes (its 6 corner terms and its 3*D
-// feature terms are contiguous in memory).  (Summation order varies with the LDS counters, as it
-// does across tiles with the float atomics.)
 template <typename T, int DMAX>
-__global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(
-    int B, int H, int W, int64_t F, int D, const T *__restrict__ grad,
-    const int64_t *__restrict__ face_idx, const T *__restrict__ weights,
-    const T *__restrict__ fvi, const T *__restrict__ feat, float eps, T *grad_fvi,
-    T *grad_feat, int dbg) {
-  constexpr int SMAX = 6 + 3 * DMAX;
-  constexpr int HT = kBlock;  // slots >= distinct faces of a tile
-  __shared__ int s_key[HT];
-  __shared__ int s_n[HT];  // pixels per slot (their ranks come from the counter)
-  __shared__ T s_con[kBlock][SMAX + 1];
-  __shared__ short s_off[HT];
-  __shared__ int s_list[HT];
-  __shared__ int s_cnt[4];
-  const int S = 6 + 3 * D;
-  const int tid = threadIdx.x;
-  const int ntx = (W + kTile - 1) / kTile;
-  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin, so XCD x gets the contiguous
-  // band of tiles [x n/8, (x+1) n/8): neighbouring tiles (which share faces) share one L2
-  const int n = gridDim.x * gridDim.y;
-  int d = blockIdx.y * gridDim.x + blockIdx.x;
-  if ((n & 7) == 0 && !(dbg & (1 << 17))) d = (d & 7) * (n >> 3) + (d >> 3);
-  const int b = d / gridDim.x, tl = d - b * gridDim.x;
-  const int px = (tl % ntx) * kTile + (tid & 15);
-  const int py = (tl / ntx) * kTile + (tid >> 4);
-  s_key[tid] = -1;
-  s_n[tid] = 0;
-  __syncthreads();
-  int h = -1, rank = 0;
-  T c[SMAX];
-  if (px < W && py < H) {
-    const int64_t p = ((int64_t)b * H + py) * W + px;
-    // the pixel's weights and incoming gradient do not depend on its face: issued with it
-    const int64_t f = face_idx[p];
-    const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
-    T gd[DMAX];
-#pragma unroll
-    for (int d = 0; d < DMAX; ++d) gd[d] = d < D ? grad[p * D + d] : (T)0;
-    if (f >= 0 && f < F) {
-      unsigned u = ((unsigned)f * 2654435761u) >> 24;
-      for (;;) {  // <= 256 keys in 256 slots: terminates
-        const int old = atomicCAS(&s_key[u], -1, (int)f);
-        if (old == -1 || old == (int)f) break;
-        u = (u + 1) & (HT - 1);
-      }
-      h = (int)u;
-      rank = atomicAdd(&s_n[h], 1);
-      const int64_t tf = (int64_t)b * F + f;
-      raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, gd, feat + tf * 3 * D, D, eps, c);
-    }
-  }
-  __syncthreads();
-  // slot sizes -> positions (prefix sum over slots), and the list of occupied slots
-  const int sz = s_n[tid];
-  int total;
-  const int off = wg_exclusive_scan(sz, s_cnt, total);
-  s_off[tid] = (short)off;
-  int nocc;
-  const bool occ = sz > 0;
-  const int pos = wg_compact(occ, s_cnt, nocc);
-  if (occ) s_list[pos] = tid;
-  __syncthreads();
-  // the pixel's terms go to its position in slot order, so a slot's terms are contiguous rows
-  if (h >= 0) {
-    const int ps = s_off[h] + rank;
-#pragma unroll
-    for (int j = 0; j < 6; ++j) s_con[ps][j] = c[j];
-#pragma unroll
-    for (int ii = 0; ii < 3; ++ii)
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d)
-        if (d < D) s_con[ps][6 + ii * D + d] = c[6 + ii * DMAX + d];
-  }
-  __syncthreads();
-  for (int idx = tid; idx < nocc * S; idx += kBlock) {
-    const int i = idx / S, j = idx - i * S;
-    const int slot = s_list[i];
-    const int n = s_n[slot];
-    const int o = s_off[slot];
-    T v = (T)0;
-    for (int r = 0; r < n; ++r) v += s_con[o + r][j];  // independent reads: pipelined
-    if (v == (T)0 || (dbg & 128)) continue;
-    const int64_t row = (int64_t)b * F + s_key[slot];
-    if (j < 6)
-      atomicAdd(grad_fvi + row * 6 + j, v);
-    else if (grad_feat)
-      atomicAdd(grad_feat + row * 3 * D + (j - 6), v);
-  }
+__global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(RasterBwdArgs<T> ra) {
+  raster_bwd_tile_body<T, DMAX>(ra, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y,
+                                gridDim.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -615,21 +472,20 @@ int raster_backward_launch(int B, int H, int W, int64_t F, int D, const T *grad,
   const int64_t total = (int64_t)B * H * W;
   if (total > 0 && nf > 0) {
     const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    const RasterBwdArgs<T> ra{B,   H,    W,   F,    D,     grad, fidx,
+                              weights, fvi, feat, eps, gfvi, gfeat, debug_flags()};
     if (D <= 3) {  // 6 + 3 D <= 15 terms: 16 KB of LDS terms, 8 workgroups per CU
       ProfScope prof(K_RASTER_BWD_TILE, stream);
-      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 3>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
-                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
-                         debug_flags());
+      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 3>), dim3(ntiles, B), dim3(kBlock), 0, stream,
+                         ra);
     } else if (D <= 4) {
       ProfScope prof(K_RASTER_BWD_TILE, stream);
-      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 4>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
-                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
-                         debug_flags());
+      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 4>), dim3(ntiles, B), dim3(kBlock), 0, stream,
+                         ra);
     } else if (D <= 8) {
       ProfScope prof(K_RASTER_BWD_TILE, stream);
-      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 8>), dim3(ntiles, B), dim3(kBlock), 0, stream, B,
-                         H, W, F, D, grad, fidx, weights, fvi, feat, eps, gfvi, gfeat,
-                         debug_flags());
+      hipLaunchKernelGGL((kd_raster_bwd_tile<T, 8>), dim3(ntiles, B), dim3(kBlock), 0, stream,
+                         ra);
     } else {
       const int64_t blocks = (total + kBlock - 1) / kBlock;
       ProfScope prof(K_RASTER_BWD_ATOMIC, stream);

@@ -223,6 +223,12 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
 // the backward over the records of soft_pairs_launch(grad = true), adding into a.grad_fvi
 template <typename T>
 int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream);
+// The soft-mask backward and the raster backward (kd_raster_bwd.hpp, D <= 3) in one launch.
+template <typename T>
+struct RasterBwdArgs;
+template <typename T>
+int dibr_backward_merged_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, const RasterBwdArgs<T> &ra,
+                                hipStream_t stream);
 // bins + pass A + pair math (+ backward coefficients when grad) + (when reduce) the soft mask
 template <typename T>
 int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, bool reduce,

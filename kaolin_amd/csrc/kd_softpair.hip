@@ -23,6 +23,7 @@
 // the record (face corners, distance type, the forward's probability) and adds s_p * h_j per
 // coordinate (same value up to rounding order, like the reference's own atomics).  The close
 // lists are never needed.
+#include "kd_raster_bwd.hpp"
 #include "kd_soft.hpp"
 
 namespace kd {
@@ -84,6 +85,35 @@ __device__ __forceinline__ void tile_pixel(int tx, int ty, int q, int &px, int &
 template <typename T>
 __device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et, T prob, float M,
                                                T h[4]) {
+  if constexpr (std::is_same<T, float>::value) {
+    {
+      // fp32 with hardware reciprocals (1 ulp): the gradient's accuracy is that of the
+      // reference's fp32 terms, whose double divisions end in float roundings too
+      const float s = prob * __builtin_amdgcn_rcpf((1.f - prob + 1e-7f) * M);
+      if (et >= 3) {
+        const int ps = (et - 3) * 2;
+        h[0] = s * (2.f * (v[ps] - x0));
+        h[1] = s * (2.f * (v[ps + 1] - y0));
+        h[2] = 0.f;
+        h[3] = 0.f;
+      } else {
+        const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
+        const float x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
+        const float A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+        const float up = A * x0 + Bc * y0 + C;
+        const float rd = __builtin_amdgcn_rcpf(A * A + Bc * Bc + 1e-7f);
+        const float dissquare = up * up * rd;
+        const float dzdA = 2.f * (x0 * up - dissquare * A) * rd;
+        const float dzdB = 2.f * (y0 * up - dissquare * Bc) * rd;
+        const float dzdC = 2.f * up * rd;
+        h[0] = s * (dzdB - y2 * dzdC);
+        h[1] = s * (x2 * dzdC - dzdA);
+        h[2] = s * (y1 * dzdC - dzdB);
+        h[3] = s * (dzdA - x1 * dzdC);
+      }
+      return;
+    }
+  }
   // the backward's coefficients need gradient accuracy, not bit-exactness: reciprocals
   const double s = (double)prob * (1.0 / ((1.0 - (double)prob + KD_SOFT_EPS) * (double)M));
   if (et >= 3) {
@@ -486,8 +516,19 @@ template <typename T>
 __device__ __forceinline__ void soft_add_pair(T g[6], int et, double sp, const SoftCoef<T> &c) {
   const int ps = et >= 3 ? (et - 3) * 2 : et * 2;
   const int ps2 = et >= 3 ? -8 : ((et + 1) % 3) * 2;  // vertex types touch one corner only
-  const T v0 = (T)(sp * (double)c.h[0]), v1 = (T)(sp * (double)c.h[1]);
-  const T v2 = (T)(sp * (double)c.h[2]), v3 = (T)(sp * (double)c.h[3]);
+  T v0, v1, v2, v3;
+  if (std::is_same<T, float>::value) {
+    const T spf = (T)sp;
+    v0 = spf * c.h[0];
+    v1 = spf * c.h[1];
+    v2 = spf * c.h[2];
+    v3 = spf * c.h[3];
+  } else {
+    v0 = (T)(sp * (double)c.h[0]);
+    v1 = (T)(sp * (double)c.h[1]);
+    v2 = (T)(sp * (double)c.h[2]);
+    v3 = (T)(sp * (double)c.h[3]);
+  }
 #pragma unroll
   for (int i = 0; i < 6; ++i)
     g[i] += i == ps ? v0 : i == ps + 1 ? v1 : i == ps2 ? v2 : i == ps2 + 1 ? v3 : (T)0;
@@ -530,14 +571,15 @@ __device__ __forceinline__ void seg_scan_shfl(int seg, int lane, T g[6]) {
 // probability (soft_pair_coef): the forward's critical path skips them, and this kernel, bound by
 // its load chains and atomics, absorbs the arithmetic (measured free).
 template <typename T, int R>
-__global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftPairBuf<T> pb) {
+__device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
+                                                    int blk, int nblk) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const int lane = threadIdx.x & (kWave - 1);
   const int nitems = pb.counters[0];
   // R items per workgroup pass; their load chains (item -> record -> the pixel's gradient and
   // soft value, the face's corners) are issued together
-  for (int it0 = blockIdx.x * R; it0 < nitems; it0 += gridDim.x * R) {
+  for (int it0 = blk * R; it0 < nitems; it0 += nblk * R) {
     int2 item[R];
     bool ok[R];
     SoftPairRec r[R];
@@ -607,6 +649,26 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftP
       }
     }
   }
+}
+
+template <typename T, int R>
+__global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  soft_bwd_items_body<T, R>(a, pb, blockIdx.x, gridDim.x);
+}
+
+// The DIB-R backward in one launch: the raster backward's tiles and the soft mask's items are
+// independent (both only add into grad_fvi), so one grid holds both, the raster tiles first
+// (their XCD band mapping keeps its block ids), and the soft items fill the raster's tail:
+// 72 us against 38 + 41 for the two launches at C3 (alternating runs of 8: 74 us).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_dibr_bwd(SoftArgs<T> a, SoftPairBuf<T> pb,
+                                                      RasterBwdArgs<T> ra, int nr, int ns,
+                                                      int ntl) {
+  const int blk = blockIdx.x;
+  if (blk < nr)
+    raster_bwd_tile_body<T, 3>(ra, blk, nr, ntl);
+  else
+    soft_bwd_items_body<T, 1>(a, pb, blk - nr, ns);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -690,6 +752,26 @@ int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t s
 }
 
 template <typename T>
+int dibr_backward_merged_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, const RasterBwdArgs<T> &ra,
+                                hipStream_t stream) {
+  KD_CHECK_ARG(ra.D <= 3, "merged backward: D > 3");
+  const int ntl = (int)pb.ntiles;
+  const int64_t nr64 = (int64_t)ra.B * ntl;
+  KD_CHECK_ARG(nr64 + kMathBlocks < (1ll << 31), "merged backward: too many tiles");
+  const int nr = (int)nr64, ns = (int)kMathBlocks;
+  a.fs.dbg = debug_flags();
+  a.fs.tbuf = debug_tile_buffer();
+  {
+    ProfScope prof(K_DIBR_BWD, stream);
+    hipLaunchKernelGGL((kd_dibr_bwd<T>), dim3((unsigned)(nr + ns)), dim3(kBlock), 0, stream, a,
+                       pb, ra, nr, ns, ntl);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr bwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+template <typename T>
 int soft_pairs_backward(SoftArgs<T> &a, void *ws, size_t ws_bytes, hipStream_t stream) {
   const FaceSet<T> &fs = a.fs;
   const size_t need = soft_pair_workspace_bytes(fs.B, fs.H, fs.W, fs.N, fs.F, a.K, sizeof(T));
@@ -710,6 +792,10 @@ template int soft_pairs_launch<double>(SoftArgs<double> &, SoftPairBuf<double> &
                                        hipStream_t);
 template int soft_pairs_backward_launch<float>(SoftArgs<float> &, SoftPairBuf<float> &,
                                                hipStream_t);
+template int dibr_backward_merged_launch<float>(SoftArgs<float> &, SoftPairBuf<float> &,
+                                                const RasterBwdArgs<float> &, hipStream_t);
+template int dibr_backward_merged_launch<double>(SoftArgs<double> &, SoftPairBuf<double> &,
+                                                 const RasterBwdArgs<double> &, hipStream_t);
 template int soft_pairs_backward_launch<double>(SoftArgs<double> &, SoftPairBuf<double> &,
                                                 hipStream_t);
 template int soft_pairs_forward<float>(SoftArgs<float> &, void *, size_t, bool, bool,

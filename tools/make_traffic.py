@@ -24,6 +24,7 @@ SLOT = {
     'kd::kd_raster_bwd_tile<float, 4>': 'kd_raster_bwd_tile',
     'kd::kd_bin_count<float>': 'kd_bin_count', 'kd::kd_bin_scan': 'kd_bin_scan',
     'kd::kd_bin_scatter<float>': 'kd_bin_scatter',
+    'kd::kd_dibr_bwd<float>': 'kd_dibr_bwd',
 }
 
 
