@@ -78,6 +78,9 @@ def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4, f
     if kernel == 'kd_soft_bwd_pairs':  # records + probabilities, grad/soft, corners in; face
         # grads added
         return pairs * (12 + e) + P * 2 * e + F * 6 * e * 3
+    if kernel == 'kd_dibr_fwd':        # raster forward + whole soft mask in one launch
+        return (algorithmic_bytes('kd_raster_fwd', P, F, Fv, D, K, lists, pairs, V, e) +
+                algorithmic_bytes('kd_soft_pairs', P, F, Fv, D, K, lists, pairs, V, e))
     if kernel == 'kd_dibr_bwd':        # the two backwards above in one launch
         return (algorithmic_bytes('kd_raster_bwd_tile', P, F, Fv, D, K, lists, pairs, V, e) +
                 algorithmic_bytes('kd_soft_bwd_pairs', P, F, Fv, D, K, lists, pairs, V, e))

@@ -32,7 +32,7 @@ const char *kNames[K_NUM_KERNELS] = {
     "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs",
     "kd_prepare_fwd", "kd_prepare_bwd", "kd_tile_order", "kd_iou_partial", "kd_iou_bwd",
     "kd_tex_fwd", "kd_tex_bwd", "kd_rast_interp", "kd_dt_bin",
-    "kd_dt_fwd", "kd_dibr_bwd"};
+    "kd_dt_fwd", "kd_dibr_bwd", "kd_dibr_fwd"};
 }  // namespace
 
 ProfScope::ProfScope(int id_, hipStream_t s) : id(id_), stream(s), on(g_prof.load()) {

@@ -38,6 +38,7 @@ enum KernelId {
   K_DT_BIN,
   K_DT_FWD,
   K_DIBR_BWD,
+  K_DIBR_FWD,
   K_NUM_KERNELS
 };
 

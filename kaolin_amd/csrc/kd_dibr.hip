@@ -16,6 +16,7 @@
 #include "kd_raster_bwd.hpp"
 #include "kd_soft.hpp"
 
+#include <type_traits>
 #include <vector>
 
 namespace kd {
@@ -92,8 +93,6 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> ra{rfs, d.rbb, fvz, fvz_fs, fvz_cs, feat, D, eps, interp, face_idx, weights};
-  int rc = raster_launch<T>(ra, stream);
-  if (rc != KD_OK) return rc;
   SoftArgs<T> sa{};
   sa.fs = sfs;
   sa.bb = d.sbb;
@@ -107,6 +106,11 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   sa.nzero0 = gz_fvi ? nf * 6 : 0;
   sa.zero1 = gz_feat;
   sa.nzero1 = gz_feat ? nf * 3 * D : 0;
+  if constexpr (std::is_same<T, float>::value) {
+    if (dibr_fwd_fusable(ra, sa)) return dibr_fwd_fused_launch(ra, sa, d.pb, stream);
+  }
+  const int rc = raster_launch<T>(ra, stream);
+  if (rc != KD_OK) return rc;
   return soft_pairs_launch<T>(sa, d.pb, want_grad != 0, true, stream);
 }
 

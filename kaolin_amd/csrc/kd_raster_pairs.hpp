@@ -1,0 +1,271 @@
+// kd_raster_pairs.hpp -- the reference's per-face raster test and the fp32 pair pipeline's tile
+// body (kd_raster_fwd_pairs), shared with the fused DIB-R forward (kd_dibr_fwd_tiles in
+// kd_softpair.hip).
+#pragma once
+
+#include "kd_binning.hpp"
+#include "kd_raster.hpp"
+#include "kd_tile.hpp"
+
+namespace kd {
+
+template <typename T>
+struct ScaleUp {  // 2^(-min normal exponent): |w| * value >= |norm| => |w / norm| >= min normal
+  static constexpr T value = 0x1p126f;
+};
+template <>
+struct ScaleUp<double> {
+  static constexpr double value = 0x1p1022;
+};
+
+// The reference per-face test (rasterization_cuda.cu:131-159) for one pixel whose centre passed
+// the box test: edge functions, eps-normalised barycentrics (division before the sign test,
+// exactly as the reference), depth.  EarlyReject adds an exact shortcut for pixels outside.
+template <typename T, bool EarlyReject = true>
+__device__ __forceinline__ bool raster_face_test(T x0, T y0, T ax, T ay, T bx, T by, T cx, T cy,
+                                                 T az, T bz, T cz, float eps, T &w0, T &w1,
+                                                 T &w2, T &z0) {
+  const T a_edge_x = ax - x0, a_edge_y = ay - y0;
+  const T b_edge_x = bx - x0, b_edge_y = by - y0;
+  const T c_edge_x = cx - x0, c_edge_y = cy - y0;
+  w0 = b_edge_x * c_edge_y - b_edge_y * c_edge_x;
+  w1 = c_edge_x * a_edge_y - c_edge_y * a_edge_x;
+  w2 = a_edge_x * b_edge_y - a_edge_y * b_edge_x;
+  T norm = w0 + w1 + w2;
+  norm = (T)((double)norm + copysign((double)eps, (double)norm));
+  // Exact early rejection: with a finite nonzero norm, a nonzero non-NaN w of the opposite sign
+  // whose quotient cannot round to -0 (|w| >= |norm| * 2^-(min normal exponent)) makes the
+  // reference's `w / norm < 0` true.  Anything else takes the reference path below.
+  if (EarlyReject && isfinite(norm) && norm != (T)0) {
+    const bool nneg = norm < (T)0;
+    const T big = ScaleUp<T>::value;
+    const T an = fabs(norm);
+    if (((w0 < (T)0) != nneg && w0 != (T)0 && !isnan(w0) && fabs(w0) * big >= an) ||
+        ((w1 < (T)0) != nneg && w1 != (T)0 && !isnan(w1) && fabs(w1) * big >= an) ||
+        ((w2 < (T)0) != nneg && w2 != (T)0 && !isnan(w2) && fabs(w2) * big >= an))
+      return false;
+  }
+  w0 /= norm;
+  w1 /= norm;
+  w2 /= norm;
+  if (w0 < (T)0. || w1 < (T)0. || w2 < (T)0.) return false;
+  z0 = w0 * az + w1 * bz + w2 * cz;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------
+// fp32 forward as a (pixel, face) pair pipeline.  The lane-per-pixel loop above runs every face
+// of the wave's sub-list on every lane, although a pixel centre is inside only ~1/5 of the boxes
+// that hold it on this workload; here the full test runs once per (pixel, candidate face) pair
+// with every lane busy, and the candidates are culled per pixel row by the triangle's edges:
+//   stage  lane = face (once per tile): the keep-interval of every edge as an affine function of
+//          the row, in tile-local pixel units, with a rigorous error margin (raster_cull_coefs);
+//   A  lane = face: per row of the 8x8 sub-tile, [ceil(max lo - d), floor(min hi + d)] clipped
+//      to the exact box span -> a 64-bit pixel mask; a 64x64 bit transpose across the wave gives
+//      each pixel lane its candidate mask over the chunk; a DPP scan places the (pixel, face)
+//      pairs in a per-wave list;
+//   B  lane = pair: the reference's edge functions, eps-norm, divisions, inside test and depth;
+//      an inside face posts key = (order-preserving bits of z, ~face index) with a 64-bit LDS
+//      atomicMax per pixel.
+//   The winner is the face with the largest z and, among equal z, the lowest index -- exactly
+//   what the reference's ascending scan with strict `z > best` keeps (rasterization_cuda.cu:162),
+//   provided no depth is NaN (-0 is folded to +0 first; -inf never wins there); a pixel that
+//   meets a NaN depth replays the reference's sequential loop over its coarse bin instead.
+//   The winner's weights are recomputed with the identical expression for the outputs.
+// ------------------------------------------------------------------------------------------
+constexpr int kRasterPairCap = 256;
+
+__device__ __forceinline__ uint32_t ordered_f32(float z) {
+  const uint32_t u = __float_as_uint(z + 0.0f);  // -0 -> +0
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// LDS of one tile of the pair pipeline
+struct RasterPairsLDS {
+  TileLists L;
+  float geo[9][kCap];   // ax ay bx by cx cy (scaled), az bz cz
+  float4 cull[2][kCap];  // raster_cull_coefs (kd_binning), face frame
+  unsigned short pair[4][kRasterPairCap];  // (q << 8) | sub-list entry
+  unsigned long long key[4][64];
+  unsigned long long nan[4];
+};
+
+// Tile tl of view b (nbin: faces of its coarse bin, or -1).  Each thread owns pixel
+// (t.px, t.py) of tile_geom(H, W, tl) and writes its outputs.
+__device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a, int b, int tl,
+                                                  int nbin, RasterPairsLDS &S) {
+  TileLists &L = S.L;
+  auto &s_geo = S.geo;
+  auto &s_cull = S.cull;
+  auto &s_pair = S.pair;
+  auto &s_key = S.key;
+  auto &s_nan = S.nan;
+  const FaceSet<float> &fs = a.fs;
+  const int H = fs.H, W = fs.W;
+  const float M = fs.M;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int64_t lo, hi;
+  view_range(fs, b, lo, hi);
+  TileGeom t = tile_geom(H, W, tl);
+  t.nbin = nbin;
+  const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
+  s_key[w][lane] = 0ull;
+  if (lane == 0) s_nan[w] = 0ull;
+  // this wave's row centres relative to its first row
+  const float ysub = px_cy(M, H, t.WY0);
+  float drow[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) drow[r] = px_cy(M, H, t.WY0 + r) - ysub;
+  constexpr float kSlack = 1.f / 64.f;
+
+  auto stage = [&](int k, int64_t fi) {
+    float v[6];
+    load_corners(fs, fi, v);
+#pragma unroll
+    for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
+    const float *zz = a.fvz + fi * a.fvz_fs;
+    s_geo[6][k] = zz[0];
+    s_geo[7][k] = zz[a.fvz_cs];
+    s_geo[8][k] = zz[2 * a.fvz_cs];
+    s_cull[0][k] = a.bb.cull[2 * fi];
+    s_cull[1][k] = a.bb.cull[2 * fi + 1];
+  };
+  // B: the reference's per-pixel test (rasterization_cuda.cu:131-162) over the current batch
+  auto test_batch = [&](int total) {
+    if (fs.dbg & 16) return;
+    wave_lds_sync();
+    for (int e0 = 0; e0 < total; e0 += kWave) {
+      const int e = e0 + lane;
+      if (e < total) {
+        const int pr = s_pair[w][e];
+        const int q = pr >> 8, k = L.sub[w][pr & 255];
+        const float x0 = sx * (float)(2 * (t.WX0 + (q & 7)) + 1 - W);
+        const float y0 = sy * (float)(H - 2 * (t.WY0 + (q >> 3)) - 1);
+        float w0, w1, w2, z0;
+        if (raster_face_test<float, false>(x0, y0, s_geo[0][k], s_geo[1][k], s_geo[2][k],
+                                           s_geo[3][k], s_geo[4][k], s_geo[5][k], s_geo[6][k],
+                                           s_geo[7][k], s_geo[8][k], a.eps, w0, w1, w2, z0)) {
+          if (isnan(z0)) {
+            atomicOr(&s_nan[w], 1ull << q);
+          } else if (z0 != -INFINITY) {
+            const unsigned long long key =
+                ((unsigned long long)ordered_f32(z0) << 32) |
+                (unsigned long long)(0xffffffffu - (uint32_t)L.f[k]);
+            atomicMax(&s_key[w][q], key);
+          }
+        }
+      }
+    }
+    wave_lds_sync();
+  };
+  auto round = [&](int nsub, int) {
+    if (nsub == 0 || (fs.dbg & 1)) return;
+    int total = 0;
+#pragma unroll 1
+    for (int c = 0; c < 4; ++c) {
+      if (c * kWave >= nsub) break;
+      // A: lane = face (chunk entry c*64 + lane): culled row intervals -> 64-bit pixel mask
+      const int j = c * kWave + lane;
+      uint64_t fm = 0ull;
+      if (j < nsub) {
+        const int k = L.sub[w][j];
+        const Span sp = L.span[k];
+        const int rx0 = max(sp.x0 - t.WX0, 0), rx1 = min(sp.x1 - t.WX0, 7);
+        const int ry0 = max(sp.y0 - t.WY0, 0), ry1 = min(sp.y1 - t.WY0, 7);
+        // face frame -> this sub-tile: columns shift by WX0 - span.x0, rows by the centre offset
+        const float xo = (float)(t.WX0 - sp.x0);
+        const float dref = ysub - px_cy(M, H, sp.y0);
+        const float4 cl = s_cull[0][k], ch = s_cull[1][k];
+        const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          const float d = drow[r] + dref;
+          const float plo = fmaxf(fmaf(cl.y, d, l0), fmaf(cl.w, d, l2)) - kSlack;
+          const float phi = fminf(fmaf(ch.y, d, h0), fmaf(ch.w, d, h2)) + kSlack;
+          const int xs = max((int)ceilf(__builtin_amdgcn_fmed3f(plo, -1.f, 9.f)), rx0);
+          const int xe = min((int)floorf(__builtin_amdgcn_fmed3f(phi, -1.f, 9.f)), rx1);
+          const bool row = r >= ry0 && r <= ry1 && xs <= xe;
+          const uint32_t bits = row ? ((2u << xe) - (1u << xs)) : 0u;
+          fm |= (uint64_t)bits << (8 * r);
+        }
+      }
+      // lane = pixel: candidate mask over the chunk, pairs placed by a DPP scan
+      uint64_t m = wave_transpose64(fm);
+      const int cnt = __popcll(m);
+      const int incl = wave_incl_scan(cnt);
+      int end_tot = total + __builtin_amdgcn_readlane(incl, 63);
+      int pos = total + incl - cnt;
+      const int qbits = (lane << 8) | (c << 6);
+      while (true) {
+        while (m && pos < kRasterPairCap) {
+          s_pair[w][pos++] = (unsigned short)(qbits | (int)__builtin_ctzll(m));
+          m &= m - 1ull;
+        }
+        if (end_tot <= kRasterPairCap) break;
+        test_batch(kRasterPairCap);  // the batch is exactly full
+        pos -= kRasterPairCap;
+        end_tot -= kRasterPairCap;
+      }
+      total = end_tot;
+    }
+    if (total) test_batch(total);
+  };
+  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
+
+  if (!t.inimg || (fs.dbg & 8192)) return;
+  const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
+  const float x0 = px_cx(M, W, t.px), y0 = px_cy(M, H, t.py);
+  int best = -1;
+  float bw0 = 0.f, bw1 = 0.f, bw2 = 0.f;
+  if ((s_nan[w] >> lane) & 1ull) {
+    // the reference's sequential loop over this pixel's coarse bin (ascending faces)
+    const BinGeom &g = a.bb.g;
+    const int ct = (t.py / g.ct) * g.nctx + (t.px / g.ct);
+    const int n = a.bb.totals[(int64_t)b * g.nct() + ct];
+    const int *bin = a.bb.bins + (int64_t)ct * fs.N + lo;
+    float max_z0 = -INFINITY;
+    for (int e = 0; e < n; ++e) {
+      const int f = bin[e];
+      if (!pspan_has(pack_span(a.bb.spans[lo + f]), t.px, t.py)) continue;
+      float v[6];
+      load_corners(fs, lo + f, v);
+      const float *zz = a.fvz + (lo + f) * a.fvz_fs;
+      float w0, w1, w2, z0;
+      if (!raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0],
+                                   zz[a.fvz_cs], zz[2 * a.fvz_cs], a.eps, w0, w1, w2, z0))
+        continue;
+      if (z0 <= max_z0) continue;
+      max_z0 = z0;
+      best = f;
+      bw0 = w0;
+      bw1 = w1;
+      bw2 = w2;
+    }
+  } else if (s_key[w][lane] != 0ull) {
+    best = (int)(0xffffffffu - (uint32_t)(s_key[w][lane] & 0xffffffffull));
+    float v[6];
+    load_corners(fs, lo + best, v);
+    const float *zz = a.fvz + (lo + best) * a.fvz_fs;
+    float z0;
+    raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[a.fvz_cs],
+                            zz[2 * a.fvz_cs], a.eps, bw0, bw1, bw2, z0);
+  }
+  a.face_idx[p] = best;
+  float *wo = a.weights + p * 3;
+  float *io = a.interp + p * a.D;
+  if (best >= 0) {
+    wo[0] = bw0;
+    wo[1] = bw1;
+    wo[2] = bw2;
+    const float *r = a.feat + (lo + best) * 3 * a.D;
+    for (int d = 0; d < a.D; ++d)
+      io[d] = bw0 * r[d] + bw1 * r[a.D + d] + bw2 * r[2 * a.D + d];
+  } else {
+    wo[0] = 0.f;
+    wo[1] = 0.f;
+    wo[2] = 0.f;
+    for (int d = 0; d < a.D; ++d) io[d] = 0.f;
+  }
+}
+
+}  // namespace kd

@@ -223,6 +223,12 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
 // the backward over the records of soft_pairs_launch(grad = true), adding into a.grad_fvi
 template <typename T>
 int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream);
+// The raster forward (fp32 pair pipeline) and the fused soft mask in one launch, when both apply.
+template <typename T>
+struct RasterFwdArgs;
+bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a);
+int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
+                          hipStream_t stream);
 // The soft-mask backward and the raster backward (kd_raster_bwd.hpp, D <= 3) in one launch.
 template <typename T>
 struct RasterBwdArgs;

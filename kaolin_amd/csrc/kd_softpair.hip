@@ -24,6 +24,7 @@
 // coordinate (same value up to rounding order, like the reference's own atomics).  The close
 // lists are never needed.
 #include "kd_raster_bwd.hpp"
+#include "kd_raster_pairs.hpp"
 #include "kd_soft.hpp"
 
 namespace kd {
@@ -226,21 +227,28 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
 // the same workgroup then runs the pair math over its own records and the ordered product of
 // each pixel's slots -- the whole soft mask in one launch.  Pass A notes each (slot, pixel)'s
 // record index in LDS, so the product reads the probabilities in slot order.
-template <typename T, bool FUSED, int OCC = 8>
-__global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
-  __shared__ unsigned short s_ridx[FUSED ? kFuseSlots : 1][kBlock];
-  TileClock clk(a.fs.tbuf, 1);
-  clk.start_to(2);
-  __shared__ TileLists L;
-  __shared__ uint64_t s_pm[4][kWave];
-  __shared__ unsigned short s_off[4][kWave];
-  __shared__ int s_nrec;
+template <bool FUSED>
+struct SoftPairsLDS {
+  unsigned short ridx[FUSED ? kFuseSlots : 1][kBlock];
+  TileLists L;
+  uint64_t pm[4][kWave];
+  unsigned short off[4][kWave];
+  int nrec, base, box[4];
+};
 
+// Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
+// (t.px, t.py) of tile_geom(H, W, tl); a.face_idx of that pixel is read by the same thread (the
+// fused forward wrote it in the same workgroup, same thread).
+template <typename T, bool FUSED>
+__device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
+                                                int b, int tl, int nbin, SoftPairsLDS<FUSED> &S) {
+  auto &s_ridx = S.ridx;
+  TileLists &L = S.L;
+  auto &s_pm = S.pm;
+  auto &s_off = S.off;
+  int &s_nrec = S.nrec;
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
-  if (fs.dbg & 16384) return;  // diagnostics: dispatch cost only
-  int b, tl, nbin;
-  tile_of_block(a.bb, H, W, b, tl, nbin, fs.dbg);
   const int tid = threadIdx.x, w = tid >> 6;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
@@ -260,7 +268,7 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
   // faces matter only where they reach an uncovered pixel: the filter boxes of tile_rounds
   // shrink to the uncovered pixels' bounding boxes (exact: a record needs the pixel centre
   // inside the face's enlarged span)
-  __shared__ int s_box[4];
+  int *s_box = S.box;
   if (tid == 0) {
     s_box[0] = s_box[2] = 1 << 30;
     s_box[1] = s_box[3] = -1;
@@ -325,7 +333,7 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
   }
   if (n > 0) {  // work items of the math and backward passes
     const int nch = (n + kBlock - 1) / kBlock;
-    __shared__ int s_base;
+    int &s_base = S.base;
     if (tid == 0) {
       s_base = atomicAdd(&pb.counters[0], nch);
       pb.tiles[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
@@ -381,6 +389,38 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
       a.soft[p] = (T)(1.0 - (double)prod);
     }
   }
+}
+
+template <typename T, bool FUSED, int OCC = 8>
+__global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  __shared__ SoftPairsLDS<FUSED> S;
+  TileClock clk(a.fs.tbuf, 1);
+  clk.start_to(2);
+  if (a.fs.dbg & 16384) return;  // diagnostics: dispatch cost only
+  int b, tl, nbin;
+  tile_of_block(a.bb, a.fs.H, a.fs.W, b, tl, nbin, a.fs.dbg);
+  soft_pairs_tile<T, FUSED>(a, pb, b, tl, nbin, S);
+}
+
+// The DIB-R forward's per-tile work in one launch: a workgroup rasterizes its tile (the pair
+// pipeline, kd_raster_pairs.hpp) and then runs the fused soft mask on the same tile; each thread
+// owns the same pixel in both, so the soft phase reads the face_idx its own thread just wrote.
+// No launch boundary between the two, and a tile's raster and soft work (heavy in different
+// tiles: interior vs silhouette) share one workgroup slot.  The two phases' LDS is a union.
+union DibrTileLDS {
+  RasterPairsLDS r;
+  SoftPairsLDS<true> s;
+};
+
+__global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
+                                                              SoftArgs<float> a,
+                                                              SoftPairBuf<float> pb) {
+  __shared__ DibrTileLDS U;
+  int b, tl, nbin;
+  tile_of_block(ra.bb, ra.fs.H, ra.fs.W, b, tl, nbin, ra.fs.dbg);
+  raster_pairs_tile(ra, b, tl, nbin, U.r);
+  __syncthreads();  // the raster phase is done with the LDS
+  soft_pairs_tile<float, true>(a, pb, b, tl, -1, U.s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -715,6 +755,25 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) {
+  return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
+         !(debug_flags() & ((1 << 26) | 4096));
+}
+
+int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
+                          hipStream_t stream) {
+  ra.fs.dbg = a.fs.dbg = debug_flags();
+  ra.fs.tbuf = a.fs.tbuf = nullptr;
+  {
+    ProfScope prof(K_DIBR_FWD, stream);
+    hipLaunchKernelGGL(kd_dibr_fwd_tiles, dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
+                       stream, ra, a, pb);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr fwd: %s", hipGetErrorString(e));
   return KD_OK;
 }
 

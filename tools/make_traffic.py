@@ -25,6 +25,7 @@ SLOT = {
     'kd::kd_bin_count<float>': 'kd_bin_count', 'kd::kd_bin_scan': 'kd_bin_scan',
     'kd::kd_bin_scatter<float>': 'kd_bin_scatter',
     'kd::kd_dibr_bwd<float>': 'kd_dibr_bwd',
+    'kd::kd_dibr_fwd_tiles': 'kd_dibr_fwd',
 }
 
 
