@@ -22,5 +22,5 @@ for r in range(reps):
             kern[f].setdefault(k, []).append(v['avg_us'])
 for f in (a, b):
     print(f'flags={f}: ms/step {sorted(res[f])}  best {min(res[f]):.4f}')
-for k in kern[a]:
+for k in list(kern[a]) + [k for k in kern[b] if k not in kern[a]]:
     print(f'  {k:22s} ' + '  '.join(f'{f}: {min(kern[f].get(k, [0])):7.2f}' for f in (a, b)))
