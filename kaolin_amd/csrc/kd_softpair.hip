@@ -15,6 +15,10 @@
 //   kd_soft_pair_math, kd_soft_reduce   the same math and product as separate launches, for
 //                      the op form with the reference's close-face lists (and knum > 32).
 //   kd_soft_bwd_items  the backward, flat over (tile, 256-record) items.
+//   kd_dibr_fwd_tiles  dibr_rasterization's forward: per tile, the raster pair pipeline
+//                      (kd_raster_pairs.hpp) and then the FUSED soft mask of the same tile.
+//   kd_dibr_bwd        dibr_rasterization's backward: the raster backward's tiles
+//                      (kd_raster_bwd.hpp) and the soft items in one grid.
 // Backward factorisation: the reference's per-pair gradient (dibr_soft_mask_cuda.cu:281-348) is
 //   dLdz * f_j / M  with  dLdz = -sigmainv * dLdp * (1 - soft) / (1 - p + 1e-7) * p
 // and f_j the geometric factors of the distance type (2(x1 - x0) ... for a vertex, the four
