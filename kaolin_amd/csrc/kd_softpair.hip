@@ -258,7 +258,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   view_range(fs, b, lo, hi);
   TileGeom t = tile_geom(H, W, tl);
   t.nbin = nbin;
-  if (fs.tbuf && tid == 0)  // diagnostics: (view, tile, coarse count) of this dispatch slot
+  if (fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, coarse count) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
@@ -420,10 +420,23 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
                                                               SoftArgs<float> a,
                                                               SoftPairBuf<float> pb) {
   __shared__ DibrTileLDS U;
+  TileClock clk(a.fs.tbuf, 1);  // diagnostics (flag 64): duration, start, raster-phase end
+  clk.start_to(2);
   int b, tl, nbin;
   tile_of_block(ra.bb, ra.fs.H, ra.fs.W, b, tl, nbin, ra.fs.dbg);
+  if (a.fs.tbuf && threadIdx.x == 0) {
+    const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
+    a.fs.tbuf[slot] = ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
+    const BinGeom &g = a.bb.g;  // the soft coarse bin's face count
+    const int tx = tl % pb.ntx, ty = tl / pb.ntx;
+    const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
+    a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
+  }
   raster_pairs_tile(ra, b, tl, nbin, U.r);
   __syncthreads();  // the raster phase is done with the LDS
+  if (a.fs.tbuf && threadIdx.x == 0)
+    a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
+        wall_clock64();
   soft_pairs_tile<float, true>(a, pb, b, tl, -1, U.s);
 }
 
@@ -770,7 +783,8 @@ bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) 
 int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
                           hipStream_t stream) {
   ra.fs.dbg = a.fs.dbg = debug_flags();
-  ra.fs.tbuf = a.fs.tbuf = nullptr;
+  ra.fs.tbuf = nullptr;
+  a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
     hipLaunchKernelGGL(kd_dibr_fwd_tiles, dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,

@@ -699,3 +699,44 @@ def test_dibr_rasterization_fused_matches_composition(dname):
     tol = dict(rtol=1e-4, atol=1e-5) if dname == 'f32' else dict(rtol=1e-9, atol=1e-10)
     torch.testing.assert_close(fvi_a.grad, fvi_b.grad, **tol)
     torch.testing.assert_close(ft_a.grad, ft_b.grad, **tol)
+
+
+@pytest.mark.parametrize('D', [3, 5])
+def test_dibr_fused_launches_match_split_launches(D):
+    """dibr_rasterization's one-launch forward (kd_dibr_fwd_tiles) and backward (kd_dibr_bwd)
+    against the same tile bodies as separate launches (debug flags 1<<26, 1<<24) on a 50k-face
+    mesh: identical forward outputs, gradients to summation-order tolerance.  (D = 5 keeps the
+    fused forward and the split backward.)"""
+    import math
+
+    from kaolin_amd import _lib, workloads
+    from kaolin_amd.render.mesh import dibr_rasterization, prepare_vertices
+    verts, faces, uvs = workloads.uv_sphere(250, 101, seed=0)
+    B, h, w = 3, 256, 192
+    cam = workloads.orbit_cameras(B, 0.4).to(DEV)
+    proj = workloads.generate_perspective_projection(math.pi / 4).to(DEV)
+    fvc, fvi, nrm = prepare_vertices(verts.to(DEV).unsqueeze(0), faces.to(DEV), proj,
+                                     camera_transform=cam)
+    F = faces.shape[0]
+    gen = torch.Generator().manual_seed(11)
+    feats = torch.rand((B, F, 3, D), generator=gen).to(DEV)
+    g1 = torch.rand((B, h, w, D), generator=gen).to(DEV)
+    g2 = torch.rand((B, h, w), generator=gen).to(DEV)
+    lib = _lib.load()
+    out = []
+    try:
+        for flags in (0, (1 << 24) | (1 << 26)):
+            lib.kd_debug_set(flags)
+            fa = fvi.detach().clone().requires_grad_(True)
+            ft = feats.clone().requires_grad_(True)
+            i, s, f = dibr_rasterization(h, w, fvc[..., 2], fa, ft, nrm[..., 2])
+            torch.autograd.backward([i, s], [g1, g2])
+            torch.cuda.synchronize()
+            out.append((i, s, f, fa.grad, ft.grad))
+    finally:
+        lib.kd_debug_set(0)
+    (i0, s0, f0, ga0, gf0), (i1, s1, f1, ga1, gf1) = out
+    assert (s0 < 1).any() and (f0 >= 0).any()
+    assert torch.equal(f0, f1) and torch.equal(i0, i1) and torch.equal(s0, s1)
+    torch.testing.assert_close(ga0, ga1, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gf0, gf1, rtol=1e-4, atol=1e-5)

@@ -1,5 +1,6 @@
-"""Dispatch-slot timeline of the fused soft-mask kernel (kd_debug_set flag 64): when do the
-heavy tiles start and end?  python tools/soft_timeline.py [config]"""
+"""Dispatch-slot timeline of the forward tile kernel (kd_dibr_fwd_tiles, or kd_soft_pairs with
+debug flag 1<<26; kd_debug_set flag 64): when do the heavy tiles start and end, and (fused) how
+long is each tile's raster phase?  python tools/soft_timeline.py [config] [extra debug flags]"""
 import os
 import sys
 
@@ -18,22 +19,31 @@ v = workloads.sphere_views(n_lon, n_lat, H, W, B, dev, elevation=elev)
 fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['normals_z']
 ntx, nty = (W + 15) // 16, (H + 15) // 16
 n = B * ntx * nty
-buf = torch.zeros(3 * n, dtype=torch.int64, device=dev)
+buf = torch.zeros(5 * n, dtype=torch.int64, device=dev)
+extra = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
 lib = _lib.load()
 lib.kd_debug_buffer(buf.data_ptr())
 for _ in range(3):
     dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
-lib.kd_debug_set(64)
+lib.kd_debug_set(64 | extra)
 dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
 lib.kd_debug_set(0)
 lib.kd_debug_buffer(None)
-t = buf.view(3, n).cpu().numpy()
+t = buf.view(5, n).cpu().numpy()
 dur = t[1] / 100.0          # us (100 MHz wall clock)
 start = (t[2] - t[2].min()) / 100.0
 end = start + dur
 print(f'kernel span {end.max():.1f} us, tiles {n}, sum {dur.sum() / 1e3:.2f} ms')
+if t[3].any():
+    rdur = (t[3] - t[2]) / 100.0
+    print(f'raster phase: sum {rdur.sum() / 1e3:.2f} ms, soft phase: sum '
+          f'{(dur - rdur).sum() / 1e3:.2f} ms')
+    for q in range(10):
+        sl = slice(q * n // 10, (q + 1) * n // 10)
+        print(f'  slots {sl.start:5d}: raster mean {rdur[sl].mean():6.1f} max {rdur[sl].max():6.1f}'
+              f'   soft mean {(dur - rdur)[sl].mean():6.1f} max {(dur - rdur)[sl].max():6.1f}')
 for q in range(10):
     sl = slice(q * n // 10, (q + 1) * n // 10)
     print(f'  slots {sl.start:5d}-{sl.stop:5d}: mean dur {dur[sl].mean():6.1f}  max dur '
@@ -51,6 +61,15 @@ for q in range(10):
     print(f'  {sl.start:5d}: unc {u_slot[sl].mean():6.1f}  nbin {nbin[sl].mean():7.1f}  heavy '
           f'{heavy.sum():4d}  heavy unc {u_slot[sl][heavy].mean() if heavy.any() else 0:6.1f} '
           f'heavy nbin {nbin[sl][heavy].mean() if heavy.any() else 0:7.1f}')
+if t[3].any():  # per-slot table for offline study: slot, tile, raster / soft bin counts, unc, us
+    out = os.path.join('gpurun_out', f'timeline_{cfg}.csv')
+    os.makedirs('gpurun_out', exist_ok=True)
+    with open(out, 'w') as fh:
+        fh.write('slot,tile,raster_nbin,soft_nbin,unc,start,raster_us,soft_us\n')
+        for i in range(n):
+            fh.write(f'{i},{tile[i]},{nbin[i]},{t[4][i]},{u_slot[i]},{start[i]:.2f},'
+                     f'{rdur[i]:.2f},{dur[i] - rdur[i]:.2f}\n')
+    print('wrote', out)
 late = np.argsort(end)[::-1][:10]
 print('latest ending (slot, start, dur):', [(int(i), round(float(start[i]), 1),
                                             round(float(dur[i]), 1)) for i in late])
