@@ -416,15 +416,19 @@ union DibrTileLDS {
   SoftPairsLDS<true> s;
 };
 
+// DIAG (debug flag 64 with a debug buffer): per dispatch slot the tile, its bin counts, start,
+// duration and raster-phase end (tools/soft_timeline.py).  A separate instantiation: the clock's
+// live registers alone make the kernel spill.
+template <bool DIAG>
 __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
                                                               SoftArgs<float> a,
                                                               SoftPairBuf<float> pb) {
   __shared__ DibrTileLDS U;
-  TileClock clk(a.fs.tbuf, 1);  // diagnostics (flag 64): duration, start, raster-phase end
-  clk.start_to(2);
+  TileClock clk(DIAG ? a.fs.tbuf : nullptr, 1);
+  if (DIAG) clk.start_to(2);
   int b, tl, nbin;
   tile_of_block(ra.bb, ra.fs.H, ra.fs.W, b, tl, nbin, ra.fs.dbg);
-  if (a.fs.tbuf && threadIdx.x == 0) {
+  if (DIAG && a.fs.tbuf && threadIdx.x == 0) {
     const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
     a.fs.tbuf[slot] = ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
     const BinGeom &g = a.bb.g;  // the soft coarse bin's face count
@@ -434,7 +438,7 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
   }
   raster_pairs_tile(ra, b, tl, nbin, U.r);
   __syncthreads();  // the raster phase is done with the LDS
-  if (a.fs.tbuf && threadIdx.x == 0)
+  if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
   soft_pairs_tile<float, true>(a, pb, b, tl, -1, U.s);
@@ -787,7 +791,8 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
-    hipLaunchKernelGGL(kd_dibr_fwd_tiles, dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
+    hipLaunchKernelGGL(a.fs.tbuf ? kd_dibr_fwd_tiles<true> : kd_dibr_fwd_tiles<false>,
+                       dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
                        stream, ra, a, pb);
   }
   const hipError_t e = hipGetLastError();

@@ -26,6 +26,7 @@ SLOT = {
     'kd::kd_bin_scatter<float>': 'kd_bin_scatter',
     'kd::kd_dibr_bwd<float>': 'kd_dibr_bwd',
     'kd::kd_dibr_fwd_tiles': 'kd_dibr_fwd',
+    'kd::kd_dibr_fwd_tiles<false>': 'kd_dibr_fwd',
 }
 
 
