@@ -1,20 +1,29 @@
 #!/usr/bin/env python
 """DIB-R forward+backward throughput on MI355X (BASELINE.json metric).
 
-One step = prepare_vertices (camera transform, projection, per-face gather, normals; fused HIP,
-kaolin_amd/csrc/kd_prepare.hip) -> dibr_rasterization (HIP: rasterize + soft mask) -> torch.autograd.backward(
-[interp, soft_mask], [g_feat, g_soft]) through the HIP backward kernels and the face->vertex
-scatter -> (N > 1) one RCCL all-reduce of the shared vertex gradient.  Inputs are resident in HBM
-before the timed region.  N GPUs: one process per GPU, each renders its own block of views of the
-same mesh (weak scaling: views per GPU fixed).
+One step = kaolin_amd.distributed.dibr_step: prepare_vertices (camera transform, projection,
+per-face gather, normals; fused HIP, kd_prepare.hip) -> dibr_rasterization (HIP: rasterize + soft
+mask) -> torch.autograd.backward([interp, soft_mask], [g_feat, g_soft]) through the HIP backward
+kernels and the face->vertex scatter -> (N > 1) one RCCL all-reduce of the shared vertex
+gradient.  Inputs are resident in HBM before the timed region.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--views-per-gpu B]
+Scaling: the headline config (C3) is a GLOBAL batch of 8 views split over the N GPUs (8/4/2/1
+views per GPU at N = 1/2/4/8: "strong").  With N > 1 a second timed phase renders the config's
+full batch on every GPU ("weak_scaling" field).  --views-per-gpu B makes the main line weak.
+
+The GPU part of the step is captured once in a HIP graph and replayed (GraphedStep; --no-graph
+runs it eagerly); the all-reduce stays an eager RCCL call.  Every kernel of the step runs in
+every replay.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--dtype f32|f64]
 For N > 1 launch with torch.distributed.run (see README / the driver contract).
 """
 import argparse
 import json
 import math
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -25,23 +34,24 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from kaolin_amd import _C, _lib, distributed, workloads  # noqa: E402
-from kaolin_amd.render.mesh import dibr, dibr_rasterization, prepare_vertices  # noqa: E402
+from kaolin_amd.render.mesh import dibr, dibr_rasterization  # noqa: E402
 
 METRIC = 'Mpixels/s DIB-R fwd+bwd, 50k-face mesh @512² bs=8, 1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
-# name -> (n_lon, n_lat, H, W, views per GPU, elevation); SURVEY.md §8(d) configs C2-C5
+# name -> (n_lon, n_lat, H, W, global batch, elevation); SURVEY.md §8(d) configs C2-C5
 CONFIGS = {
     'c2': (100, 51, 256, 256, 4, 0.3),
     'c3': (250, 101, 512, 512, 8, 0.3),
     'c4': (250, 101, 1024, 1024, 8, 0.3),
     'c5': (500, 201, 512, 512, 16, 0.6),
 }
-# name -> (faces, H, W, views per GPU): the C5 stress soup (workloads.soup, seed 3); a step is
+# name -> (faces, H, W, global batch): the C5 stress soup (workloads.soup, seed 3); a step is
 # dibr_rasterization fwd + bwd on per-view face soups (no shared mesh: no all-reduce)
 SOUP_CONFIGS = {
     'c5soup': (200000, 512, 512, 16),
 }
+DTYPES = {'f32': torch.float32, 'f64': torch.float64}
 
 
 def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4, fused=True):
@@ -89,11 +99,136 @@ def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4, f
 
 def survey_step_bytes(P, F, D, K, esize=4):
     """SURVEY.md §8(d) whole-step formula (K-lists counted as the reference writes them, the
-    N_read term omitted): bytes of one DIB-R fwd+bwd step."""
+    N_read term omitted): bytes of one DIB-R fwd+bwd step under the reference's op contract."""
     e = esize
     pix = (8 + 3 * e + D * e) + (8 + e + 13 * K) + (D * e + 8 + 3 * e) + (e + e + 8)
     face = (e * (3 + 6 + 3 * D) + 4) + 24 + 2 * (24 + 12 * D) + 2 * 24
     return P * pix + F * face
+
+
+class Workload:
+    """Inputs of one rank: views [first, first + n) of a global batch, resident on `dev`."""
+
+    def __init__(self, args, dev, first, n, total):
+        dt = DTYPES[args.dtype]
+        self.soup = args.config in SOUP_CONFIGS
+        self.n = n
+        kw = dict(sigmainv=args.sigmainv, boxlen=args.boxlen, knum=args.knum)
+        self.kw = kw
+        if self.soup:
+            F, H, W, _ = SOUP_CONFIGS[args.config]
+            sz, si, sn = workloads.soup(F, seed=3, batch=total, dtype=dt)
+            self.fvz = sz[first:first + n].to(dev).contiguous()
+            self.fvi = si[first:first + n].to(dev).contiguous().requires_grad_(True)
+            self.nz = sn[first:first + n].to(dev).contiguous()
+            g = torch.Generator().manual_seed(4)
+            uvs = torch.rand((total, F, 3, 2), generator=g, dtype=dt)[first:first + n].to(dev)
+            self.vertices = None
+            self.desc = f'soup({F}, seed=3) per view'
+        else:
+            n_lon, n_lat, H, W, _, elev = CONFIGS[args.config]
+            verts, faces, face_uvs = workloads.uv_sphere(n_lon, n_lat, seed=0, dtype=dt)
+            F = faces.shape[0]
+            self.vertices = verts.to(dev).requires_grad_(True)
+            self.faces = faces.to(dev)
+            self.cam = workloads.orbit_cameras(n, elev, first_view=first, total_views=total,
+                                               dtype=dt).to(dev)
+            self.proj = workloads.generate_perspective_projection(math.pi / 4, dtype=dt).to(dev)
+            uvs = face_uvs.to(dev).unsqueeze(0).repeat(n, 1, 1, 1)
+            self.desc = f'uv_sphere({n_lon},{n_lat}) {F} faces'
+        # learnable per-view, per-face-vertex features (uv + mask ones, ian_dibr.py:240-243)
+        self.feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
+        self.feats.requires_grad_(True)
+        self.F, self.H, self.W, self.D = F, H, W, self.feats.shape[-1]
+        g_feat, g_soft = workloads.view_grads(first, n, H, W, self.D, dtype=dt)
+        self.g_feat, self.g_soft = g_feat.to(dev), g_soft.to(dev)
+        self.params = [self.fvi, self.feats] if self.soup else [self.vertices, self.feats]
+
+    def forward_backward(self):
+        """The GPU part of the step (no collective)."""
+        if self.soup:
+            interp, soft, face_idx = dibr_rasterization(self.H, self.W, self.fvz, self.fvi,
+                                                        self.feats, self.nz, **self.kw)
+            torch.autograd.backward([interp, soft], [self.g_feat, self.g_soft])
+            return face_idx
+        return distributed.dibr_forward_backward(
+            self.vertices, self.faces, self.proj, self.cam, self.feats, self.H, self.W,
+            self.g_feat, self.g_soft, **self.kw)
+
+    def clear(self):
+        for p in self.params:
+            p.grad = None
+
+    def eager_step(self):
+        self.clear()
+        face_idx = self.forward_backward()
+        if not self.soup:
+            distributed.allreduce_grads_([self.vertices.grad])
+        return face_idx
+
+    def inputs(self):
+        """(fvz, fvi, normals_z) of the rank's views (detached)."""
+        with torch.no_grad():
+            if self.soup:
+                return self.fvz, self.fvi.detach(), self.nz
+            from kaolin_amd.render.mesh import prepare_vertices
+            fvc, fvi, nrm = prepare_vertices(self.vertices.detach().unsqueeze(0), self.faces,
+                                             self.proj, camera_transform=self.cam)
+            return fvc[..., 2], fvi, nrm[..., 2]
+
+
+def make_step(wl, use_graph):
+    """(callable step, launch description).  The graph holds the GPU part; the all-reduce of the
+    shared vertex gradient runs eagerly after each replay."""
+    if use_graph:
+        try:
+            gs = distributed.GraphedStep(wl.params, wl.forward_backward,
+                                         params_to_reduce=[] if wl.soup else [wl.vertices])
+            return gs, 'hip graph replay (GPU part) + eager RCCL all-reduce'
+        except Exception as e:  # noqa: BLE001 -- report and fall back to eager launches
+            torch.cuda.synchronize()
+            return wl.eager_step, f'eager (graph capture failed: {type(e).__name__}: {e})'[:200]
+    return wl.eager_step, 'eager'
+
+
+def timed(step, steps, warmup, dev, world):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def load_pmc(path, config, dtype, lists, views):
+    """Per-launch HBM traffic of each kernel from a committed PMC summary of the same workload:
+    FETCH_SIZE x 2 + WRITE_SIZE (MI355X_MICROARCH.md, HBM: gfx950's FETCH_SIZE reads half of a
+    wide streaming read; WRITE_SIZE is exact)."""
+    try:
+        with open(path) as f:
+            pm = json.load(f)
+    except (OSError, ValueError):
+        return {}, None
+    if (pm.get('config') != config or bool(pm.get('lists')) != lists or
+            pm.get('dtype', 'f32') != dtype or pm.get('views_per_gpu', views) != views):
+        return {}, None
+    out = {}
+    for k, ent in pm.get('kernels', {}).items():
+        if 'FETCH_SIZE_KiB' in ent and 'WRITE_SIZE_KiB' in ent:
+            out[k] = round((2 * ent['FETCH_SIZE_KiB'] + ent['WRITE_SIZE_KiB']) * 1024)
+    return out, os.path.relpath(path, ROOT)
 
 
 def main():
@@ -102,17 +237,20 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=3)
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS) + sorted(SOUP_CONFIGS))
-    ap.add_argument('--views-per-gpu', type=int, default=None)
+    ap.add_argument('--dtype', default='f32', choices=sorted(DTYPES))
+    ap.add_argument('--views-per-gpu', type=int, default=None,
+                    help='weak scaling: this many views on every GPU (default: the global batch '
+                         'of the config split over the GPUs)')
     ap.add_argument('--knum', type=int, default=30)
     ap.add_argument('--sigmainv', type=float, default=7000.)
     ap.add_argument('--boxlen', type=float, default=0.02)
     ap.add_argument('--lists', action='store_true',
                     help='materialise the (B,H,W,K) close-face lists (reference structure)')
+    ap.add_argument('--no-graph', action='store_true', help='launch every kernel eagerly')
+    ap.add_argument('--no-weak', action='store_true', help='skip the N > 1 weak-scaling phase')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--cpu-sample-views', type=int, default=8)
-    ap.add_argument('--cpu-min-seconds', type=float, default=10.0,
-                    help='repeat the CPU sample until at least this much CPU time has passed')
-    ap.add_argument('--pmc', default=os.path.join(ROOT, 'profiles', 'pmc_traffic.json'))
+    ap.add_argument('--pmc', default=None,
+                    help='PMC traffic summary (default profiles/r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
 
     # KD_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (ranks share cuda:0;
@@ -124,183 +262,141 @@ def main():
     dev = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     _lib.load()
-    dibr.SAVE_CLOSE_LISTS = args.lists
-
     soup = args.config in SOUP_CONFIGS
-    kw = dict(sigmainv=args.sigmainv, boxlen=args.boxlen, knum=args.knum)
-    if soup:
-        F, H, W, B_def = SOUP_CONFIGS[args.config]
-        Bl = args.views_per_gpu or B_def
-        first, _ = distributed.shard_views(Bl * world, rank, world)
-        sz, si, sn = workloads.soup(F, seed=3, batch=Bl * world)
-        sfvz = sz[first:first + Bl].to(dev).contiguous()
-        sfvi = si[first:first + Bl].to(dev).contiguous().requires_grad_(True)
-        snz = sn[first:first + Bl].to(dev).contiguous()
-        g = torch.Generator().manual_seed(4)
-        uvs = torch.rand((Bl, F, 3, 2), generator=g).to(dev)
-        feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
-        feats.requires_grad_(True)
-        n_lon = n_lat = None
-        verts = None
+    B_global = SOUP_CONFIGS[args.config][3] if soup else CONFIGS[args.config][4]
+    weak_main = args.views_per_gpu is not None
+    if weak_main:
+        total = args.views_per_gpu * world
+        first, n = rank * args.views_per_gpu, args.views_per_gpu
     else:
-        n_lon, n_lat, H, W, B_def, elev = CONFIGS[args.config]
-        Bl = args.views_per_gpu or B_def
-        first, _ = distributed.shard_views(Bl * world, rank, world)
-        verts, faces, face_uvs = workloads.uv_sphere(n_lon, n_lat, seed=0)
-        F = faces.shape[0]
-        vertices = verts.to(dev).requires_grad_(True)
-        faces = faces.to(dev)
-        cam = workloads.orbit_cameras(Bl, elev, first_view=first,
-                                      total_views=Bl * world).to(dev)
-        proj = workloads.generate_perspective_projection(math.pi / 4).to(dev)
-        uvs = face_uvs.to(dev).unsqueeze(0).repeat(Bl, 1, 1, 1)
-        feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
-        feats.requires_grad_(True)  # learnable per-face-vertex features: grad_feat is computed
-    D = feats.shape[-1]
-    g = torch.Generator().manual_seed(1)
-    g_feat = torch.rand((Bl, H, W, D), generator=g).to(dev)
-    g = torch.Generator().manual_seed(2)
-    g_soft = torch.rand((Bl, H, W), generator=g).to(dev)
-
-    def inputs():
-        if soup:
-            return sfvz, sfvi, snz
-        # one mesh, Bl cameras: vertices batch 1 broadcast over the views (utils.py:128-175)
-        fvc, fvi, nrm = prepare_vertices(vertices.unsqueeze(0), faces, proj,
-                                         camera_transform=cam)
-        return fvc[..., 2], fvi, nrm[..., 2]
-
-    def step():
-        fvz, fvi, nz = inputs()
-        interp, soft, face_idx = dibr_rasterization(H, W, fvz, fvi, feats, nz, **kw)
-        torch.autograd.backward([interp, soft], [g_feat, g_soft])
-        if soup:
-            sfvi.grad = None
-        else:
-            distributed.allreduce_grads_([vertices.grad])
-            vertices.grad = None
-        feats.grad = None
-        return face_idx
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    # ---- timed region --------------------------------------------------------------------
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        total = B_global
+        first, n = distributed.shard_views(B_global, rank, world)
+    use_graph = not args.no_graph and not args.lists and backend == 'nccl'
+    with dibr.close_lists(args.lists):
+        wl = Workload(args, dev, first, n, total)
+        step, launch = make_step(wl, use_graph)
+        elapsed = timed(step, args.steps, args.warmup, dev, world)
     ms_per_step = elapsed * 1e3 / args.steps
-    pixels = Bl * world * H * W
+    H, W = wl.H, wl.W
+    pixels = total * H * W
     value = pixels * args.steps / elapsed / 1e6
 
-    # ---- per-kernel durations: HIP events recorded on the launch stream, second pass ------
-    _lib.profile_enable(True)
-    face_idx = None
-    for _ in range(args.steps):
-        face_idx = step()
-    torch.cuda.synchronize(dev)
-    _lib.profile_enable(False)
-    prof = _lib.profile_collect()
-    fv = int((face_idx >= 0).sum().item())  # covered pixels (for the record)
+    weak = None
+    if world > 1 and not weak_main and not args.no_weak:
+        del step
+        with dibr.close_lists(args.lists):
+            wl2 = Workload(args, dev, rank * B_global, B_global, B_global * world)
+            step2, _ = make_step(wl2, use_graph)
+            el2 = timed(step2, args.steps, args.warmup, dev, world)
+        weak = {'value': round(B_global * world * H * W * args.steps / el2 / 1e6, 2),
+                'ms_per_step': round(el2 * 1e3 / args.steps, 4), 'views_per_gpu': B_global,
+                'global_batch': B_global * world}
+        del step2, wl2
 
-    with torch.no_grad():
-        fvz, fvi, nz = inputs()
-        fvi = fvi.detach()
-        Fv = int((nz >= 0).sum().item())
-    P = Bl * H * W
-    Ftot = Bl * F
-    V = 0 if soup else vertices.shape[0]
+    # ---- per-kernel durations: HIP events recorded on the launch stream, eager pass ---------
+    with dibr.close_lists(args.lists):
+        _lib.profile_enable(True)
+        for _ in range(args.steps):
+            face_idx = wl.eager_step()
+        torch.cuda.synchronize(dev)
+        _lib.profile_enable(False)
+    prof = _lib.profile_collect()
+    covered = int((face_idx >= 0).sum().item())
+
+    fvz, fvi, nz = wl.inputs()
+    Fv = int((nz >= 0).sum().item())
+    P = n * H * W
+    Ftot = n * wl.F
+    V = 0 if soup else wl.vertices.shape[0]
+    esize = 8 if args.dtype == 'f64' else 4
     pairs = None
     if not args.lists:
         with torch.no_grad():
             _, _, _, _, ws = _C.render.mesh.dibr_rasterization_forward_fused(
-                H, W, fvz, fvi, feats, nz, args.sigmainv, args.boxlen,
+                H, W, fvz, fvi, wl.feats.detach(), nz, args.sigmainv, args.boxlen,
                 args.knum, 1000., 1e-8, want_grad=True)
-            pairs = int(_lib.load().kd_dibr_pair_count(ws.data_ptr(), Bl, H, W, F, args.knum, 0,
-                                                       torch.cuda.current_stream(dev).cuda_stream))
+            pairs = int(_lib.load().kd_dibr_pair_count(
+                ws.data_ptr(), n, H, W, wl.F, args.knum, 1 if args.dtype == 'f64' else 0,
+                torch.cuda.current_stream(dev).cuda_stream))
             del ws
     fused = 'kd_soft_pair_math' not in prof  # the one-launch soft mask (kd_softpair.hip)
+    pmc_path = args.pmc or os.path.join(ROOT, 'profiles', 'r02',
+                                        f'pmc_traffic_{args.config}.json')
+    pmc, pmc_src = load_pmc(pmc_path, args.config, args.dtype, args.lists, n)
     kernels = {}
-    for name, (ms, n) in prof.items():
-        avg_us = ms * 1e3 / n
-        ab = algorithmic_bytes(name, P, Ftot, Fv, D, args.knum, args.lists, pairs, V,
+    moved = 0
+    for name, (ms, cnt) in prof.items():
+        avg_us = ms * 1e3 / cnt
+        ab = algorithmic_bytes(name, P, Ftot, Fv, wl.D, args.knum, args.lists, pairs, V, esize,
                                fused=fused)
-        kernels[name] = {'avg_us': round(avg_us, 2), 'launches': n,
+        kernels[name] = {'avg_us': round(avg_us, 2), 'launches': cnt,
                          'share': round(ms / max(sum(v[0] for v in prof.values()), 1e-9), 3)}
         if ab is not None:
             kernels[name]['alg_bytes'] = ab
             kernels[name]['GB_s'] = round(ab / (avg_us * 1e-6) / 1e9, 1)
+            moved += ab * cnt / args.steps
+        if name in pmc:
+            kernels[name]['traffic'] = pmc[name]
+            if ab:
+                kernels[name]['traffic_ratio'] = round(pmc[name] / ab, 3)
     dom = max(prof.items(), key=lambda kv: kv[1][0])[0] if prof else None
     roofline = None
     if dom is not None:
-        ms, n = prof[dom]
-        avg_s = ms / n / 1e3
-        ab = algorithmic_bytes(dom, P, Ftot, Fv, D, args.knum, args.lists, pairs, V,
-                               fused=fused)
+        ms, cnt = prof[dom]
+        avg_s = ms / cnt / 1e3
+        ab = kernels[dom].get('alg_bytes')
         achieved = ab / avg_s / 1e9 if ab else None
-        traffic = None
-        if os.path.exists(args.pmc):
-            try:
-                with open(args.pmc) as f:
-                    pm = json.load(f)
-                ent = pm.get('kernels', {}).get(dom)
-                if ent and pm.get('config') == args.config and bool(pm.get('lists')) == args.lists:
-                    traffic = ent.get('hbm_bytes_per_launch')
-            except (OSError, ValueError):
-                traffic = None
+        traffic = pmc.get(dom)
         roofline = {'kernel': dom, 'bound': 'hbm',
                     'achieved': None if achieved is None else round(achieved, 1),
                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                     'frac': None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
                     'traffic': traffic,
+                    'traffic_ratio': round(traffic / ab, 3) if traffic and ab else None,
+                    'traffic_source': pmc_src and f'{pmc_src}: FETCH_SIZE x 2 + WRITE_SIZE',
                     'alg_bytes_per_launch': ab, 'avg_launch_us': round(avg_s * 1e6, 2)}
+    ref_bytes = survey_step_bytes(P, Ftot, wl.D, args.knum, esize)
+    step_roof = {
+        'bytes_per_step_per_gpu': round(moved),
+        'formula': 'sum over the step\'s kernels of their algorithmic bytes per launch '
+                   '(the bytes this implementation must move)',
+        'achieved': round(moved / (ms_per_step * 1e-3) / 1e9, 1) if moved else None,
+        'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+        'frac': round(moved / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if moved else None,
+        'pairs_per_step': pairs,
+        'reference_contract': {
+            'formula': 'SURVEY.md §8(d): 482 B/px + 268 B/face at D=3, K=30, fp32 (the (B,H,W,K) '
+                       'close lists counted as the reference op writes them; N_read omitted)',
+            'bytes_per_step_per_gpu': ref_bytes,
+            'equivalent_GB_s': round(ref_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+            'note': 'not HBM traffic of this path: the K-lists are ' +
+                    ('written (--lists)' if args.lists else 'never materialised here')}}
 
-    sb = survey_step_bytes(P, Ftot, D, args.knum)
-    step_roof = {'formula': 'SURVEY.md §8(d): 482 B/px + 268 B/face at D=3, K=30 (K-lists as '
-                            'the reference writes them, N_read omitted)',
-                 'bytes_per_step_per_gpu': sb,
-                 'achieved': round(sb / (ms_per_step * 1e-3) / 1e9, 1), 'peak': HBM_PEAK_GBS,
-                 'unit': 'GB/s', 'frac': round(sb / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                 'pairs_per_step': pairs}
-
-    # ---- CPU baseline: the oracle (C port of the reference kernels), rank 0, N == 1 -------
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, fvz, fvi, nz, feats, g_feat, g_soft, H, W, kw)
+        cpu = cpu_baseline(wl, fvz, fvi, nz)
 
     out = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
-        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32',
-        'data': 'synthetic (seeded uv-sphere, orbit cameras; no dataset)',
-        'config': {'workload': f'{args.config.upper()}: ' +
-                               (f'soup({F}, seed=3) per view' if soup else
-                                f'uv_sphere({n_lon},{n_lat}) {F} faces') + ', '
-                               f'{H}x{W}, {Bl} views/GPU, D={D}, knum={args.knum}, '
+        'higher_is_better': True, 'scaling': 'weak' if weak_main else 'strong',
+        'vs_baseline': None, 'dtype': args.dtype,
+        'data': 'synthetic (seeded ' + ('triangle soup' if soup else 'uv-sphere, orbit cameras')
+                + '; no dataset)',
+        'config': {'workload': f'{args.config.upper()}: {wl.desc}, {H}x{W}, global batch '
+                               f'{total} ({n} views/GPU), D={wl.D}, knum={args.knum}, '
                                f'sigmainv={args.sigmainv:g}, boxlen={args.boxlen:g}',
-                   'faces': F, 'height': H, 'width': W, 'views_per_gpu': Bl,
-                   'global_batch': Bl * world,
+                   'faces': wl.F, 'height': H, 'width': W, 'views_per_gpu': n,
+                   'global_batch': total,
                    'parallelism': f'view-sharded x{world}' +
                                   (' + RCCL vertex-grad all-reduce'
                                    if world > 1 and not soup else ''),
+                   'launch': launch,
                    'close_lists': 'materialised' if args.lists else 'not materialised',
-                   'covered_px_per_step': fv, 'front_faces': Fv},
+                   'covered_px_per_step': covered, 'front_faces': Fv},
         'roofline': roofline,
         'step_roofline': step_roof,
+        'weak_scaling': weak,
         'cpu_baseline': cpu,
         'kernels': kernels,
     }
@@ -311,36 +407,62 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(args, fvz, fvi, nz, feats, g_feat, g_soft, H, W, kw):
-    """The CPU oracle (oracle/dibr_oracle.c, OpenMP) doing the same fwd+bwd on a bounded sample
-    (the first `--cpu-sample-views` views of the workload)."""
+def _cpu_model():
+    try:
+        txt = subprocess.run(['lscpu'], capture_output=True, text=True, timeout=10).stdout
+        for line in txt.splitlines():
+            if line.startswith('Model name'):
+                return line.split(':', 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return None
+
+
+def cpu_baseline(wl, fvz, fvi, nz, runs=5):
+    """The CPU oracle (oracle/dibr_oracle.c: the reference's brute-force loops in C, OpenMP) on a
+    bounded sample of the same workload, SURVEY.md §8(d) protocol: median of `runs` after one
+    warmup, on the box's host cores (OMP_NUM_THREADS) and on one thread.  Sample: the rank's
+    first view, fwd+bwd (all threads); rows 3/8..5/8 of it (one thread)."""
     import numpy as np
     import oracle
     threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or os.cpu_count()
-    oracle.set_num_threads(threads)
-    nb = max(1, min(args.cpu_sample_views, fvi.shape[0]))
-    n = lambda t: t[:nb].detach().cpu().numpy()  # noqa: E731
-    fvz_, fvi_, nz_, ft_ = n(fvz), n(fvi), n(nz), n(feats)
-    gf_, gs_ = n(g_feat), n(g_soft)
-    reps = 0
-    t0 = time.perf_counter()
-    while True:
-        interp, face_idx, weights = oracle.rasterize(H, W, fvz_, fvi_, ft_, nz_ >= 0)
+    H, W, kw = wl.H, wl.W, wl.kw
+    n = lambda t: np.ascontiguousarray(t[:1].detach().cpu().numpy())  # noqa: E731
+    fvz_, fvi_, nz_, ft_ = n(fvz), n(fvi), n(nz), n(wl.feats)
+    gf_, gs_ = n(wl.g_feat), n(wl.g_soft)
+
+    def once(rows):
+        t0 = time.perf_counter()
+        _, face_idx, weights = oracle.rasterize(H, W, fvz_, fvi_, ft_, nz_ >= 0, rows=rows)
         soft, prob, cidx, ctype, sfvi = oracle.soft_mask_forward(
-            fvi_, face_idx, kw['sigmainv'], kw['boxlen'], kw['knum'], 1000.)
+            fvi_, face_idx, kw['sigmainv'], kw['boxlen'], kw['knum'], 1000., rows=rows)
         oracle.rasterize_backward(gf_, face_idx, weights, fvi_, ft_, 1e-8)
         oracle.soft_mask_backward(gs_, soft, face_idx, prob, cidx, ctype, sfvi, kw['sigmainv'],
                                   1000.)
-        reps += 1
-        dt = time.perf_counter() - t0
-        if dt >= args.cpu_min_seconds:
-            break
-    px = nb * H * W * reps
-    return {'value': round(px / dt / 1e6, 5), 'unit': 'Mpixels/s', 'cores': threads,
-            'kind': 'port',
-            'sample': f'{nb} view(s) of the same workload ({nb * H * W} px, {fvi.shape[1]} '
-                      f'faces) x {reps} repetition(s), fwd+bwd, brute-force reference loops '
-                      f'(oracle/dibr_oracle.c, OpenMP), {dt:.2f} s'}
+        return time.perf_counter() - t0
+
+    def median_rate(px, rows):
+        once(rows)  # warmup
+        ts = [once(rows) for _ in range(runs)]
+        med = statistics.median(ts)
+        return px / med / 1e6, med, ts
+
+    oracle.set_num_threads(threads)
+    rate, med, ts = median_rate(H * W, None)
+    r0, r1 = (3 * H) // 8, (5 * H) // 8
+    oracle.set_num_threads(1)
+    rate1, med1, _ = median_rate((r1 - r0) * W, (r0, r1))
+    oracle.set_num_threads(threads)
+    return {'value': round(rate, 5), 'unit': 'Mpixels/s', 'cores': threads, 'kind': 'port',
+            'sample': f'1 view of the workload ({H}x{W} px, {fvi.shape[1]} faces), fwd+bwd, '
+                      f'brute-force reference loops (oracle/dibr_oracle.c, OpenMP, {threads} '
+                      f'threads): median of {runs} runs after 1 warmup = {med:.3f} s',
+            'runs_s': [round(t, 3) for t in ts],
+            'single_thread': {'value': round(rate1, 5), 'unit': 'Mpixels/s',
+                              'sample': f'rows {r0}..{r1 - 1} of the same view, 1 thread, '
+                                        f'median of {runs} after 1 warmup = {med1:.3f} s'},
+            'host': {'lscpu_model': _cpu_model(), 'nproc': os.cpu_count(),
+                     'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}}
 
 
 if __name__ == '__main__':

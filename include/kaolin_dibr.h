@@ -392,6 +392,26 @@ int kd_deftet_sparse_render_forward_f64(int batch, int64_t num_pixels, int64_t n
                                         const double *fvi, const double *feat, float eps,
                                         double *interp, int64_t *face_idx, double *weights,
                                         void *workspace, size_t workspace_bytes, void *stream);
+/* The reference's op form, _C.render.mesh.deftet_sparse_render_forward_cuda (bindings.cpp:81,
+ * deftet.cpp:48-106, called at deftet.py:292-299): the caller's face_bboxes (B, F, 4) =
+ * (xmin, ymin, xmax, ymax) for the half-open box test, and per pixel the first knum hits in
+ * face-index order, unsorted: face_idx (B, P, knum) int64, pixel_depths, w0, w1 (B, P, knum);
+ * empty slots -1 / -inf / 0 / 0 (deftet.cpp:88-94).  Same workspace as above. */
+int kd_deftet_sparse_render_forward_raw_f32(int batch, int64_t num_pixels, int64_t num_faces,
+                                            int knum, const float *fvz, const float *fvi,
+                                            const float *face_bboxes, const float *pixel_coords,
+                                            const float *render_ranges, float eps,
+                                            int64_t *face_idx, float *pixel_depths, float *w0,
+                                            float *w1, void *workspace, size_t workspace_bytes,
+                                            void *stream);
+int kd_deftet_sparse_render_forward_raw_f64(int batch, int64_t num_pixels, int64_t num_faces,
+                                            int knum, const double *fvz, const double *fvi,
+                                            const double *face_bboxes,
+                                            const double *pixel_coords,
+                                            const double *render_ranges, float eps,
+                                            int64_t *face_idx, double *pixel_depths, double *w0,
+                                            double *w1, void *workspace, size_t workspace_bytes,
+                                            void *stream);
 int kd_deftet_sparse_render_backward_f32(int batch, int64_t num_pixels, int64_t num_faces,
                                          int knum, int feat_dim, const float *grad_interp,
                                          const int64_t *face_idx, const float *weights,

@@ -8,6 +8,9 @@ Each call validates its arguments like ``at::checkAllSameGPU`` / ``checkAllConti
 reference's ``at::full(-1)`` / ``at::zeros`` pre-fills are not needed) and launches on the
 current HIP stream of the inputs' device.
 
+Also the reference's two DefTet operators (bindings.cpp:81-82, deftet.cpp:48-160) with their
+positional signatures: ``deftet_sparse_render_forward_cuda`` / ``_backward_cuda``.
+
 Extra entry points (used by kaolin_amd.render.mesh's autograd functions, not in the reference):
 ``rasterize_forward_fused``, ``rasterize_backward_autograd``, ``dibr_soft_mask_forward_fused``,
 ``dibr_soft_mask_backward_binned``.
@@ -652,6 +655,69 @@ def deftet_sparse_render_backward(grad_interp, face_idx, weights, face_vertices_
     return gfvi, gfeat
 
 
+def deftet_sparse_render_forward_cuda(face_vertices_z, face_vertices_image, face_bboxes,
+                                      pixel_coords, pixel_depth_ranges, knum, eps):
+    """deftet.cpp:48-106 (bindings.cpp:81) -> [selected_face_idx, pixel_depths, w0, w1]: per
+    pixel the first knum hits in face-index order, unsorted; empty slots -1 / -inf / 0 / 0."""
+    fn = 'deftet_sparse_render_forward_cuda'
+    dev = _check_same_gpu(fn, face_vertices_z=face_vertices_z,
+                          face_vertices_image=face_vertices_image, face_bboxes=face_bboxes,
+                          pixel_coords=pixel_coords, pixel_depth_ranges=pixel_depth_ranges)
+    _check_contiguous(fn, face_vertices_z=face_vertices_z,
+                      face_vertices_image=face_vertices_image, face_bboxes=face_bboxes,
+                      pixel_coords=pixel_coords, pixel_depth_ranges=pixel_depth_ranges)
+    B, F = face_vertices_z.shape[:2]
+    P = pixel_coords.shape[1]
+    _check_size(fn, 'face_vertices_z', face_vertices_z, (B, F, 3))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'face_bboxes', face_bboxes, (B, F, 4))
+    _check_size(fn, 'pixel_coords', pixel_coords, (B, P, 2))
+    _check_size(fn, 'pixel_depth_ranges', pixel_depth_ranges, (B, P, 2))
+    sfx = _sfx(face_vertices_z, fn)
+    _check_dtype(fn, face_vertices_z, face_vertices_image=face_vertices_image,
+                 face_bboxes=face_bboxes, pixel_coords=pixel_coords,
+                 pixel_depth_ranges=pixel_depth_ranges)
+    knum = int(knum)
+    if knum < 1:
+        raise RuntimeError(f'{fn}: knum must be >= 1, got {knum}')
+    opts = dict(device=dev, dtype=face_vertices_z.dtype)
+    face_idx = torch.empty((B, P, knum), device=dev, dtype=torch.long)
+    depths = torch.empty((B, P, knum), **opts)
+    w0 = torch.empty((B, P, knum), **opts)
+    w1 = torch.empty((B, P, knum), **opts)
+    nb = int(_lib.load().kd_deftet_workspace_size(B, F, 1 if sfx == 'f64' else 0))
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+    _lib.call(f'kd_deftet_sparse_render_forward_raw_{sfx}', B, P, F, knum, _ptr(face_vertices_z),
+              _ptr(face_vertices_image), _ptr(face_bboxes), _ptr(pixel_coords),
+              _ptr(pixel_depth_ranges), float(eps), _ptr(face_idx), _ptr(depths), _ptr(w0),
+              _ptr(w1), _ptr(ws), nb, _stream(dev))
+    return [face_idx, depths, w0, w1]
+
+
+def deftet_sparse_render_backward_cuda(grad_interpolated_features, face_idx, weights,
+                                       face_vertices_image, face_features, eps):
+    """deftet.cpp:108-160 (bindings.cpp:82) -> [grad_face_vertices_image, grad_face_features]"""
+    fn = 'deftet_sparse_render_backward_cuda'
+    _check_same_gpu(fn, grad_interpolated_features=grad_interpolated_features,
+                    face_idx=face_idx, weights=weights, face_vertices_image=face_vertices_image,
+                    face_features=face_features)
+    _check_contiguous(fn, grad_interpolated_features=grad_interpolated_features,
+                      face_idx=face_idx, weights=weights,
+                      face_vertices_image=face_vertices_image, face_features=face_features)
+    B, P, K, D = grad_interpolated_features.shape
+    F = face_vertices_image.shape[1]
+    _check_size(fn, 'face_idx', face_idx, (B, P, K))
+    _check_size(fn, 'weights', weights, (B, P, K, 3))
+    _check_size(fn, 'face_vertices_image', face_vertices_image, (B, F, 3, 2))
+    _check_size(fn, 'face_features', face_features, (B, F, 3, D))
+    _sfx(face_vertices_image, fn)
+    _check_dtype(fn, face_vertices_image, grad_interpolated_features=grad_interpolated_features,
+                 weights=weights, face_features=face_features)
+    gfvi, gfeat = deftet_sparse_render_backward(grad_interpolated_features, face_idx, weights,
+                                                face_vertices_image, face_features, eps)
+    return [gfvi, gfeat]
+
+
 render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     packed_rasterize_forward_cuda=packed_rasterize_forward_cuda,
     rasterize_backward_cuda=rasterize_backward_cuda,
@@ -670,6 +736,8 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     rast_interpolate=rast_interpolate,
     deftet_sparse_render_forward=deftet_sparse_render_forward,
     deftet_sparse_render_backward=deftet_sparse_render_backward,
+    deftet_sparse_render_forward_cuda=deftet_sparse_render_forward_cuda,
+    deftet_sparse_render_backward_cuda=deftet_sparse_render_backward_cuda,
 ))
 metrics = types.SimpleNamespace(mask_iou_forward=mask_iou_forward,
                                 mask_iou_backward=mask_iou_backward)

@@ -59,6 +59,8 @@ _SIGS = {
     'kd_rast_interpolate': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p, c_p, c_p],
     'kd_deftet_sparse_render_forward': [c_int, c_i64, c_i64, c_int, c_int, c_p, c_p, c_p, c_p,
                                         c_p, c_float, c_p, c_p, c_p, c_p, c_size, c_p],
+    'kd_deftet_sparse_render_forward_raw': [c_int, c_i64, c_i64, c_int, c_p, c_p, c_p, c_p, c_p,
+                                            c_float, c_p, c_p, c_p, c_p, c_p, c_size, c_p],
     'kd_deftet_sparse_render_backward': [c_int, c_i64, c_i64, c_int, c_int, c_p, c_p, c_p, c_p,
                                          c_p, c_float, c_p, c_p, c_p],
     'kd_texture_mapping_backward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,

@@ -64,9 +64,25 @@ __device__ __forceinline__ bool dt_box(const T *v, T &xmin, T &ymin, T &xmax, T 
 // lists[c * N + b * F] with room for all F faces of the view; cursor[b][c] = list length.
 // Neighbouring faces share cells, so a workgroup counts its 256 faces per cell in LDS, reserves
 // one range per touched cell with a single global atomic, and places its faces in it.
+// Box of face row i: the caller's (xmin, ymin, xmax, ymax) when given (the op form takes the
+// reference's face_bboxes argument, deftet.cpp:48-55), else the corners' min / max (deftet.py:287-289).
+template <typename T>
+__device__ __forceinline__ bool dt_face_box(const T *fvi, const T *bbox, int64_t i, T &xmin,
+                                            T &ymin, T &xmax, T &ymax) {
+  if (bbox) {
+    const T *q = bbox + i * 4;
+    xmin = q[0];
+    ymin = q[1];
+    xmax = q[2];
+    ymax = q[3];
+    return !(isnan(xmin) || isnan(xmax) || isnan(ymin) || isnan(ymax));
+  }
+  return dt_box<T>(fvi + i * 6, xmin, ymin, xmax, ymax);
+}
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_dt_bin(int64_t F, int64_t N, int G, const T *fvi,
-                                                    int *cursor, int *lists) {
+                                                    const T *bbox, int *cursor, int *lists) {
   __shared__ int s_cnt[kDtGridMax * kDtGridMax];
   const int b = blockIdx.y, cells = G * G;
   const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -74,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void kd_dt_bin(int64_t F, int64_t N, int G,
   __syncthreads();
   T xmin, ymin, xmax, ymax;
   int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
-  if (f < F && dt_box<T>(fvi + ((int64_t)b * F + f) * 6, xmin, ymin, xmax, ymax)) {
+  if (f < F && dt_face_box<T>(fvi, bbox, (int64_t)b * F + f, xmin, ymin, xmax, ymax)) {
     cx0 = dt_cell(xmin, G);
     cx1 = dt_cell(xmax, G);
     cy0 = dt_cell(ymin, G);
@@ -101,11 +117,21 @@ __global__ __launch_bounds__(kBlock) void kd_dt_bin(int64_t F, int64_t N, int G,
 // eps-normalised barycentrics (copysignf of the float eps, also for fp64 data), all >= 0, depth
 // in [min, max).
 template <typename T>
-__device__ __forceinline__ bool dt_face_test(const T *v, const T *z, T x0, T y0, T dmin, T dmax,
-                                             T eps, T &w0, T &w1, T &depth) {
+__device__ __forceinline__ bool dt_face_test(const T *v, const T *z, const T *bbox, T x0, T y0,
+                                             T dmin, T dmax, T eps, T &w0, T &w1, T &depth) {
   const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
-  const T xmin = nmin3(ax, bx, cx), xmax = nmax3(ax, bx, cx);
-  const T ymin = nmin3(ay, by, cy), ymax = nmax3(ay, by, cy);
+  T xmin, xmax, ymin, ymax;
+  if (bbox) {
+    xmin = bbox[0];
+    ymin = bbox[1];
+    xmax = bbox[2];
+    ymax = bbox[3];
+  } else {
+    xmin = nmin3(ax, bx, cx);
+    xmax = nmax3(ax, bx, cx);
+    ymin = nmin3(ay, by, cy);
+    ymax = nmax3(ay, by, cy);
+  }
   if (!(x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax)) return false;
   const T aex = ax - x0, aey = ay - y0, bex = bx - x0, bey = by - y0;
   const T cex = cx - x0, cey = cy - y0;
@@ -138,6 +164,10 @@ struct DtArgs {
   T *interp;          // (B, P, K, D)
   int64_t *face_idx;  // (B, P, K)
   T *weights;         // (B, P, K, 3)
+  // op form (deftet_sparse_render_forward_cuda, deftet_cuda.cu:31-192): the caller's boxes, and
+  // per slot in face-index order (unsorted) face, depth, w0, w1 instead of interp / weights
+  const T *bbox;      // (B, F, 4) or nullptr
+  T *depth, *w0, *w1; // (B, P, K) each, or nullptr (sorted mode)
 };
 
 constexpr int kDtWaves = 4;  // pixels per workgroup
@@ -170,6 +200,7 @@ __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
   const T dmin = a.range[2 * pp], dmax = a.range[2 * pp + 1];
   const T *fvi = a.fvi + (int64_t)b * a.F * 6;
   const T *fvz = a.fvz + (int64_t)b * a.F * 3;
+  const T *bbox = a.bbox ? a.bbox + (int64_t)b * a.F * 4 : nullptr;
   const T eps = (T)a.eps;
   const int G = a.G;
   const int c = dt_cell(y0, G) * G + dt_cell(x0, G);
@@ -185,8 +216,10 @@ __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
       int f = 0;
       if (j < nl) {
         f = list[j];
-        if (f < limit) hit = dt_face_test<T>(fvi + (int64_t)f * 6, fvz + (int64_t)f * 3, x0, y0,
-                                             dmin, dmax, eps, w0, w1, depth);
+        if (f < limit)
+          hit = dt_face_test<T>(fvi + (int64_t)f * 6, fvz + (int64_t)f * 3,
+                                bbox ? bbox + (int64_t)f * 4 : nullptr, x0, y0, dmin, dmax, eps,
+                                w0, w1, depth);
       }
       const uint64_t hm = __ballot(hit);
       if (store && hit) {
@@ -219,6 +252,30 @@ __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
   wave_lds_sync();
   // the reference keeps the first K hits by face index: mark the others (face rank >= K)
   int *frank = fid + C;
+  const int64_t row = pp * K;
+  if (a.depth) {
+    // op form: slot = face rank among the hits (the reference kernel's insertion order,
+    // deftet_cuda.cu:166-180), unsorted; the empty slots keep -1 / -inf / 0 / 0
+    // (deftet.cpp:88-94)
+    for (int i = lane; i < nh; i += kWave) {
+      const int fi = fid[i];
+      int r = 0;
+      for (int j = 0; j < nh; ++j) r += fid[j] < fi ? 1 : 0;
+      if (r < K) {
+        a.face_idx[row + r] = fi;
+        a.depth[row + r] = dep[i];
+        a.w0[row + r] = lw0[i];
+        a.w1[row + r] = lw1[i];
+      }
+    }
+    for (int s = min(nh, K) + lane; s < K; s += kWave) {
+      a.face_idx[row + s] = -1;
+      a.depth[row + s] = (T)-INFINITY;
+      a.w0[row + s] = (T)0;
+      a.w1[row + s] = (T)0;
+    }
+    return;
+  }
   const bool cut = nh > K;
   for (int i = lane; i < nh; i += kWave) {
     int r = 0;
@@ -232,7 +289,6 @@ __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
   // rank the kept hits: depth descending, then face index (deftet.py:300-303, stable order)
   const int n = cut ? K : nh;
   const int D = a.D;
-  const int64_t row = pp * K;
   const T *feat = a.feat + (int64_t)b * a.F * 3 * D;
   for (int i = lane; i < nh; i += kWave) {
     if (frank[i] >= K) continue;
@@ -277,7 +333,9 @@ static int dt_capacity(int K) { return K < 256 ? 256 : K; }
 template <typename T>
 static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, const T *range,
                       const T *fvz, const T *fvi, const T *feat, float eps, T *interp,
-                      int64_t *face_idx, T *weights, void *ws, size_t wsb, hipStream_t stream) {
+                      int64_t *face_idx, T *weights, void *ws, size_t wsb, hipStream_t stream,
+                      const T *bbox = nullptr, T *depth = nullptr, T *w0 = nullptr,
+                      T *w1 = nullptr) {
   KD_CHECK_ARG(B >= 0 && B <= 65535 && P >= 0 && F >= 0 && D >= 0, "deftet: bad sizes");
   KD_CHECK_ARG(K >= 1, "deftet: knum must be >= 1");
   KD_CHECK_ARG(F < (1ll << 31) && (int64_t)B * F < (1ll << 40), "deftet: too many faces");
@@ -298,10 +356,11 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
   if (F > 0) {
     ProfScope prof(K_DT_BIN, stream);
     hipLaunchKernelGGL(kd_dt_bin<T>, dim3((unsigned)((F + kBlock - 1) / kBlock), B),
-                       dim3(kBlock), 0, stream, F, N, G, fvi, cursor, lists);
+                       dim3(kBlock), 0, stream, F, N, G, fvi, bbox, cursor, lists);
   }
-  DtArgs<T> a{B, P, F, N, K, D, C, G, eps, px, range, fvz, fvi, feat, cursor, lists, interp,
-              face_idx, weights};
+  DtArgs<T> a{B,   P,      F,     N,      K,       D,        C,       G,
+              eps, px,     range, fvz,    fvi,     feat,     cursor,  lists,
+              interp, face_idx, weights, bbox, depth, w0, w1};
   const int64_t gx = (P + kDtWaves - 1) / kDtWaves;
   KD_CHECK_ARG(gx < (1ll << 31), "deftet: too many pixels");
   {
@@ -360,6 +419,29 @@ int kd_deftet_sparse_render_forward_f64(int B, int64_t P, int64_t F, int knum, i
                                         void *ws, size_t wsb, void *stream) {
   return dt_forward<double>(B, P, F, knum, D, pixel_coords, render_ranges, fvz, fvi, feat, eps,
                             interp, face_idx, weights, ws, wsb, (hipStream_t)stream);
+}
+int kd_deftet_sparse_render_forward_raw_f32(int B, int64_t P, int64_t F, int knum,
+                                            const float *fvz, const float *fvi,
+                                            const float *face_bboxes, const float *pixel_coords,
+                                            const float *render_ranges, float eps,
+                                            int64_t *face_idx, float *pixel_depths, float *w0,
+                                            float *w1, void *ws, size_t wsb, void *stream) {
+  KD_CHECK_ARG(face_idx && pixel_depths && w0 && w1, "deftet: NULL output");
+  return dt_forward<float>(B, P, F, knum, 0, pixel_coords, render_ranges, fvz, fvi, nullptr, eps,
+                           nullptr, face_idx, nullptr, ws, wsb, (hipStream_t)stream, face_bboxes,
+                           pixel_depths, w0, w1);
+}
+int kd_deftet_sparse_render_forward_raw_f64(int B, int64_t P, int64_t F, int knum,
+                                            const double *fvz, const double *fvi,
+                                            const double *face_bboxes,
+                                            const double *pixel_coords,
+                                            const double *render_ranges, float eps,
+                                            int64_t *face_idx, double *pixel_depths, double *w0,
+                                            double *w1, void *ws, size_t wsb, void *stream) {
+  KD_CHECK_ARG(face_idx && pixel_depths && w0 && w1, "deftet: NULL output");
+  return dt_forward<double>(B, P, F, knum, 0, pixel_coords, render_ranges, fvz, fvi, nullptr,
+                            eps, nullptr, face_idx, nullptr, ws, wsb, (hipStream_t)stream,
+                            face_bboxes, pixel_depths, w0, w1);
 }
 int kd_deftet_sparse_render_backward_f32(int B, int64_t P, int64_t F, int knum, int D,
                                          const float *grad_interp, const int64_t *face_idx,

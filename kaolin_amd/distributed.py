@@ -1,11 +1,16 @@
-"""View sharding across GPUs (one process per GPU) and the one exchange step of the path.
+"""View sharding across GPUs (one process per GPU), the one exchange step of the path, and the
+DIB-R training step that bench.py times and the multi-process tests run.
 
 The reference has no distributed code.  DIB-R views are independent through the
 whole forward and the per-view backward kernels (no cross-view terms: rasterization_cuda.cu:62,
 dibr_soft_mask_cuda.cu:47-51), so views are sharded in contiguous blocks and the only exchange is
 the sum over views of the shared mesh parameters' gradients -- the ``.repeat(batch_size, 1, 1)``
-backward of the reference training loop (examples/tutorial/ian_dibr.py:225-229) -- done as ONE
+backward of the reference training loop (examples/tutorial/ian_dibr.py:208-229) -- done as ONE
 bucketed all-reduce (RCCL over xGMI with backend "nccl"; gloo on CPU for tests).
+
+``dibr_step`` is that training step (prepare_vertices -> dibr_rasterization -> backward ->
+all-reduce); ``GraphedStep`` captures its GPU part (everything up to the all-reduce) in one HIP
+graph, so a step costs one graph launch plus one collective however few views a rank holds.
 """
 import os
 
@@ -39,11 +44,15 @@ def shard_views(total_views, rank, world):
     return first, base + (1 if rank < rem else 0)
 
 
+def _distributed(group=None):
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+
+
 def allreduce_grads_(tensors, group=None):
     """Sum `tensors` (e.g. shared-parameter .grad) over all ranks in place, as one flat bucket
     (one collective per step).  No-op when not distributed."""
     tensors = [t for t in tensors if t is not None]
-    if not tensors or not dist.is_initialized() or dist.get_world_size(group) == 1:
+    if not tensors or not _distributed(group):
         return tensors
     if len(tensors) == 1 and tensors[0].is_contiguous():  # in place: no pack / unpack kernels
         dist.all_reduce(tensors[0], op=dist.ReduceOp.SUM, group=group)
@@ -56,3 +65,118 @@ def allreduce_grads_(tensors, group=None):
         t.copy_(flat[off:off + n].view_as(t))
         off += n
     return tensors
+
+
+class EarlyReduce:
+    """Overlap for shared parameters whose gradients are final before the end of the backward
+    (e.g. a texture, whose gradient comes out of texture_mapping's backward before the DIB-R
+    backward runs): a post-accumulate hook starts their all-reduce asynchronously as soon as
+    autograd has written it, so the collective runs on RCCL's stream while the rest of the
+    backward runs on the compute stream.  ``wait()`` joins them.  The vertex gradient (the last
+    one produced) is reduced by the caller."""
+
+    def __init__(self, params, group=None):
+        self.group = group
+        self.works = []
+        self.handles = []
+        if _distributed(group):
+            for p in params:
+                self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
+
+    def _hook(self, p):
+        self.works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,
+                                          async_op=True))
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+
+    def remove(self):
+        for h in self.handles:
+            h.remove()
+        self.handles = []
+
+
+def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_features, height,
+                          width, grad_interp, grad_soft, sigmainv=7000., boxlen=0.02, knum=30,
+                          prepare=None, render=None):
+    """The GPU part of one DIB-R training step on this rank's views: project the
+    shared mesh to the rank's cameras (``prepare_vertices``, utils.py:128-175), render
+    (``dibr_rasterization``, dibr.py:119-209, valid faces = normals z >= 0) and back-propagate
+    the fixed upstream gradients ``[grad_interp, grad_soft]`` into ``vertices.grad`` (summed over
+    the rank's views) and the features' gradient.
+
+    vertices (V, 3) leaf, faces (F, 3) int64, camera_transform (B_rank, 4, 3), face_features
+    (B_rank, F, 3, D) or (1, F, 3, D) shared.  `prepare` / `render` default to the HIP kernels
+    (kaolin_amd.render.mesh); the CPU tests pass oracle-backed ones with the same signatures.
+    Returns face_idx (B_rank, H, W)."""
+    if prepare is None or render is None:
+        from .render.mesh import dibr_rasterization, prepare_vertices
+        prepare = prepare or prepare_vertices
+        render = render or dibr_rasterization
+    B = camera_transform.shape[0]
+    fvc, fvi, nrm = prepare(vertices.unsqueeze(0), faces, camera_proj,
+                            camera_transform=camera_transform)
+    feats = face_features if face_features.shape[0] == B else \
+        face_features.expand(B, *face_features.shape[1:])
+    interp, soft, face_idx = render(height, width, fvc[..., 2], fvi, feats, nrm[..., 2],
+                                    sigmainv, boxlen, knum)
+    torch.autograd.backward([interp, soft], [grad_interp, grad_soft])
+    return face_idx
+
+
+def dibr_step(vertices, faces, camera_proj, camera_transform, face_features, height, width,
+              grad_interp, grad_soft, sigmainv=7000., boxlen=0.02, knum=30, shared=(),
+              group=None, prepare=None, render=None):
+    """One DIB-R training step: ``dibr_forward_backward`` then the step's one exchange, a single
+    bucketed all-reduce of the shared parameters' gradients (vertices + `shared`, e.g. a feature
+    table shared by every view).  `shared` parameters are reduced early and asynchronously when
+    their gradients are final before the vertex gradient (``EarlyReduce``).  The caller resets
+    the .grad fields between steps (as an optimizer's zero_grad would)."""
+    early = EarlyReduce(shared, group)
+    try:
+        face_idx = dibr_forward_backward(vertices, faces, camera_proj, camera_transform,
+                                         face_features, height, width, grad_interp, grad_soft,
+                                         sigmainv, boxlen, knum, prepare, render)
+        late = [vertices.grad] + [p.grad for p in shared if not early.handles]
+        allreduce_grads_(late, group)
+        early.wait()
+    finally:
+        early.remove()
+    return face_idx
+
+
+class GraphedStep:
+    """``dibr_step`` with its GPU part captured once in a HIP graph (torch.cuda.CUDAGraph over
+    the library's stream-ordered launches) and replayed; the all-reduce of the shared gradients
+    stays an eager RCCL call after the replay.  Inputs and the .grad tensors are static: the
+    replay overwrites the gradients in place (they are None at capture, so the captured backward
+    assigns instead of accumulating).  `warmup` eager steps on a side stream come first (they
+    also build the per-topology vertex->face table, a one-time host copy)."""
+
+    def __init__(self, params, fn, params_to_reduce=None, group=None, warmup=3):
+        self.params = list(params)  # every parameter whose .grad the step writes
+        self.reduce = self.params if params_to_reduce is None else list(params_to_reduce)
+        self.fn = fn
+        self.group = group
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._clear()
+                fn()
+        torch.cuda.current_stream().wait_stream(s)
+        self._clear()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = fn()
+
+    def _clear(self):
+        for p in self.params:
+            p.grad = None
+
+    def __call__(self):
+        self.graph.replay()
+        allreduce_grads_([p.grad for p in self.reduce], self.group)
+        return self.out

@@ -6,20 +6,38 @@ boxes, runs the per-pixel all-faces scan and saves the (B, H, W, K) close-face l
 boxes are computed in the kernel, the scan runs over ordered tile bins, and by default the lists
 are NOT materialised: the forward keeps, per (pixel, close face) pair, the face and the pair's
 backward coefficients in its workspace (kd_softpair.hip), and the backward multiplies them by the
-incoming gradient and sums them per face and tile.  Set ``SAVE_CLOSE_LISTS = True`` to
-materialise the lists and use the reference-structured atomic backward instead (same results up
-to float-sum order).
+incoming gradient and sums them per face and tile.  Inside ``with close_lists():`` the lists are
+materialised and the reference-structured atomic backward is used instead (same results up to
+float-sum order); the switch is per thread, so it never changes another thread's graphs.
 """
+import contextlib
+import threading
+
 import torch
 from torch.autograd import Function
 
 from ... import _C
 from .rasterization import rasterize
 
-__all__ = ['dibr_soft_mask', 'dibr_rasterization']
+__all__ = ['dibr_soft_mask', 'dibr_rasterization', 'close_lists']
 
-#: materialise the (B, H, W, K) close-face lists in the autograd path (reference structure)
-SAVE_CLOSE_LISTS = False
+_tls = threading.local()
+
+
+def _lists_enabled():
+    return getattr(_tls, 'lists', False)
+
+
+@contextlib.contextmanager
+def close_lists(enabled=True):
+    """Within the block (this thread only), the autograd path materialises the (B, H, W, K)
+    close-face lists and uses the reference-structured backward (dibr.py:27-73)."""
+    old = _lists_enabled()
+    _tls.lists = bool(enabled)
+    try:
+        yield
+    finally:
+        _tls.lists = old
 
 
 class DibrSoftMaskCuda(Function):
@@ -30,7 +48,7 @@ class DibrSoftMaskCuda(Function):
                 multiplier):
         face_vertices_image = face_vertices_image.contiguous()
         selected_face_idx = selected_face_idx.contiguous()
-        lists = SAVE_CLOSE_LISTS
+        lists = _lists_enabled()
         want_grad = face_vertices_image.requires_grad and not lists
         soft_mask, workspace, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
             face_vertices_image, selected_face_idx, sigmainv, boxlen, knum, multiplier,
@@ -40,12 +58,14 @@ class DibrSoftMaskCuda(Function):
         ctx.boxlen = boxlen
         ctx.knum = knum
         ctx.lists = lists
-        ctx.workspace = None if lists else workspace
         if lists:
             ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, prob, cidx,
                                   ctype)
         else:
-            ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx)
+            # the workspace (records + probabilities) is a saved tensor like the reference's
+            # K-lists (dibr.py:51-54): it lives until autograd frees the graph, so a second
+            # backward over a retained graph reads the same records
+            ctx.save_for_backward(soft_mask, face_vertices_image, selected_face_idx, workspace)
         return soft_mask
 
     @staticmethod
@@ -59,11 +79,10 @@ class DibrSoftMaskCuda(Function):
                 grad_soft_mask, soft_mask, face_idx, prob, cidx, ctype,
                 (fvi * ctx.multiplier).contiguous(), ctx.sigmainv, ctx.multiplier)
         else:
-            soft_mask, fvi, face_idx = ctx.saved_tensors
+            soft_mask, fvi, face_idx, workspace = ctx.saved_tensors
             grad = _C.render.mesh.dibr_soft_mask_backward_binned(
                 grad_soft_mask, soft_mask, face_idx, fvi, ctx.multiplier, ctx.boxlen,
-                ctx.sigmainv, ctx.knum, ctx.workspace)
-            ctx.workspace = None
+                ctx.sigmainv, ctx.knum, workspace)
         return grad, None, None, None, None, None
 
 
@@ -85,6 +104,10 @@ class DibrRasterizationHip(Function):
     def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features,
                 face_normals_z, sigmainv, boxlen, knum, multiplier, eps):
         want_grad = face_vertices_image.requires_grad or face_features.requires_grad
+        # the kernels read dense rows; the backward must read the same copies the forward did
+        # (an expanded or permuted input would otherwise be read through the wrong strides)
+        face_vertices_image = face_vertices_image.contiguous()
+        face_features = face_features.contiguous()
         # the backward's gradient buffers, zeroed inside the forward's soft reduction
         bufs = None
         if want_grad:
@@ -96,8 +119,10 @@ class DibrRasterizationHip(Function):
         interp, face_idx, weights, soft, ws = _C.render.mesh.dibr_rasterization_forward_fused(
             height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z,
             sigmainv, boxlen, knum, multiplier, eps, want_grad=want_grad, grad_buffers=bufs)
-        ctx.save_for_backward(face_idx, weights, soft, face_vertices_image, face_features)
-        ctx.workspace = ws if want_grad else None
+        # the workspace is saved like the reference's K-lists (dibr.py:51-54): freed with the
+        # graph, kept for a second backward over a retained graph
+        ctx.save_for_backward(face_idx, weights, soft, face_vertices_image, face_features,
+                              ws if want_grad else None)
         ctx.grad_buffers = bufs
         ctx.params = (eps, multiplier, boxlen, sigmainv, knum)
         ctx.mark_non_differentiable(face_idx)
@@ -109,13 +134,14 @@ class DibrRasterizationHip(Function):
         need_fvi, need_feat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         if not (need_fvi or need_feat) or (grad_interp is None and grad_soft is None):
             return (None,) * 11
-        face_idx, weights, soft, fvi, feat = ctx.saved_tensors
+        face_idx, weights, soft, fvi, feat, workspace = ctx.saved_tensors
         eps, multiplier, boxlen, sigmainv, knum = ctx.params
+        # the forward zeroed one set of gradient buffers: the first backward fills them; a
+        # second backward (retained graph) gets fresh ones, zeroed by the backward itself
+        bufs, ctx.grad_buffers = ctx.grad_buffers, None
         gfvi, gfeat = _C.render.mesh.dibr_rasterization_backward_fused(
             grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier, boxlen,
-            sigmainv, knum, ctx.workspace, need_feat=need_feat, grad_buffers=ctx.grad_buffers)
-        ctx.workspace = None
-        ctx.grad_buffers = None
+            sigmainv, knum, workspace, need_feat=need_feat, grad_buffers=bufs)
         return (None, None, None, gfvi if need_fvi else None, gfeat, None, None, None, None,
                 None, None)
 
@@ -126,10 +152,10 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
     r"""DIB-R renderer (dibr.py:119-209): rasterize the front faces (normal z >= 0), then the
     soft mask over all faces.  Returns (interpolated_features, soft_mask, face_idx).
 
-    Runs as one fused forward / backward (DibrRasterizationHip); with ``SAVE_CLOSE_LISTS`` it is
+    Runs as one fused forward / backward (DibrRasterizationHip); inside ``close_lists()`` it is
     the reference composition of ``rasterize`` and ``dibr_soft_mask`` instead."""
     _multiplier = 1000. if multiplier is None else multiplier
-    if SAVE_CLOSE_LISTS or rast_backend != 'cuda':
+    if _lists_enabled() or rast_backend != 'cuda':
         # the reference composition (dibr.py:193-208); other backends go through rasterize
         interpolated_features, face_idx = rasterize(
             height, width, face_vertices_z, face_vertices_image, face_features,

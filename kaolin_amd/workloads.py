@@ -156,3 +156,19 @@ def sphere_views(n_lon, n_lat, height, width, batch, device, dtype=torch.float32
     return dict(vertices=verts, faces=faces, cam=cam, proj=proj, fvz=fvc[..., 2].contiguous(),
                 fvi=fvi.contiguous(), normals_z=nrm[..., 2].contiguous(), feats=feats,
                 height=height, width=width)
+
+
+def view_grads(first_view, num_views, height, width, feat_dim, seed=1, dtype=torch.float32):
+    """Upstream gradients of the bench step (g_feat ~ U(0,1), g_soft ~ U(0,1)),
+    drawn per GLOBAL view index, so a view gets the same numbers however the views are sharded.
+    Returns (g_feat (B, H, W, D), g_soft (B, H, W)) on the CPU."""
+    gf, gs = [], []
+    for v in range(first_view, first_view + num_views):
+        g = torch.Generator().manual_seed(seed * 1000003 + 2 * v)
+        gf.append(torch.rand((height, width, feat_dim), generator=g, dtype=dtype))
+        g = torch.Generator().manual_seed(seed * 1000003 + 2 * v + 1)
+        gs.append(torch.rand((height, width), generator=g, dtype=dtype))
+    if not gf:
+        return (torch.empty((0, height, width, feat_dim), dtype=dtype),
+                torch.empty((0, height, width), dtype=dtype))
+    return torch.stack(gf), torch.stack(gs)

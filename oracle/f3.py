@@ -17,6 +17,57 @@ naive renderer's outputs (tests/golden/deftet.npz, tests/golden/make_golden_f3.p
 import numpy as np
 
 
+def deftet_forward_raw(px, ranges, fvz, fvi, bbox, knum, eps=1e-8):
+    """The reference's op form (deftet.cpp:48-106, deftet_cuda.cu:31-190): the caller's boxes
+    bbox (B, F, 4) = (xmin, ymin, xmax, ymax) for the half-open test, and per pixel the first knum
+    hits in face-index order, unsorted -> face_idx (-1), pixel_depths (-inf), w0 (0), w1 (0)."""
+    B, P = px.shape[:2]
+    face_idx = np.full((B, P, knum), -1, np.int64)
+    depths = np.full((B, P, knum), -np.inf, fvi.dtype)
+    w0o = np.zeros((B, P, knum), fvi.dtype)
+    w1o = np.zeros((B, P, knum), fvi.dtype)
+    for b in range(B):
+        hit, depth, w0, w1, _ = _hits(px[b], ranges[b], fvz[b], fvi[b], eps, bbox[b])
+        for p in range(P):
+            fs = np.nonzero(hit[p])[0][:knum]
+            n = fs.size
+            face_idx[b, p, :n] = fs
+            depths[b, p, :n] = depth[p, fs]
+            w0o[b, p, :n] = w0[p, fs]
+            w1o[b, p, :n] = w1[p, fs]
+    return face_idx, depths, w0o, w1o
+
+
+def _hits(px, ranges, fvz, v, eps, bbox=None):
+    """(P, F) hit mask, depth, w0, w1, w2 of one view (deftet_cuda.cu:114-160)."""
+    dt = v.dtype.type
+    eps32 = np.float32(eps)
+    with np.errstate(invalid='ignore', divide='ignore', over='ignore'):
+        ax, ay, bx, by, cx, cy = (v[:, i // 2, i % 2][None, :] for i in range(6))
+        if bbox is None:
+            xmin, xmax = v[:, :, 0].min(axis=1)[None], v[:, :, 0].max(axis=1)[None]
+            ymin, ymax = v[:, :, 1].min(axis=1)[None], v[:, :, 1].max(axis=1)[None]
+        else:
+            xmin, ymin, xmax, ymax = (bbox[None, :, i] for i in range(4))
+        x0 = px[:, 0][:, None]
+        y0 = px[:, 1][:, None]
+        inbox = (x0 >= xmin) & (x0 < xmax) & (y0 >= ymin) & (y0 < ymax)
+        aex, aey, bex, bey = ax - x0, ay - y0, bx - x0, by - y0
+        cex, cey = cx - x0, cy - y0
+        w0_ = bex * cey - bey * cex
+        w1_ = cex * aey - cey * aex
+        w2_ = aex * bey - aey * bex
+        norm = w0_ + w1_ + w2_
+        ne = np.copysign(eps32, norm.astype(np.float32)).astype(dt)
+        w0 = w0_ / (norm + ne)
+        w1 = w1_ / (norm + ne)
+        w2 = w2_ / (norm + ne)
+        depth = w0 * fvz[None, :, 0] + w1 * fvz[None, :, 1] + w2 * fvz[None, :, 2]
+        hit = inbox & (w0 >= 0) & (w1 >= 0) & (w2 >= 0) & \
+            (depth < ranges[:, 1][:, None]) & (depth >= ranges[:, 0][:, None])
+    return hit, depth, w0, w1, w2
+
+
 def deftet_forward(px, ranges, fvz, fvi, feat, knum, eps=1e-8):
     dt = fvi.dtype.type
     B, P = px.shape[:2]

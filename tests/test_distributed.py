@@ -1,10 +1,12 @@
 """Multi-process (world size 2, gloo, CPU) tests of the view-sharded DIB-R step (SURVEY §8 e).
 
-The per-view renderer here is the CPU oracle (tests may use it); the code under test is the
-sharding and the one exchange step bench.py uses: ``distributed.shard_views`` +
-``workloads.orbit_cameras(first_view=...)`` and ``distributed.allreduce_grads_`` of the shared
-vertex gradient.  The summed vertex gradient of 2 ranks must equal the single-process gradient
-over all views (up to fp32 summation order).
+The code under test is the product's step, ``kaolin_amd.distributed.dibr_step`` -- the function
+bench.py times (prepare_vertices -> dibr_rasterization -> backward -> one bucketed all-reduce of
+the shared gradients, with early asynchronous reduction of shared parameters) -- together with
+``shard_views`` and ``workloads.orbit_cameras(first_view=...)``.  On CPU its two GPU stages are
+swapped for test doubles with the same signatures: the reference's PyTorch prepare_vertices
+composition and an autograd Function over the CPU oracle (tests may use it).  The summed
+gradients of 2 ranks must equal the single-process gradients over all views (fp32 sum order).
 """
 import math
 import os
@@ -31,55 +33,88 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _vertex_grad(first, nviews, total):
-    """Oracle DIB-R fwd+bwd for views [first, first+nviews) of `total`; returns vertices.grad."""
-    import oracle
+def _prepare(vertices, faces, camera_proj, camera_transform):
+    """The reference composition of prepare_vertices (utils.py:128-175), CPU."""
+    B = camera_transform.shape[0]
+    return workloads.prepare_vertices(vertices.expand(B, -1, -1), faces, camera_proj,
+                                      camera_transform)
+
+
+class _OracleDibr(torch.autograd.Function):
+    """dibr_rasterization (dibr.py:119-209) forward / backward through the CPU oracle."""
+
+    @staticmethod
+    def forward(ctx, height, width, fvz, fvi, feats, nz, sigmainv, boxlen, knum):
+        import oracle
+        n = lambda t: np.ascontiguousarray(t.detach().numpy())  # noqa: E731
+        interp, fidx, wts = oracle.rasterize(height, width, n(fvz), n(fvi), n(feats), n(nz) >= 0)
+        soft, prob, cidx, ctype, sfvi = oracle.soft_mask_forward(n(fvi), fidx, sigmainv, boxlen,
+                                                                 knum, 1000.)
+        ctx.state = (fidx, wts, n(fvi), n(feats), soft, prob, cidx, ctype, sfvi, sigmainv)
+        fi = torch.as_tensor(fidx)
+        ctx.mark_non_differentiable(fi)
+        return torch.as_tensor(interp), torch.as_tensor(soft), fi
+
+    @staticmethod
+    def backward(ctx, g_interp, g_soft, _):
+        import oracle
+        fidx, wts, fvi, feats, soft, prob, cidx, ctype, sfvi, sigmainv = ctx.state
+        gr, gfeat = oracle.rasterize_backward(g_interp.numpy(), fidx, wts, fvi, feats, 1e-8)
+        gs = oracle.soft_mask_backward(g_soft.numpy(), soft, fidx, prob, cidx, ctype, sfvi,
+                                       sigmainv, 1000.)
+        return (None, None, None, torch.as_tensor(gr + gs), torch.as_tensor(gfeat), None, None,
+                None, None)
+
+
+def _render(height, width, fvz, fvi, feats, nz, sigmainv, boxlen, knum):
+    return _OracleDibr.apply(height, width, fvz, fvi, feats, nz, sigmainv, boxlen, knum)
+
+
+def _rank_step(first, nviews, total, shared):
+    """dibr_step on views [first, first+nviews) of `total`; returns (vertices.grad, feature
+    table grad or None)."""
     verts, faces, face_uvs = workloads.uv_sphere(12, 9, seed=0)
     vertices = verts.clone().requires_grad_(True)
     cam = workloads.orbit_cameras(nviews, 0.3, first_view=first, total_views=total)
     proj = workloads.generate_perspective_projection(math.pi / 4)
-    fvc, fvi, nrm = workloads.prepare_vertices(vertices.unsqueeze(0).expand(nviews, -1, -1),
-                                               faces, proj, cam)
-    uvs = face_uvs.unsqueeze(0).repeat(nviews, 1, 1, 1)
-    feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1)
-    n = lambda t: t.detach().numpy()  # noqa: E731
-    interp, fidx, wts = oracle.rasterize(H, W, n(fvc[..., 2]), n(fvi), n(feats),
-                                         n(nrm[..., 2]) >= 0)
-    soft, prob, cidx, ctype, sfvi = oracle.soft_mask_forward(n(fvi), fidx, 7000, 0.02, 30, 1000.)
+    table = torch.cat([face_uvs, torch.ones_like(face_uvs[..., :1])], dim=-1).unsqueeze(0)
+    if shared:  # one feature table shared by every view: its gradient is reduced too
+        feats = table.clone().requires_grad_(True)
+        params = (feats,)
+    else:
+        feats = table.repeat(nviews, 1, 1, 1).requires_grad_(True)
+        params = ()
     # per-view upstream grads seeded by the GLOBAL view index (same numbers however sharded)
-    g_feat = np.stack([np.random.default_rng(100 + first + b).random((H, W, 3), np.float32)
-                       for b in range(nviews)])
-    g_soft = np.stack([np.random.default_rng(200 + first + b).random((H, W), np.float32)
-                       for b in range(nviews)])
-    gfvi_r, _ = oracle.rasterize_backward(g_feat, fidx, wts, n(fvi), n(feats), 1e-8)
-    gfvi_s = oracle.soft_mask_backward(g_soft, soft, fidx, prob, cidx, ctype, sfvi, 7000, 1000.)
-    torch.autograd.backward(fvi, torch.as_tensor(gfvi_r + gfvi_s))
-    return vertices.grad.detach().clone()
+    g_feat, g_soft = workloads.view_grads(first, nviews, H, W, 3)
+    distributed.dibr_step(vertices, faces, proj, cam, feats, H, W, g_feat, g_soft,
+                          shared=params, prepare=_prepare, render=_render)
+    return vertices.grad.detach().clone(), (feats.grad.detach().clone() if shared else None)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, shared, q):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     try:
         r, wsz, _ = distributed.init_from_env('gloo')
         first, nv = distributed.shard_views(TOTAL_VIEWS, r, wsz)
-        g = _vertex_grad(first, nv, TOTAL_VIEWS)
-        distributed.allreduce_grads_([g])
-        q.put((r, first, nv, g.numpy()))
+        gv, gf = _rank_step(first, nv, TOTAL_VIEWS, shared)
+        q.put((r, first, nv, gv.numpy(), None if gf is None else gf.numpy()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # surface the failure to the parent
-        q.put((rank, 'error', repr(e), None))
+        q.put((rank, 'error', repr(e), None, None))
 
 
 @pytest.mark.parametrize('world', [2])
-def test_sharded_step_matches_single_process(world):
+@pytest.mark.parametrize('shared', [False, True])
+def test_sharded_step_matches_single_process(world, shared):
     import oracle
     oracle.lib()  # build the checker once, before the workers load it
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, shared, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
@@ -92,11 +127,13 @@ def test_sharded_step_matches_single_process(world):
     spans = [(r[1], r[2]) for r in res]
     assert spans[0][0] == 0 and sum(s[1] for s in spans) == TOTAL_VIEWS
     assert all(spans[i][0] + spans[i][1] == spans[i + 1][0] for i in range(world - 1))
-    # every rank holds the same all-reduced gradient == the single-process full-batch gradient
-    ref = _vertex_grad(0, TOTAL_VIEWS, TOTAL_VIEWS).numpy()
+    # every rank holds the same all-reduced gradients == the single-process full-batch ones
+    ref_v, ref_f = _rank_step(0, TOTAL_VIEWS, TOTAL_VIEWS, shared)
     for r in res:
-        np.testing.assert_allclose(r[3], ref, rtol=1e-4, atol=1e-5)
-    assert np.abs(ref).sum() > 0
+        np.testing.assert_allclose(r[3], ref_v.numpy(), rtol=1e-4, atol=1e-5)
+        if shared:
+            np.testing.assert_allclose(r[4], ref_f.numpy(), rtol=1e-4, atol=1e-5)
+    assert np.abs(ref_v.numpy()).sum() > 0
 
 
 def test_shard_views_partition():

@@ -157,3 +157,88 @@ def test_large_knum_and_edges():
     assert interp.shape == (1, 0, 4, 3)
     with pytest.raises(RuntimeError):
         deftet_sparse_render(T(px), T(rr), T(fvz), T(fvi), T(feat), 100000)
+
+
+# --------------------------------------------------------------------------------------------
+# the reference's op form: _C.render.mesh.deftet_sparse_render_{forward,backward}_cuda
+# --------------------------------------------------------------------------------------------
+class _RefGlue(torch.autograd.Function):
+    """kaolin/render/mesh/deftet.py:269-330 (DeftetSparseRenderer) written against the op form,
+    as an unmodified reference deftet.py would call it after swapping its ``_C`` import (the
+    INTEGRATION.md level-2 drop-in).  Sort: stable (the reference's argsort ties are unpinned)."""
+
+    @staticmethod
+    def forward(ctx, pixel_coords, render_ranges, fvz, fvi, feat, knum, eps):
+        from kaolin_amd import _C
+        B, F, D = fvz.shape[0], fvz.shape[1], feat.shape[-1]
+        P = pixel_coords.shape[1]
+        bboxes = torch.cat((torch.min(fvi, dim=2)[0], torch.max(fvi, dim=2)[0]), dim=2)
+        face_idx, depth, w0, w1 = _C.render.mesh.deftet_sparse_render_forward_cuda(
+            fvz.contiguous(), fvi.contiguous(), bboxes, pixel_coords.contiguous(),
+            render_ranges.contiguous(), knum, eps)
+        order = torch.argsort(depth, descending=True, dim=-1, stable=True)
+        sfi = torch.gather(face_idx, -1, order).contiguous()
+        sw0, sw1 = torch.gather(w0, -1, order), torch.gather(w1, -1, order)
+        sw2 = (sfi != -1).to(fvi.dtype) - (sw0 + sw1)
+        idx = (sfi + 1).reshape(B, -1, 1, 1).expand(B, P * knum, 3, D)
+        sel = torch.gather(torch.nn.functional.pad(feat, (0, 0, 0, 0, 1, 0), value=0.), 1,
+                           idx).reshape(B, P, knum, 3, D)
+        weights = torch.stack([sw0, sw1, sw2], dim=-1).contiguous()
+        interp = torch.sum(weights.unsqueeze(-1) * sel, dim=-2).contiguous()
+        ctx.save_for_backward(sfi, weights, fvi, feat)
+        ctx.mark_non_differentiable(sfi)
+        ctx.eps = eps
+        return interp, sfi
+
+    @staticmethod
+    def backward(ctx, g, _):
+        from kaolin_amd import _C
+        sfi, weights, fvi, feat = ctx.saved_tensors
+        gfvi, gfeat = _C.render.mesh.deftet_sparse_render_backward_cuda(
+            g.contiguous(), sfi, weights, fvi.contiguous(), feat.contiguous(), ctx.eps)
+        return None, None, None, gfvi, gfeat, None, None
+
+
+@pytest.mark.parametrize('k', ['f32', 'f64'])
+@pytest.mark.parametrize('P', [31, 1025])
+@pytest.mark.parametrize('knum', [20, 30])
+def test_reference_op_form_vs_goldens(g, k, P, knum):
+    center = 1
+    key = f'{P}_{center}_{knum}_{k}'
+    px, rr = g[f'sphere_px_{P}_{k}'], g[f'sphere_rr_{P}_{center}_{k}']
+    fvz, fvi, uvs = g[f'sphere_fvz_{k}'], g[f'sphere_fvi_{k}'], g[f'sphere_uvs_{k}']
+    tfvi, tfeat = T(fvi).requires_grad_(True), T(uvs).requires_grad_(True)
+    interp, fidx = _RefGlue.apply(T(px), T(rr), T(fvz), tfvi, tfeat, knum, 1e-8)
+    np.testing.assert_array_equal(N(fidx), g[f'sphere_face_idx_{key}'])
+    np.testing.assert_allclose(N(interp), g[f'sphere_interp_{key}'], rtol=1e-4, atol=1e-4)
+    go = grad_out(g[f'sphere_interp_{key}'].shape, fvi.dtype, 1000 + P + 10 * center + knum)
+    gfvi, gfeat = torch.autograd.grad(interp, [tfvi, tfeat], T(go))
+    np.testing.assert_allclose(N(gfvi), g[f'sphere_grad_fvi_{key}'], rtol=5e-3, atol=5e-3)
+    np.testing.assert_allclose(N(gfeat), g[f'sphere_grad_feat_{key}'], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize('dt', [np.float32, np.float64])
+@pytest.mark.parametrize('knum', [1, 20])
+@pytest.mark.parametrize('boxes', ['tight', 'enlarged'])
+def test_reference_op_form_raw_vs_oracle(dt, knum, boxes):
+    """The raw op outputs (unsorted, face order, -1 / -inf / 0 / 0 padding) bit-exact against the
+    op-form oracle, with the caller's boxes honoured (an enlarged box admits no extra hit: the
+    barycentric test still applies; a shrunk box below removes hits)."""
+    from kaolin_amd import _C
+    px, rr, fvz, fvi, feat = soup(2, 3000, 700, dt, knum + 7, nan_faces=5)
+    bbox = np.concatenate([fvi.min(2), fvi.max(2)], -1)
+    if boxes == 'enlarged':
+        bbox = bbox + np.array([-0.05, -0.05, 0.05, 0.05], dt)
+    bbox[:, ::3] = bbox[:, ::3] * dt(0.5)  # shrink every third box towards the origin
+    fi, d, a0, a1 = _C.render.mesh.deftet_sparse_render_forward_cuda(
+        T(fvz), T(fvi), T(bbox), T(px), T(rr), knum, 1e-8)
+    ofi, od, oa0, oa1 = f3.deftet_forward_raw(px, rr, fvz, fvi, bbox, knum)
+    assert (ofi >= 0).sum(-1).max() == knum
+    np.testing.assert_array_equal(N(fi), ofi)
+    np.testing.assert_array_equal(N(d), od)
+    np.testing.assert_array_equal(N(a0), oa0)
+    np.testing.assert_array_equal(N(a1), oa1)
+    with pytest.raises(RuntimeError):  # the reference's checkAllContiguous
+        _C.render.mesh.deftet_sparse_render_forward_cuda(
+            T(fvz), T(fvi).transpose(-1, -2).contiguous().transpose(-1, -2), T(bbox), T(px),
+            T(rr), knum, 1e-8)

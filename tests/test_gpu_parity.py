@@ -215,14 +215,10 @@ def test_simple_soft_mask_backward(simple_golden, dname, sigmainv, boxlen, multi
     tag = f'{sigmainv}_{boxlen}'
     fvi = T(g['simple_fvi'].astype(DTYPES[dname])).requires_grad_(True)
     face_idx = T(g['simple_new_face_idx'].astype(np.int64))
-    old = dibr.SAVE_CLOSE_LISTS
-    dibr.SAVE_CLOSE_LISTS = lists
-    try:
+    with dibr.close_lists(lists):
         soft = dibr_soft_mask(fvi, face_idx, sigmainv, boxlen, knum, multiplier)
         loss = mask_iou(soft, shifted_mask(face_idx))
         loss.backward()
-    finally:
-        dibr.SAVE_CLOSE_LISTS = old
     np.testing.assert_allclose(N(soft), g[f'simple_soft_{tag}'], atol=1e-5, rtol=1e-5)
     np.testing.assert_allclose(N(fvi.grad), g[f'simple_grad_{tag}'], rtol=1e-5, atol=1e-5)
 
@@ -382,13 +378,9 @@ def test_c5_soup_rows_and_grad_consistency():
     grads = []
     for lists in (False, True):
         fvi = fvi0.clone().requires_grad_(True)
-        old = dibr.SAVE_CLOSE_LISTS
-        dibr.SAVE_CLOSE_LISTS = lists
-        try:
+        with dibr.close_lists(lists):
             interp, soft, face_idx = dibr_rasterization(h, w, fvz, fvi, feats, nz)
             torch.autograd.backward([interp, soft], [g_feat, g_soft])
-        finally:
-            dibr.SAVE_CLOSE_LISTS = old
         grads.append(fvi.grad)
         if not lists:
             out = (interp, soft, face_idx)

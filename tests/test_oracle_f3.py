@@ -55,3 +55,24 @@ def test_sphere_vs_naive(g, k, P, center, knum):
     gfvi, gfeat = oracle.rasterize_backward(go, fidx, w, fvi, uvs, 1e-8)
     np.testing.assert_allclose(gfvi, g[f'sphere_grad_fvi_{key}'], rtol=5e-3, atol=5e-3)
     np.testing.assert_allclose(gfeat, g[f'sphere_grad_feat_{key}'], rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize('k', ['f32', 'f64'])
+@pytest.mark.parametrize('knum', [20, 30])
+def test_raw_op_oracle_sorts_to_the_goldens(g, k, knum):
+    """The op-form oracle (deftet_forward_raw: the reference kernel's unsorted first-knum hits,
+    deftet_sparse_render_forward_cuda) sorted by depth like deftet.py:300-303 gives the golden
+    face indices."""
+    P, center = 1025, 1
+    fvi = g[f'sphere_fvi_{k}']
+    bbox = np.concatenate([fvi.min(2), fvi.max(2)], -1)  # deftet.py:287-289
+    fidx, depth, w0, w1 = f3.deftet_forward_raw(g[f'sphere_px_{P}_{k}'],
+                                                g[f'sphere_rr_{P}_{center}_{k}'],
+                                                g[f'sphere_fvz_{k}'], fvi, bbox, knum)
+    m = fidx >= 0  # hits first (ascending face index), padding last
+    assert (m[..., 1:] <= m[..., :-1]).all()
+    assert (np.diff(fidx, axis=-1)[m[..., 1:]] > 0).all()
+    assert np.isneginf(depth[fidx < 0]).all() and (w0[fidx < 0] == 0).all()
+    order = np.argsort(-depth, axis=-1, kind='stable')
+    np.testing.assert_array_equal(np.take_along_axis(fidx, order, -1),
+                                  g[f'sphere_face_idx_{P}_{center}_{knum}_{k}'])

@@ -1,9 +1,10 @@
-"""Turn a tools/pmc_summary.py summary.json into profiles/pmc_traffic.json for bench.py.
+"""Turn a tools/pmc_summary.py summary.json into profiles/rNN/pmc_traffic_<config>.json for
+bench.py.  Usage: make_traffic.py SUMMARY OUT CONFIG [DTYPE VIEWS_PER_GPU [lists]]
 
 HBM bytes per launch (MI355X_MICROARCH.md, HBM / rocprofv3): FETCH_SIZE and WRITE_SIZE are KiB
-per dispatch, collected in separate passes; the gfx950 FETCH_SIZE x2 correction applies to wide
-(16 B/lane) streaming reads only -- our kernels read 4-8 B per lane scattered through L2, so the
-raw figure is used as `traffic` and the x2 variant is kept beside it."""
+per dispatch, collected in separate passes; traffic = FETCH_SIZE x 2 + WRITE_SIZE (gfx950's
+FETCH_SIZE tallies half the bytes of a read; WRITE_SIZE is exact).  bench.py recomputes the
+same sum from the raw KiB stored here."""
 import json
 import sys
 
@@ -30,20 +31,23 @@ SLOT = {
 }
 
 
-def main(summary, out, config, lists=False):
+def main(summary, out, config, dtype='f32', views=8, lists=False):
     src = json.load(open(summary))
     kern = {}
     for name, m in src.items():
         slot = SLOT.get(name)
         if slot is None or 'hbm_bytes_raw' not in m:
             continue
-        kern[slot] = {'device_kernel': name, 'hbm_bytes_per_launch': round(m['hbm_bytes_raw']),
-                      'hbm_bytes_fetch_x2': round(m['hbm_bytes_fetch_x2']),
+        kern[slot] = {'device_kernel': name,
+                      'hbm_bytes_per_launch': round(m['hbm_bytes_fetch_x2']),
                       'FETCH_SIZE_KiB': m['FETCH_SIZE'], 'WRITE_SIZE_KiB': m['WRITE_SIZE']}
-    json.dump({'config': config, 'lists': lists, 'source': summary, 'kernels': kern},
-              open(out, 'w'), indent=1)
+    json.dump({'config': config, 'dtype': dtype, 'views_per_gpu': views, 'lists': lists,
+               'source': summary, 'traffic': 'FETCH_SIZE x 2 + WRITE_SIZE (KiB x 1024)',
+               'kernels': kern}, open(out, 'w'), indent=1)
     print(json.dumps(kern, indent=1))
 
 
 if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else 'c3')
+    a = sys.argv[1:]
+    main(a[0], a[1], a[2] if len(a) > 2 else 'c3', a[3] if len(a) > 3 else 'f32',
+         int(a[4]) if len(a) > 4 else 8, len(a) > 5 and a[5] == 'lists')
