@@ -67,11 +67,11 @@ def test_dibr_rasterization_retained_graph_twice(dname):
     # backward() twice accumulates: 2x the single gradient
     torch.autograd.backward([interp, soft], [g1, g2], retain_graph=True)
     torch.autograd.backward([interp, soft], [g1, g2])
-    assert torch.equal(a[0], b[0]) or torch.allclose(a[0], b[0], rtol=1e-6, atol=0)
-    assert torch.allclose(a[1], b[1], rtol=1e-6, atol=0)
-    torch.testing.assert_close(fvi.grad, 2 * a[0], rtol=1e-6, atol=1e-7)
-    torch.testing.assert_close(feats.grad, 2 * a[1], rtol=1e-6, atol=1e-7)
-    # and the gradient is the oracle's
+    # equal up to the float atomics' summation order
+    for x, y in ((a[0], b[0]), (a[1], b[1]), (fvi.grad, 2 * a[0]), (feats.grad, 2 * a[1])):
+        scale = y.abs().max().item()
+        torch.testing.assert_close(x, y, rtol=1e-5, atol=1e-6 * scale)
+    # and both gradients are the oracle's
     valid = N(nz) >= 0
     _, rf, rw = oracle.rasterize(h, h, N(fvz), N(fvi), N(feats), valid)
     np.testing.assert_array_equal(N(face_idx), rf)
@@ -80,8 +80,10 @@ def test_dibr_rasterization_retained_graph_twice(dname):
     gs = oracle.soft_mask_backward(N(g2), osoft, rf, oprob, ocidx, octype, sfvi, 7000, 1000.)
     tol = 1e-4 if dname == 'f32' else 1e-9
     ref = gr + gs
-    np.testing.assert_allclose(N(a[0]), ref, rtol=tol, atol=tol * 0.1 * np.abs(ref).max())
-    np.testing.assert_allclose(N(a[1]), gfeat, rtol=tol, atol=tol * 0.1 * np.abs(gfeat).max())
+    for x in (a, b):
+        np.testing.assert_allclose(N(x[0]), ref, rtol=tol, atol=tol * 0.1 * np.abs(ref).max())
+        np.testing.assert_allclose(N(x[1]), gfeat, rtol=tol,
+                                   atol=tol * 0.1 * np.abs(gfeat).max())
 
 
 @pytest.mark.parametrize('dname', ['f32', 'f64'])
@@ -99,8 +101,8 @@ def test_dibr_soft_mask_retained_graph_twice(dname, lists):
     a = torch.autograd.grad(soft, fvi, g, retain_graph=True)[0]
     b = torch.autograd.grad(soft, fvi, g, retain_graph=True)[0]
     c = torch.autograd.grad(soft, fvi, g)[0]  # frees the graph
-    torch.testing.assert_close(a, b, rtol=1e-6, atol=1e-7 * a.abs().max().item())
-    torch.testing.assert_close(a, c, rtol=1e-6, atol=1e-7 * a.abs().max().item())
+    torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6 * a.abs().max().item())
+    torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-6 * a.abs().max().item())
     with pytest.raises(RuntimeError):
         torch.autograd.grad(soft, fvi, g)  # freed like any PyTorch graph
     osoft, oprob, ocidx, octype, sfvi = oracle.soft_mask_forward(N(fvi), N(face_idx))
