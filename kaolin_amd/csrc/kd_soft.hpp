@@ -5,54 +5,27 @@
 
 #include "kd_binning.hpp"
 #include "kd_capi.hpp"
+#include "kd_softdist.hpp"
 #include "kd_tile.hpp"
 
 #include <type_traits>
 
 namespace kd {
 
-#define KD_SOFT_EPS 1e-7  // dibr_soft_mask_cuda.cu:23 (a double literal)
+// v_rcp_f32: the approximate reciprocal of soft_face_dist_fast (<= 1 ulp)
+struct DeviceRcp {
+  __device__ float operator()(float x) const { return __builtin_amdgcn_rcpf(x); }
+};
 
-__device__ __forceinline__ float kexp(float x) { return expf(x); }
-__device__ __forceinline__ double kexp(double x) { return exp(x); }
-
-// dibr_soft_mask_cuda.cu:100-163: squared distance type (0..5) and probability of one face.
+// dibr_soft_mask_cuda.cu:100-163: squared distance type (0..5) and probability of one face,
+// bit-identical to the reference (kd_softdist.hpp; fp32 through the exact filter).
 template <typename T>
 __device__ __forceinline__ void soft_face_dist(T x0, T y0, const T v[6], float M, float sigmainv,
                                                int &edgeid, T &prob) {
-  T pdis[6];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int j = (i + 1) % 3;
-    const T x1 = v[i * 2], y1 = v[i * 2 + 1], x2 = v[j * 2], y2 = v[j * 2 + 1];
-    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-    const T up = A * x0 + Bc * y0 + C;
-    const T down = A * A + Bc * Bc;
-    T x3 = Bc * Bc * x0 - A * Bc * y0 - A * C;
-    T y3 = A * A * y0 - A * Bc * x0 - Bc * C;
-    x3 = (T)((double)x3 / ((double)down + KD_SOFT_EPS));
-    y3 = (T)((double)y3 / ((double)down + KD_SOFT_EPS));
-    const T direct = (x3 - x1) * (x3 - x2) + (y3 - y1) * (y3 - y2);
-    if (direct > (T)0)
-      pdis[i] = (T)(4.0f * M * M);
-    else
-      pdis[i] = (T)((double)(up * up) / ((double)down + KD_SOFT_EPS));
-  }
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const T x1 = v[i * 2], y1 = v[i * 2 + 1];
-    pdis[i + 3] = (x0 - x1) * (x0 - x1) + (y0 - y1) * (y0 - y1);
-  }
-  edgeid = 0;
-  T d = pdis[0];
-#pragma unroll
-  for (int i = 1; i < 6; ++i)
-    if (d > pdis[i]) {
-      d = pdis[i];
-      edgeid = i;
-    }
-  const T z = (T)sigmainv * d / (T)M / (T)M;
-  prob = kexp(-z);
+  if constexpr (std::is_same<T, float>::value)
+    soft_face_dist_fast(x0, y0, v, M, sigmainv, edgeid, prob, DeviceRcp());
+  else
+    soft_face_dist_ref<T>(x0, y0, v, M, sigmainv, edgeid, prob);
 }
 
 // backward terms of one (pixel, close face) pair, dibr_soft_mask_cuda.cu:281-348; adds to the
