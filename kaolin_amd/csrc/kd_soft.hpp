@@ -12,20 +12,12 @@
 
 namespace kd {
 
-// v_rcp_f32: the approximate reciprocal of soft_face_dist_fast (<= 1 ulp)
-struct DeviceRcp {
-  __device__ float operator()(float x) const { return __builtin_amdgcn_rcpf(x); }
-};
-
 // dibr_soft_mask_cuda.cu:100-163: squared distance type (0..5) and probability of one face,
-// bit-identical to the reference (kd_softdist.hpp; fp32 through the exact filter).
+// bit-identical to the reference (kd_softdist.hpp).
 template <typename T>
 __device__ __forceinline__ void soft_face_dist(T x0, T y0, const T v[6], float M, float sigmainv,
                                                int &edgeid, T &prob) {
-  if constexpr (std::is_same<T, float>::value)
-    soft_face_dist_fast(x0, y0, v, M, sigmainv, edgeid, prob, DeviceRcp());
-  else
-    soft_face_dist_ref<T>(x0, y0, v, M, sigmainv, edgeid, prob);
+  soft_face_dist_ref<T>(x0, y0, v, M, sigmainv, edgeid, prob);
 }
 
 // backward terms of one (pixel, close face) pair, dibr_soft_mask_cuda.cu:281-348; adds to the
