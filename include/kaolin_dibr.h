@@ -61,6 +61,14 @@ const char *kd_profile_kernel_name(int id);
 int kd_debug_set(int flags);
 int kd_debug_buffer(void *device_ptr);
 
+/* Pool limits (a test and tuning hook; both 1 by default).  The workspaces hold two bounded
+ * pools whose layout depends only on the call's sizes: the coarse bins (16 entries per face row)
+ * and the soft mask's (pixel, close face) records (min(knum, 12) per pixel plus block slack).
+ * A forward uses the given fraction of each; what does not fit takes the overflow paths (a bin
+ * walks all faces of its view; a tile computes its soft mask without records and its backward
+ * recomputes them), which change the time, never the results.  Values in [0, 1]. */
+int kd_set_pool_limits(double bin_fraction, double pair_fraction);
+
 /* ---------------------------------------------------------------------------------------------
  * Packed rasterize forward.  Replaces _C.render.mesh.packed_rasterize_forward_cuda
  * (reference kaolin/csrc/bindings.cpp:77 -> kaolin/csrc/render/mesh/rasterization.cpp:49-104,

@@ -105,6 +105,8 @@ def load():
             lib.kd_debug_set.restype = c_int
             lib.kd_debug_buffer.argtypes = [c_p]
             lib.kd_debug_buffer.restype = c_int
+            lib.kd_set_pool_limits.argtypes = [ctypes.c_double, ctypes.c_double]
+            lib.kd_set_pool_limits.restype = c_int
             lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
             lib.kd_prepare_vertices_ranges.restype = c_i64
             # diagnostics only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
@@ -132,6 +134,14 @@ def workspace_size(kind, B, H, W, n_total, max_per_view):
 
 def soft_mask_workspace_size(B, H, W, F, knum, double_precision):
     return int(load().kd_soft_mask_workspace_size(B, H, W, F, knum, 1 if double_precision else 0))
+
+
+def set_pool_limits(bins=1.0, pairs=1.0):
+    """Fractions of the bin and record pools a forward may use (kd_set_pool_limits): a test
+    hook that forces the overflow paths; 1, 1 restores the default."""
+    call_plain = load().kd_set_pool_limits(float(bins), float(pairs))
+    if call_plain != KD_OK:
+        raise RuntimeError(load().kd_last_error().decode(errors='replace'))
 
 
 def profile_enable(on=True):

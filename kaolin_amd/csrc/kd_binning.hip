@@ -19,7 +19,9 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view)
   s += align_up(sizeof(Span) * (size_t)N);
   s += align_up(sizeof(int) * (size_t)B * (size_t)(nchunk > 0 ? nchunk : 1) * g.nct());
   s += align_up(sizeof(int) * (size_t)B * g.nct());
-  s += align_up(sizeof(int) * (size_t)g.nct() * (size_t)(N > 0 ? N : 1));
+  s += align_up(sizeof(int) * (size_t)B * g.nct());
+  s += align_up(sizeof(int) * (size_t)(B > 0 ? B : 1));
+  s += align_up(sizeof(int) * (size_t)kBinEntriesPerFace * (size_t)(N > 0 ? N : 1));
   s += align_up(sizeof(float4) * 2 * (size_t)N);
   s += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
   return s;
@@ -37,8 +39,14 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   off += align_up(sizeof(int) * (size_t)B * (size_t)(bb.nchunk > 0 ? bb.nchunk : 1) * bb.g.nct());
   bb.totals = (int *)(base + off);
   off += align_up(sizeof(int) * (size_t)B * bb.g.nct());
+  bb.base = (int *)(base + off);
+  off += align_up(sizeof(int) * (size_t)B * bb.g.nct());
+  bb.cursor = (int *)(base + off);
+  off += align_up(sizeof(int) * (size_t)(B > 0 ? B : 1));
   bb.bins = (int *)(base + off);
-  off += align_up(sizeof(int) * (size_t)bb.g.nct() * (size_t)(N > 0 ? N : 1));
+  bb.xper = kBinEntriesPerFace;
+  bb.limit = pool_limit_bins();
+  off += align_up(sizeof(int) * (size_t)kBinEntriesPerFace * (size_t)(N > 0 ? N : 1));
   bb.cull = (float4 *)(base + off);
   off += align_up(sizeof(float4) * 2 * (size_t)N);
   bb.order = (int2 *)(base + off);
@@ -131,6 +139,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   const int nct = bb.g.nct();
   for (int c = tid; c < nct; c += kBlock) s_cnt[c] = 0;
   if (bb.clear && b == 0 && chunk == 0 && tid < bb.n_clear) bb.clear[tid] = 0;
+  if (chunk == 0 && tid == 0) bb.cursor[b] = 0;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   __syncthreads();
@@ -176,27 +185,33 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 // One wave per (coarse tile, view, set), four per workgroup: exclusive scan of counts[b][*][c]
 // over the chunks.  Lane l owns the contiguous run of chunks [l*per, l*per + per), held in
 // registers; the run sums are scanned with DPP (wave_incl_scan).  No LDS, no barriers: every
-// wave's loads are in flight at once and the grid is one round on the chip.
-__global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers bb1) {
-  const BinBuffers &bb = blockIdx.z ? bb1 : bb0;
+// wave's loads are in flight at once and the grid is one round on the chip.  Then the
+// workgroup's four bins take their room in the view's region with one atomic on its cursor; a
+// bin past the usable end of the region is marked overflowed (base -1, see kd_binning.hpp).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
+  const FaceSet<T> &fs = jobs.fs[blockIdx.z];
+  const BinBuffers &bb = jobs.bb[blockIdx.z];
+  __shared__ int s_tot[kBlock / kWave], s_base;
   const int nct = bb.g.nct();
-  const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+  const int wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * (kBlock / kWave) + wv;
   const int b = blockIdx.y, lane = threadIdx.x & (kWave - 1);
-  if (c >= nct) return;
   const int n = bb.nchunk;
   const int per = (n + kWave - 1) / kWave;
   int *base = bb.counts + (int64_t)b * n * nct + c;
   constexpr int kMaxPer = 16;  // register-held run (n <= 1024 chunks = 262k faces per view)
   int v[kMaxPer];
   int local = 0;
-  if (per <= kMaxPer) {
+  const bool live = c < nct;
+  if (live && per <= kMaxPer) {
 #pragma unroll
     for (int k = 0; k < kMaxPer; ++k) {
       const int j = lane * per + k;
       v[k] = (k < per && j < n) ? base[(int64_t)j * nct] : 0;
       local += v[k];
     }
-  } else {
+  } else if (live) {
     for (int k = 0; k < per; ++k) {
       const int j = lane * per + k;
       if (j < n) local += base[(int64_t)j * nct];
@@ -205,7 +220,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers
   const int incl = wave_incl_scan(local);
   int run = incl - local;  // exclusive prefix of this lane's run
   const int total = __builtin_amdgcn_readlane(incl, kWave - 1);
-  if (per <= kMaxPer) {
+  if (live && per <= kMaxPer) {
 #pragma unroll
     for (int k = 0; k < kMaxPer; ++k) {
       const int j = lane * per + k;
@@ -214,7 +229,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers
         run += v[k];
       }
     }
-  } else {
+  } else if (live) {
     for (int k = 0; k < per; ++k) {
       const int j = lane * per + k;
       if (j < n) {
@@ -224,7 +239,24 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinBuffers bb0, BinBuffers
       }
     }
   }
-  if (lane == 0) bb.totals[(int64_t)b * nct + c] = total;
+  if (lane == 0) s_tot[wv] = live ? total : 0;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int sum = 0;
+#pragma unroll
+    for (int k = 0; k < kBlock / kWave; ++k) sum += s_tot[k];
+    s_base = sum > 0 ? atomicAdd(&bb.cursor[b], sum) : 0;
+  }
+  __syncthreads();
+  if (live && lane == 0) {
+    int off = s_base;
+    for (int k = 0; k < wv; ++k) off += s_tot[k];
+    int64_t lo, hi;
+    view_range(fs, b, lo, hi);
+    const int64_t room = (int64_t)((double)bb.limit * (double)bb.xper * (double)(hi - lo));
+    bb.totals[(int64_t)b * nct + c] = total;
+    bb.base[(int64_t)b * nct + c] = (int64_t)off + total <= room ? off : -1;
+  }
 }
 
 template <typename T>
@@ -265,6 +297,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
   }
   __syncthreads();
   const int *offs = bb.counts + ((int64_t)b * bb.nchunk + chunk) * nct;
+  const int *bbase = bb.base + (int64_t)b * nct;
+  int *bins = bb.bins + (int64_t)bb.xper * lo;
 #pragma unroll
   for (int u = 0; u < kPerT; ++u) {
     if (span_empty(sp[u])) continue;
@@ -275,10 +309,12 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
     for (int cy = sp[u].y0 / bb.g.ct; cy <= sp[u].y1 / bb.g.ct; ++cy)
       for (int cx = sp[u].x0 / bb.g.ct; cx <= sp[u].x1 / bb.g.ct; ++cx) {
         const int c = cy * bb.g.nctx + cx;
+        const int bc = bbase[c];
+        if (bc < 0) continue;  // overflowed: its tiles walk all faces of the view
         const uint32_t *m = s_mask + c * kWords;
         int rank = __popc(m[word] & (bit - 1u));
         for (int k = 0; k < word; ++k) rank += __popc(m[k]);
-        bb.bins[(int64_t)c * fs.N + lo + offs[c] + rank] = local;
+        bins[bc + offs[c] + rank] = local;
       }
   }
 }
@@ -368,8 +404,11 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
         const hipError_t e = hipMemsetAsync(b.clear, 0, sizeof(int) * b.n_clear, stream);
         if (e != hipSuccess) return e;
       }
-      const hipError_t e = hipMemsetAsync(
+      hipError_t e = hipMemsetAsync(
           b.totals, 0, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * b.g.nct(), stream);
+      if (e != hipSuccess) return e;
+      e = hipMemsetAsync(b.base, 0, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * b.g.nct(),
+                         stream);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -382,8 +421,7 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
   }
   {
     ProfScope prof(K_BIN_SCAN, stream);
-    hipLaunchKernelGGL(kd_bin_scan, grid_t, dim3(kBlock), 0, stream, jobs.bb[0],
-                       jobs.bb[njobs - 1]);
+    hipLaunchKernelGGL(kd_bin_scan<T>, grid_t, dim3(kBlock), 0, stream, jobs);
   }
   {  // + one column of workgroups for the tile order (kd_bin_scatter, tile_order)
     // kChunk-bit masks per coarse tile: up to 64 KB of dynamic LDS at 1024 coarse tiles (a

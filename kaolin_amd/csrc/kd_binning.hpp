@@ -7,7 +7,9 @@
 // order, produced without sorting by a three-pass counting scatter:
 //   1. kd_bin_count   one workgroup per (256-face chunk, view): each face computes its exact
 //                     pixel span (kd::make_span), stores it, and counts per coarse tile in LDS.
-//   2. kd_bin_scan    one wave per (coarse tile, view): exclusive scan over the chunks.
+//   2. kd_bin_scan    one wave per (coarse tile, view): exclusive scan over the chunks; each
+//                     workgroup (4 bins of a view) then takes its bins' room from the view's
+//                     region with one atomic.
 //   3. kd_bin_scatter one workgroup per (chunk, view): the rank of a face inside its chunk for a
 //                     tile is a popcount over an LDS bitmask of the chunk's faces touching that
 //                     tile, so the global position is scan offset + rank: ascending by face.
@@ -15,8 +17,14 @@
 //   spans  [N]           Span (8 B)
 //   counts [B][nchunk][nct] int32 (turned into exclusive offsets by the scan)
 //   totals [B][nct]      int32
-//   bins   [nct][N]      int32 local face index; the (b, c) bin starts at c*N + first[b] and has
-//                        room for the view's whole face count.
+//   base   [B][nct]      int32 start of bin (b, c) inside view b's region, -1 = overflowed
+//   cursor [B]           int32 allocation cursor of each view's region (kd_bin_scan)
+//   bins   [xper * N]    int32 local face index; view b owns the region [xper*lo, xper*hi) of
+//                        its rows [lo, hi) and kd_bin_scan hands each of its bins a contiguous
+//                        piece of it (one atomic per 4 bins).  A bin that does not fit is marked
+//                        overflowed: its tiles walk every face of the view (entry e = face e),
+//                        which the exact span filter of the walk turns into the same face list,
+//                        so an overflow costs time, never correctness.
 //   cull   [N][2]        float4: fp32 raster edge-culling coefficients (raster_cull_coefs), only
 //                        written when BinBuffers::cull is set (fp32 rasterization).
 //   order  [B * tiles]   int2 (view * tiles + fine tile, coarse bin face count), heaviest
@@ -27,11 +35,18 @@
 
 namespace kd {
 
+// Region entries per face row (xper): 16 covers a face whose box reaches 4 x 4 coarse tiles.
+constexpr int kBinEntriesPerFace = 16;
+
 struct BinBuffers {
   Span *spans;
   int *counts;
   int *totals;
+  int *base;       // [B][nct]: start of bin (b, c) in view b's region, -1 = overflowed
+  int *cursor;     // [B]: region cursors (zeroed by kd_bin_count)
   int *bins;
+  int xper;        // region entries per face row
+  float limit;     // usable fraction of each region (kd_set_pool_limits; 1 in production)
   float4 *cull;    // nullptr: not computed
   float cull_eps;  // the raster eps (cull coefficients only)
   int *clear;      // nullable: n_clear ints zeroed by kd_bin_count (counters of later passes)
@@ -46,6 +61,26 @@ struct BinBuffers {
 // kd_binning.hip.  out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}.
 __device__ void raster_cull_coefs(const float v[6], float M, int H, int W, Span sp, float eps,
                                   float out[8]);
+
+// Bin (b, c) of view b (rows [lo, lo + nview)): its ascending local face indices and count, or
+// nullptr when the bin overflowed its region -- then the caller walks all nview faces of the
+// view (entry e = local face e) and its exact span filter selects the same faces.
+__device__ __forceinline__ const int *bin_list(const BinBuffers &bb, int b, int c, int64_t lo,
+                                               int nview, int nbin, int &n) {
+  const int64_t bc = (int64_t)b * bb.g.nct() + c;
+  const int base = bb.base[bc];
+  if (base < 0) {
+    n = nview;
+    return nullptr;
+  }
+  n = nbin >= 0 ? nbin : bb.totals[bc];
+  return bb.bins + (int64_t)bb.xper * lo + base;
+}
+
+// Process-wide fractions of the pool capacities usable by a forward (kd_set_pool_limits; a test
+// hook that forces the overflow paths).  The workspace layout never depends on them.
+float pool_limit_bins();
+float pool_limit_pairs();
 
 size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view);
 // Carves the buffers from `ws` starting at *offset (advanced past them).

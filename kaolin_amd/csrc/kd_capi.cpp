@@ -16,6 +16,9 @@ char *error_buffer() {
 std::atomic<int> g_debug{0};
 int debug_flags() { return g_debug.load(); }
 std::atomic<long long *> g_tbuf{nullptr};
+std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
+float pool_limit_bins() { return g_lim_bins.load(); }
+float pool_limit_pairs() { return g_lim_pairs.load(); }
 long long *debug_tile_buffer() { return (g_debug.load() & 64) ? g_tbuf.load() : nullptr; }
 
 namespace {
@@ -32,7 +35,7 @@ const char *kNames[K_NUM_KERNELS] = {
     "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs",
     "kd_prepare_fwd", "kd_prepare_bwd", "kd_tile_order", "kd_iou_partial", "kd_iou_bwd",
     "kd_tex_fwd", "kd_tex_bwd", "kd_rast_interp", "kd_dt_bin",
-    "kd_dt_fwd", "kd_dibr_bwd", "kd_dibr_fwd"};
+    "kd_dt_fwd", "kd_dibr_bwd", "kd_dibr_fwd", "kd_soft_ovf_fwd", "kd_soft_ovf_bwd"};
 }  // namespace
 
 ProfScope::ProfScope(int id_, hipStream_t s) : id(id_), stream(s), on(g_prof.load()) {
@@ -72,6 +75,14 @@ void kd_profile_enable(int on) { kd::g_prof.store(on != 0); }
 
 int kd_debug_set(int flags) {
   kd::g_debug.store(flags);
+  return KD_OK;
+}
+
+int kd_set_pool_limits(double bins, double pairs) {
+  if (!(bins >= 0.0 && bins <= 1.0 && pairs >= 0.0 && pairs <= 1.0))
+    return kd::set_error(KD_ERR_INVALID_ARGUMENT, "pool limits must be in [0, 1]");
+  kd::g_lim_bins.store((float)bins);
+  kd::g_lim_pairs.store((float)pairs);
   return KD_OK;
 }
 

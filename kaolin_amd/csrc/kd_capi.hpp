@@ -39,6 +39,8 @@ enum KernelId {
   K_DT_FWD,
   K_DIBR_BWD,
   K_DIBR_FWD,
+  K_SOFT_OVF_FWD,
+  K_SOFT_OVF_BWD,
   K_NUM_KERNELS
 };
 

@@ -89,7 +89,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   d.rbb.cull_eps = eps;
   d.sbb.cull = nullptr;
   d.sbb.clear = d.pb.counters;
-  d.sbb.n_clear = 2;
+  d.sbb.n_clear = 3;
   hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> ra{rfs, d.rbb, fvz, fvz_fs, fvz_cs, feat, D, eps, interp, face_idx, weights};
@@ -177,13 +177,13 @@ int64_t kd_dibr_pair_count(const void *ws, int B, int H, int W, int64_t F, int k
                                           : dibr_carve<float>(w, B, H, W, F, knum).pb.ntile;
   const int64_t tiles =
       (int64_t)B * ((W + kTile - 1) / kTile) * (int64_t)((H + kTile - 1) / kTile);
-  std::vector<int32_t> nt((size_t)tiles * 2);
+  std::vector<int32_t> nt((size_t)tiles);
   if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -1;
   if (hipMemcpy(nt.data(), ntile, sizeof(int32_t) * nt.size(), hipMemcpyDeviceToHost) !=
       hipSuccess)
     return -1;
   int64_t n = 0;
-  for (int64_t i = 0; i < tiles; ++i) n += nt[2 * i];
+  for (int64_t i = 0; i < tiles; ++i) n += nt[i];
   return n;
 }
 

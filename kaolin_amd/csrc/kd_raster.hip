@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
       }
     }
   };
-  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
+  tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
 
   if (!t.inimg) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;

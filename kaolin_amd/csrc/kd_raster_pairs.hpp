@@ -210,7 +210,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
     }
     if (total) test_batch(total);
   };
-  tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg);
+  tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
 
   if (!t.inimg || (fs.dbg & 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
@@ -221,11 +221,11 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
     // the reference's sequential loop over this pixel's coarse bin (ascending faces)
     const BinGeom &g = a.bb.g;
     const int ct = (t.py / g.ct) * g.nctx + (t.px / g.ct);
-    const int n = a.bb.totals[(int64_t)b * g.nct() + ct];
-    const int *bin = a.bb.bins + (int64_t)ct * fs.N + lo;
+    int n;
+    const int *bin = bin_list(a.bb, b, ct, lo, (int)(hi - lo), -1, n);
     float max_z0 = -INFINITY;
     for (int e = 0; e < n; ++e) {
-      const int f = bin[e];
+      const int f = bin ? bin[e] : e;
       if (!pspan_has(pack_span(a.bb.spans[lo + f]), t.px, t.py)) continue;
       float v[6];
       load_corners(fs, lo + f, v);

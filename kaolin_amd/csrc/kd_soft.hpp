@@ -150,11 +150,11 @@ __device__ __forceinline__ void soft_stage(const FaceSet<T> &fs, T (*geo)[kCap],
 // pair pipeline of the autograd path (kd_softpair.hip)
 // ------------------------------------------------------------------------------------------
 struct SoftPairRec {
-  int32_t row;    // face row (view offset + face index)
-  uint32_t lid;   // position of the face in the tile's face list (all batches)
+  int32_t row;    // face row (view offset + face index); -1: unused pool entry
+  uint32_t tile;  // view * tiles + fine tile
   uint16_t slot;  // close-face slot of the pixel, 0..K-1
   uint8_t q;      // pixel of the tile (tile_geom thread index)
-  uint8_t type;   // distance type 0..5 (set by the math pass)
+  uint8_t pad;
 };
 
 template <typename T>
@@ -162,17 +162,31 @@ struct SoftCoef {
   T h[4];
 };
 
+constexpr int kFuseSlots = 32;      // knum bound of the one-launch soft mask (LDS slot table)
+constexpr int kMaxWaveBlocks = 32;  // pool blocks one wave can hold in a tile (64 K records)
+constexpr int kPoolPairsPerPixel = 12;  // record pool: min(knum, 12) pairs per pixel + slack
+
+// The record pool.  Records are written by pass A, one wave's records at a time into pool
+// blocks of bs = 64 * 2^s records (64 * knum records per wave need at most 32 blocks) taken with
+// one device atomic per block run; every taken block ends up holding valid records or row -1
+// (the tail of a wave's last block, the blocks of a tile that overflowed), so the backward runs
+// flat over the taken blocks.  A tile whose wave finds the pool exhausted drops its records and
+// computes its soft mask without them (`ovf` list); its backward recomputes the pairs.
 template <typename T>
 struct SoftPairBuf {
-  SoftPairRec *rec;   // [B * ntiles][cap]
-  T *sprob;           // [B * ntiles][cap] probability of each record
-  int32_t *npix;      // [B * H * W] close faces of each uncovered pixel
-  int32_t *ntile;     // [B * ntiles][2]: records, faces in the tile list
-  int2 *items;        // [B * ntiles * ceil(cap / 256)] (tile, 256-record chunk) work items
-  int32_t *tiles;     // [B * ntiles] tiles with records
-  int32_t *counters;  // [2]: items, tiles (zeroed by the binning's count kernel)
-  int64_t ntiles, cap, npixels;
-  int ntx;
+  SoftPairRec *rec;   // [cap_blocks * bs]
+  T *sprob;           // [cap_blocks * bs] probability of each record
+  uint8_t *stype;     // [cap_blocks * bs] distance type 0..5 of each record
+  int32_t *npix;      // [P] close faces of each uncovered pixel (split pipeline)
+  int32_t *ntile;     // [tiles] records of each tile (diagnostics)
+  int32_t *ovf;       // [tiles] tiles that computed their soft mask without records
+  int32_t *tblk;      // [tiles][4][kMaxWaveBlocks] each wave's blocks (split pipeline)
+  int32_t *twn;       // [tiles][4] each wave's records (split pipeline)
+  int32_t *tiles;     // [tiles] tiles with records (split pipeline)
+  int32_t *counters;  // [4]: blocks taken, overflow tiles, tiles with records (zeroed by
+                      // kd_bin_count), usable blocks of the forward (written by it)
+  int64_t ntiles, npixels, cap_blocks, lim_blocks;
+  int bs, bs_shift, ntx;
 };
 
 // bins + pair buffers for B views of F faces, K close faces, element size esize
@@ -180,8 +194,8 @@ size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int 
 // pair buffers carved from a workspace after the soft mask's bins
 template <typename T>
 SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K);
-// pass A + pair math (+ backward coefficients when grad) + (when reduce) the soft mask, over
-// already built bins (a.bb) whose kd_bin_count cleared pb.counters
+// pass A + pair math + (when reduce) the soft mask, over already built bins (a.bb) whose
+// kd_bin_count cleared pb.counters
 template <typename T>
 int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce,
                       hipStream_t stream);

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
     };
     // once every uncovered pixel of the tile holds K close faces, later faces cannot enter
     auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
-    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg, done);
+    tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg, done);
   }
 
   if (!t.wave_live) return;

@@ -6,19 +6,26 @@
 // ~16 pairs each at C3).
 //   kd_soft_pairs<FUSED>  one workgroup per 16x16 tile: walks the tile's ordered bin
 //                      (kd_tile.hpp); pass A picks each uncovered pixel's first K close faces by
-//                      face index and writes (pixel, slot, face) records to the tile's region,
-//                      stopping once every uncovered pixel holds K.  FUSED (knum <= 32, no close
-//                      lists): the same workgroup then does the pair math over its records
-//                      (distance type and probability, bit-identical to the reference) and the
-//                      ordered product soft = 1 - prod(1 - p) (dibr_soft_mask_cuda.cu:174-181,
-//                      double-promoted) -- the whole soft mask in one launch.
+//                      face index and writes (pixel, slot, face) records into the record pool
+//                      (SoftPairBuf, kd_soft.hpp), stopping once every uncovered pixel holds K.
+//                      FUSED (knum <= 32, no close lists): the same workgroup then does the pair
+//                      math over its records (distance type and probability, bit-identical to
+//                      the reference) and the ordered product soft = 1 - prod(1 - p)
+//                      (dibr_soft_mask_cuda.cu:174-181, double-promoted) -- the whole soft mask
+//                      in one launch.
 //   kd_soft_pair_math, kd_soft_reduce   the same math and product as separate launches, for
 //                      the op form with the reference's close-face lists (and knum > 32).
-//   kd_soft_bwd_items  the backward, flat over (tile, 256-record) items.
+//   kd_soft_bwd_items  the backward, flat over the pool's 256-record items, then the tiles that
+//                      overflowed the pool (their pairs recomputed).
 //   kd_dibr_fwd_tiles  dibr_rasterization's forward: per tile, the raster pair pipeline
 //                      (kd_raster_pairs.hpp) and then the FUSED soft mask of the same tile.
 //   kd_dibr_bwd        dibr_rasterization's backward: the raster backward's tiles
 //                      (kd_raster_bwd.hpp) and the soft items in one grid.
+// Pool overflow (a workload with more pairs than the pool's min(knum, 12) per pixel, or
+// kd_set_pool_limits): the tile drops its records and runs the same walk again, each pixel lane
+// computing its pairs' probabilities in slot order and the product directly ("streaming": the
+// reference's per-pixel loop over the tile's face list), so the soft mask is bit-identical; its
+// backward walks the tile again in kd_soft_bwd_items.
 // Backward factorisation: the reference's per-pair gradient (dibr_soft_mask_cuda.cu:281-348) is
 //   dLdz * f_j / M  with  dLdz = -sigmainv * dLdp * (1 - soft) / (1 - p + 1e-7) * p
 // and f_j the geometric factors of the distance type (2(x1 - x0) ... for a vertex, the four
@@ -33,22 +40,39 @@
 
 namespace kd {
 
-constexpr unsigned kPersistentBlocks = 2048;  // 8 workgroups per CU for the item loops
-constexpr int kFuseSlots = 32;               // knum bound of the fused soft-mask kernel
-constexpr int kMathItems = 1;                 // items per pair-math workgroup pass (4: slower)
-constexpr unsigned kMathBlocks = 8192;        // pair-math grid
+constexpr unsigned kMathBlocks = 8192;  // pair-math / backward-item grid
+
+// Pool blocks are 64 << shift records: 64 * knum records of one wave fit kMaxWaveBlocks blocks.
+static int pool_shift(int K) {
+  int s = 0;
+  while ((kMaxWaveBlocks << s) < K) ++s;
+  return s;
+}
+
+static int64_t pool_blocks(int B, int H, int W, int K) {
+  const int64_t bs = (int64_t)kWave << pool_shift(K);
+  const int64_t ntiles = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+  const int64_t P = (int64_t)B * H * W, tiles = (int64_t)B * ntiles;
+  // pairs + on average one partly used block per tile (a tile that does not fit streams)
+  const int64_t recs = P * std::min(K, kPoolPairsPerPixel) + tiles * bs;
+  return (recs + bs - 1) / bs;
+}
 
 size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize) {
   const int64_t ntiles = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-  const int64_t tiles = (int64_t)B * ntiles, cap = (int64_t)kBlock * K, P = (int64_t)B * H * W;
+  const int64_t tiles = (int64_t)B * ntiles, P = (int64_t)B * H * W;
+  const int64_t recs = pool_blocks(B, H, W, K) << (6 + pool_shift(K));
   size_t s = bin_workspace_bytes(B, H, W, N, F);
-  s += align_up(sizeof(SoftPairRec) * (size_t)(tiles * cap));
-  s += align_up((size_t)esize * (size_t)(tiles * cap));
+  s += align_up(sizeof(SoftPairRec) * (size_t)recs);
+  s += align_up((size_t)esize * (size_t)recs);
+  s += align_up((size_t)recs);
   s += align_up(sizeof(int32_t) * (size_t)P);
-  s += align_up(sizeof(int32_t) * 2 * (size_t)tiles);
-  s += align_up(sizeof(int2) * (size_t)(tiles * ((cap + kBlock - 1) / kBlock)));
   s += align_up(sizeof(int32_t) * (size_t)tiles);
-  s += align_up(sizeof(int32_t) * 2);
+  s += align_up(sizeof(int32_t) * (size_t)tiles);
+  s += align_up(sizeof(int32_t) * 4 * kMaxWaveBlocks * (size_t)tiles);
+  s += align_up(sizeof(int32_t) * 4 * (size_t)tiles);
+  s += align_up(sizeof(int32_t) * (size_t)tiles);
+  s += align_up(sizeof(int32_t) * 4);
   return s;
 }
 
@@ -57,25 +81,41 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   SoftPairBuf<T> pb;
   pb.ntx = (W + kTile - 1) / kTile;
   pb.ntiles = (int64_t)pb.ntx * ((H + kTile - 1) / kTile);
-  pb.cap = (int64_t)kBlock * K;
+  pb.bs_shift = 6 + pool_shift(K);
+  pb.bs = 1 << pb.bs_shift;
+  pb.cap_blocks = pool_blocks(B, H, W, K);
+  pb.lim_blocks = (int64_t)((double)pool_limit_pairs() * (double)pb.cap_blocks);
   const int64_t tiles = (int64_t)B * pb.ntiles, P = (int64_t)B * H * W;
+  const int64_t recs = pb.cap_blocks << pb.bs_shift;
   pb.npixels = P;
   char *base = (char *)ws;
   pb.rec = (SoftPairRec *)(base + off);
-  off += align_up(sizeof(SoftPairRec) * (size_t)(tiles * pb.cap));
+  off += align_up(sizeof(SoftPairRec) * (size_t)recs);
   pb.sprob = (T *)(base + off);
-  off += align_up(sizeof(T) * (size_t)(tiles * pb.cap));
+  off += align_up(sizeof(T) * (size_t)recs);
+  pb.stype = (uint8_t *)(base + off);
+  off += align_up((size_t)recs);
   pb.npix = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)P);
   pb.ntile = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * 2 * (size_t)tiles);
-  pb.items = (int2 *)(base + off);
-  off += align_up(sizeof(int2) * (size_t)(tiles * ((pb.cap + kBlock - 1) / kBlock)));
+  off += align_up(sizeof(int32_t) * (size_t)tiles);
+  pb.ovf = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * (size_t)tiles);
+  pb.tblk = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * 4 * kMaxWaveBlocks * (size_t)tiles);
+  pb.twn = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * 4 * (size_t)tiles);
   pb.tiles = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.counters = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * 2);
+  off += align_up(sizeof(int32_t) * 4);
   return pb;
+}
+
+// Blocks of the pool a backward reads: those the forward took, up to its usable limit.
+__device__ __forceinline__ int64_t pool_used_records(const int32_t *counters, int bs_shift) {
+  const int64_t taken = counters[0], lim = counters[3];
+  return (taken < lim ? taken : lim) << bs_shift;
 }
 
 // pixel of tile-local thread index q (kd_tile.hpp tile_geom layout)
@@ -165,18 +205,11 @@ __device__ __forceinline__ uint64_t lowest_bits(uint64_t m, int need) {
   return m & ((pos >= 63) ? ~0ull : ((2ull << pos) - 1ull));
 }
 
-// One 64-face chunk of a wave's sub-list (lane j = chunk entry j): every uncovered pixel lane
-// takes the first K - kid faces of the chunk whose exact enlarged span holds its centre
-// (ascending face index = ascending entry, dibr_soft_mask_cuda.cu:95 and :165-171).  Records
-// are placed face-major (face j's pixels contiguous, pixels ascending): the transposed
-// selections give each face its record count and offset; each pixel lane then writes its own
-// records (slot = its running close-face count) at offset[j] + rank of the pixel in face j.
-__device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
-                                                   int K, const TileGeom &t, int64_t lo,
-                                                   int lbase, int &my_kid, uint64_t *s_pm,
-                                                   unsigned short *s_off, int *s_nrec,
-                                                   SoftPairRec *rec,
-                                                   unsigned short (*s_ridx)[kBlock] = nullptr) {
+// The faces of one 64-face chunk of a wave's sub-list (lane j = chunk entry j) this pixel lane
+// takes: the first K - kid whose exact enlarged span holds its centre (ascending face index =
+// ascending entry, dibr_soft_mask_cuda.cu:95 and :165-171).
+__device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, int c, bool unc,
+                                                 int K, const TileGeom &t, int kid) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int qx = lane & 7, qy = lane >> 3;
   const int j = c * kWave + lane;
@@ -192,17 +225,72 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
     mc = (qx == i) ? bc : mc;
     mr = (qy == i) ? br : mr;
   }
-  uint64_t sel = (unc && my_kid < K) ? (mc & mr) : 0ull;
-  if (__popcll(sel) > K - my_kid) sel = lowest_bits(sel, K - my_kid);
+  uint64_t sel = (unc && kid < K) ? (mc & mr) : 0ull;
+  if (__popcll(sel) > K - kid) sel = lowest_bits(sel, K - kid);
+  return sel;
+}
+
+// One wave's records of the current tile: n records in the pool blocks blk[0 .. nblk) (LDS).
+struct WavePool {
+  int n, nblk;
+  int *blk;
+  bool ovf;
+};
+
+template <typename T>
+__device__ __forceinline__ int64_t pool_index(const SoftPairBuf<T> &pb, const int *blk, int j) {
+  return ((int64_t)blk[j >> pb.bs_shift] << pb.bs_shift) + (j & (pb.bs - 1));
+}
+
+// Room for `tot` more records of this wave (wave-uniform): one device atomic per run of new
+// blocks.  false: the usable pool is exhausted; the part of the failed run inside it is marked
+// unused (the backward reads every taken block).
+template <typename T>
+__device__ __forceinline__ bool wave_reserve(const SoftPairBuf<T> &pb, WavePool &wp, int tot) {
+  const int lane = threadIdx.x & 63;
+  const int need = wp.n + tot - (wp.nblk << pb.bs_shift);
+  if (need <= 0) return true;
+  const int nnew = (need + pb.bs - 1) >> pb.bs_shift;
+  int g0 = 0;
+  if (lane == 0) g0 = atomicAdd(&pb.counters[0], nnew);
+  g0 = __builtin_amdgcn_readfirstlane(g0);
+  if ((int64_t)g0 + nnew > pb.lim_blocks || wp.nblk + nnew > kMaxWaveBlocks) {
+    const int64_t e = min((int64_t)g0 + nnew, pb.lim_blocks) << pb.bs_shift;
+    for (int64_t i = ((int64_t)g0 << pb.bs_shift) + lane; i < e; i += kWave) pb.rec[i].row = -1;
+    return false;
+  }
+  if (lane < nnew) wp.blk[wp.nblk + lane] = g0 + lane;
+  wp.nblk += nnew;
+  return true;
+}
+
+// One 64-face chunk of a wave's sub-list: each uncovered pixel lane takes its chunk_select faces.
+// Records are placed face-major (face j's pixels contiguous, pixels ascending): the transposed
+// selections give each face its record count and offset; each pixel lane then writes its own
+// records (slot = its running close-face count) at offset[j] + rank of the pixel in face j.
+template <typename T>
+__device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
+                                                   int K, const TileGeom &t, int64_t lo,
+                                                   uint32_t tile, int &my_kid, uint64_t *s_pm,
+                                                   unsigned short *s_off,
+                                                   const SoftPairBuf<T> &pb, WavePool &wp,
+                                                   int *s_ovf,
+                                                   unsigned short (*s_ridx)[kBlock] = nullptr) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
   // face lanes: pixel masks, record counts and offsets
   const uint64_t pm = wave_transpose64(sel);
   const int cnt = __popcll(pm);
   const int incl = wave_incl_scan(cnt);
   const int tot = __builtin_amdgcn_readlane(incl, 63);
   if (tot == 0) return;
-  int base = 0;
-  if (lane == 0) base = atomicAdd(s_nrec, tot);
-  base = __builtin_amdgcn_readfirstlane(base);
+  if (!wave_reserve(pb, wp, tot)) {
+    wp.ovf = true;
+    if (lane == 0) *s_ovf = 1;
+    return;
+  }
+  const int base = wp.n;
+  wp.n += tot;
   s_pm[lane] = pm;
   s_off[lane] = (unsigned short)(incl - cnt);
   wave_lds_sync();
@@ -215,29 +303,98 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
     const int kk = L.sub[w][c * kWave + jj];
     SoftPairRec r;
     r.row = (int32_t)(lo + L.f[kk]);
-    r.lid = (uint32_t)(lbase + kk);
+    r.tile = tile;
     r.slot = (uint16_t)slot++;
     r.q = (uint8_t)tile_q;
-    r.type = 0;
+    r.pad = 0;
     const int ri = base + s_off[jj] + __popcll(s_pm[jj] & below);
-    rec[ri] = r;
-    if (s_ridx) s_ridx[r.slot][tile_q] = (unsigned short)ri;  // (slot, pixel) -> record
+    pb.rec[pool_index(pb, wp.blk, ri)] = r;
+    if (s_ridx) s_ridx[r.slot][tile_q] = (unsigned short)ri;  // (slot, pixel) -> wave record
   }
   my_kid = slot;
   wave_lds_sync();
 }
 
+// The streaming form of one chunk (a tile without records): the pixel lane visits the same
+// faces in slot order and hands each (face row, slot) to fn.
+template <typename PairFn>
+__device__ __forceinline__ void soft_chunk_stream(const TileLists &L, int nsub, int c, bool unc,
+                                                  int K, const TileGeom &t, int64_t lo,
+                                                  int &my_kid, PairFn fn) {
+  const int w = threadIdx.x >> 6;
+  for (uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid); sel; sel &= sel - 1ull) {
+    const int kk = L.sub[w][c * kWave + __builtin_ctzll(sel)];
+    fn(lo + L.f[kk], my_kid++);
+  }
+}
+
+// The soft mask of the tiles whose pass A found the pool exhausted (kd_soft_pairs dropped
+// their records): each uncovered pixel lane walks its first K close faces in slot order and
+// multiplies their probabilities into its product -- the reference's per-pixel loop over the
+// tile list, bit-identical to the pair pipeline; the split pipeline also gets its lists here.
+// One workgroup per such tile; a grid that finds none exits at once.
+template <typename T, bool FUSED>
+__global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  __shared__ TileLists L;
+  const FaceSet<T> &fs = a.fs;
+  const int H = fs.H, W = fs.W, K = a.K;
+  const float M = fs.M;
+  const int novf = pb.counters[1];
+  for (int i = blockIdx.x; i < novf; i += gridDim.x) {
+    const int64_t tile = pb.ovf[i];
+    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+    int64_t lo, hi;
+    view_range(fs, b, lo, hi);
+    const TileGeom t = tile_geom(H, W, tl);
+    const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
+    const bool unc = t.inimg && a.face_idx[p] < 0;
+    const bool wave_unc = __ballot(unc) != 0ull;
+    const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
+    int my_kid = 0;
+    T prod = (T)1.0;
+    auto stage = [&](int, int64_t) {};
+    auto round = [&](int nsub, int) {
+      if (wave_unc)
+        for (int c = 0; c * kWave < nsub; ++c)
+          soft_chunk_stream(L, nsub, c, unc, K, t, lo, my_kid, [&](int64_t row, int slot) {
+            T v[6];
+            load_corners(fs, row, v);
+            int et = 0;
+            T prob = (T)0;
+            soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+            prod = (T)((double)prod * (1.0 - (double)prob));
+            if (!FUSED) {
+              if (a.prob) {
+                a.prob[p * K + slot] = prob;
+                a.cidx[p * K + slot] = row - lo;
+                a.ctype[p * K + slot] = (uint8_t)(et + 1);
+              }
+              if (a.last && slot == K - 1) a.last[p] = (int32_t)(row - lo);
+            }
+          });
+    };
+    auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
+    if (__syncthreads_or(unc))
+      tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg, done);
+    if (unc && my_kid > 0 && a.soft) a.soft[p] = (T)(1.0 - (double)prod);
+    __syncthreads();
+  }
+}
+
 // Records of one tile's pixel set (pass A).  FUSED (knum <= kFuseSlots, no close-face lists):
 // the same workgroup then runs the pair math over its own records and the ordered product of
 // each pixel's slots -- the whole soft mask in one launch.  Pass A notes each (slot, pixel)'s
-// record index in LDS, so the product reads the probabilities in slot order.
+// record (its index among the wave's records) in LDS, so the product reads the probabilities
+// in slot order.
 template <bool FUSED>
 struct SoftPairsLDS {
   unsigned short ridx[FUSED ? kFuseSlots : 1][kBlock];
   TileLists L;
   uint64_t pm[4][kWave];
   unsigned short off[4][kWave];
-  int nrec, base, box[4];
+  int blk[4][kMaxWaveBlocks];
+  int wn[4], box[4];
+  int ovf;
 };
 
 // Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
@@ -246,28 +403,28 @@ struct SoftPairsLDS {
 template <typename T, bool FUSED>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                 int b, int tl, int nbin, SoftPairsLDS<FUSED> &S) {
-  auto &s_ridx = S.ridx;
   TileLists &L = S.L;
-  auto &s_pm = S.pm;
-  auto &s_off = S.off;
-  int &s_nrec = S.nrec;
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
-  const int tid = threadIdx.x, w = tid >> 6;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const float M = fs.M;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
+  const int nview = (int)(hi - lo);
   TileGeom t = tile_geom(H, W, tl);
   t.nbin = nbin;
   if (fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, coarse count) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
+  if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0)
+    pb.counters[3] = (int32_t)pb.lim_blocks;  // the pool this forward may use (for the readers)
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const bool unc = t.inimg && a.face_idx[p] < 0;
   const bool wave_unc = __ballot(unc) != 0ull;
   const int64_t tile = (int64_t)b * pb.ntiles + tl;
-  SoftPairRec *rec = pb.rec + tile * pb.cap;
-  int my_kid = 0, lbase = 0;
-  if (tid == 0) s_nrec = 0;
+  WavePool wp{0, 0, S.blk[w], false};
+  int my_kid = 0;
+  if (tid == 0) S.ovf = 0;
 
   // faces matter only where they reach an uncovered pixel: the filter boxes of tile_rounds
   // shrink to the uncovered pixels' bounding boxes (exact: a record needs the pixel centre
@@ -277,7 +434,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     s_box[0] = s_box[2] = 1 << 30;
     s_box[1] = s_box[3] = -1;
   }
-  if (!(fs.dbg & 512)) {
+  {
     const uint64_t um = __ballot(unc);
     t.wave_live = t.wave_live && um != 0ull;
     if (um) {
@@ -291,34 +448,47 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     }
   }
   __syncthreads();
-  if (!(fs.dbg & 512) && t.wave_live && (tid & 63) == 0) {
+  if (t.wave_live && lane == 0) {
     atomicMin(&s_box[0], t.SX0);
     atomicMax(&s_box[1], t.SX1);
     atomicMin(&s_box[2], t.SY0);
     atomicMax(&s_box[3], t.SY1);
   }
+  bool ovf = false;
+  auto stage = [&](int, int64_t) {};  // pass A needs the spans only
+  // once every uncovered pixel holds K close faces, later faces cannot enter
+  auto all_full = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
   if (__syncthreads_or(unc)) {
-    if (!(fs.dbg & 512)) {
-      t.FX0 = s_box[0];
-      t.FX1 = s_box[1];
-      t.FY0 = s_box[2];
-      t.FY1 = s_box[3];
-    }
-    auto stage = [&](int, int64_t) {};  // pass A needs the spans only
-    auto round = [&](int nsub, int cnt) {
+    t.FX0 = s_box[0];
+    t.FX1 = s_box[1];
+    t.FY0 = s_box[2];
+    t.FY1 = s_box[3];
+    auto round = [&](int nsub, int) {
       if (wave_unc && !(fs.dbg & 1024))
-        for (int c = 0; c * kWave < nsub; ++c)
-          soft_chunk_records(L, nsub, c, unc, K, t, lo, lbase, my_kid, s_pm[w], s_off[w],
-                             &s_nrec, rec, FUSED ? s_ridx : nullptr);
-      lbase += cnt;
+        for (int c = 0; c * kWave < nsub && !wp.ovf; ++c)
+          soft_chunk_records<T>(L, nsub, c, unc, K, t, lo, (uint32_t)tile, my_kid, S.pm[w],
+                                S.off[w], pb, wp, &S.ovf, FUSED ? S.ridx : nullptr);
     };
-    // once every uncovered pixel holds K close faces, later faces cannot enter
-    auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
-    tile_rounds(L, a.bb, fs.N, b, lo, t, stage, round, fs.dbg, done);
+    // (a wave that found the pool exhausted ends the walk at the next round)
+    auto done = [&]() { return all_full() || S.ovf != 0; };
+    tile_rounds(L, a.bb, nview, b, lo, t, stage, round, fs.dbg, done);
+    ovf = S.ovf != 0;  // tile_rounds ends on a barrier
+  }
+  if (ovf) {
+    // the pool is exhausted: drop this tile's records (every block its waves took); its soft
+    // mask is computed by kd_soft_ovf_fwd and its backward by kd_soft_ovf_bwd (pb.ovf)
+    for (int i = lane; i < (wp.nblk << pb.bs_shift); i += kWave)
+      pb.rec[pool_index(pb, wp.blk, i)].row = -1;
+    wp.n = 0;
+    my_kid = 0;
+    if (tid == 0) pb.ovf[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
+  } else {
+    // the unused tail of each wave's last block
+    for (int i = wp.n + lane; i < (wp.nblk << pb.bs_shift); i += kWave)
+      pb.rec[pool_index(pb, wp.blk, i)].row = -1;
   }
   if (t.inimg) {
-    pb.npix[p] = unc ? my_kid : 0;
-    // pixels without close faces are final here; the others get soft from kd_soft_reduce
+    if (!FUSED) pb.npix[p] = (unc && !ovf) ? my_kid : 0;  // the split pipeline's reduce
     if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
     else if (a.soft && my_kid == 0) a.soft[p] = (T)0.0;
     if (a.last && my_kid < K) a.last[p] = -1;
@@ -329,23 +499,15 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
         a.ctype[p * K + s] = 0;
       }
   }
+  if (lane == 0) S.wn[w] = wp.n;
   __syncthreads();
-  const int n = s_nrec;
-  if (tid == 0) {
-    pb.ntile[2 * tile] = n;
-    pb.ntile[2 * tile + 1] = lbase;
-  }
-  if (n > 0) {  // work items of the math and backward passes
-    const int nch = (n + kBlock - 1) / kBlock;
-    int &s_base = S.base;
-    if (tid == 0) {
-      s_base = atomicAdd(&pb.counters[0], nch);
-      pb.tiles[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
-    }
-    __syncthreads();
-    // item = (tile, chunk | records in the chunk << 16): the math pass needs no tile lookup
-    for (int c = tid; c < nch; c += kBlock)
-      pb.items[s_base + c] = make_int2((int)tile, c | (min(kBlock, n - c * kBlock) << 16));
+  const int n0 = S.wn[0], n01 = n0 + S.wn[1], n012 = n01 + S.wn[2], n = n012 + S.wn[3];
+  if (tid == 0) pb.ntile[tile] = n;
+  if (!FUSED && n > 0) {  // where the split pipeline's reduce finds this tile's records
+    if (tid < 4 * kMaxWaveBlocks)
+      pb.tblk[tile * 4 * kMaxWaveBlocks + tid] = S.blk[tid / kMaxWaveBlocks][tid % kMaxWaveBlocks];
+    if (tid < 4) pb.twn[tile * 4 + tid] = S.wn[tid];
+    if (tid == 0) pb.tiles[atomicAdd(&pb.counters[2], 1)] = (int32_t)tile;
   }
   if constexpr (FUSED) {
     // side job of the launch: the backward's gradient buffers (grid-stride, coalesced)
@@ -359,12 +521,13 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
         a.zero1[i - a.nzero0] = (T)0;
     }
     if (n == 0) return;
-    // pair math over this tile's records (record order: coalesced reads)
-    const float M = fs.M;
+    // pair math over this tile's records: record i of the tile is record j of wave ww
     const int tx = tl % pb.ntx, ty = tl / pb.ntx;
-    T *sp = pb.sprob + tile * pb.cap;  // record order
     for (int i = tid; i < n; i += kBlock) {
-      const SoftPairRec r = rec[i];
+      const int ww = (i >= n0) + (i >= n01) + (i >= n012);
+      const int j = i - (ww == 0 ? 0 : ww == 1 ? n0 : ww == 2 ? n01 : n012);
+      const int64_t ri = pool_index(pb, S.blk[ww], j);
+      const SoftPairRec r = pb.rec[ri];
       T v[6];
       load_corners(fs, (int64_t)r.row, v);
       int px, py;
@@ -373,8 +536,8 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       int et = 0;
       T prob = (T)0;
       soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
-      sp[i] = prob;
-      rec[i].type = (uint8_t)et;
+      pb.sprob[ri] = prob;
+      pb.stype[ri] = (uint8_t)et;
       // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
     }
     __syncthreads();  // the workgroup's probabilities are visible to it
@@ -385,7 +548,9 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       for (int s0 = 0; s0 < my_kid; s0 += U) {
         T pv[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) pv[u] = s0 + u < my_kid ? sp[s_ridx[s0 + u][tid]] : (T)0;
+        for (int u = 0; u < U; ++u)
+          pv[u] = s0 + u < my_kid ? pb.sprob[pool_index(pb, S.blk[w], S.ridx[s0 + u][tid])]
+                                  : (T)0;
 #pragma unroll
         for (int u = 0; u < U; ++u)
           if (s0 + u < my_kid) prod = (T)((double)prod * (1.0 - (double)pv[u]));
@@ -445,13 +610,13 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
 }
 
 // ------------------------------------------------------------------------------------------
-// per-pair math
+// the split pipeline: pair math and product as their own launches
 // ------------------------------------------------------------------------------------------
 // soft = 1 - prod(1 - p) over the close faces of the 256 pixels of one tile, in slot order
-// (dibr_soft_mask_cuda.cu:174-181, double-promoted product).  The probabilities are stored in
-// record order; kReduceSlots slots at a time are placed into an LDS table by (slot, pixel) and
-// each pixel lane multiplies its slots in order.  Pixels without close faces were written by
-// kd_soft_pairs.
+// (dibr_soft_mask_cuda.cu:174-181, double-promoted product).  The tile's records are found
+// through its waves' block lists; kReduceSlots slots at a time are placed into an LDS table by
+// (slot, pixel) and each pixel lane multiplies its slots in order.  Pixels without close faces
+// (and the tiles that streamed) were written by kd_soft_pairs.
 constexpr int kReduceSlots = 32;
 
 template <typename T>
@@ -460,32 +625,24 @@ __device__ __forceinline__ void soft_reduce_tile(const SoftArgs<T> &a, const Sof
   const int K = a.K, H = a.fs.H, W = a.fs.W;
   const int tid = threadIdx.x;
   const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-  const int n = pb.ntile[2 * tile];
+  const int32_t *wn = pb.twn + tile * 4;
+  const int32_t *blk = pb.tblk + tile * 4 * kMaxWaveBlocks;
+  const int n0 = wn[0], n01 = n0 + wn[1], n012 = n01 + wn[2], n = n012 + wn[3];
   int px, py;
   tile_pixel(tl % pb.ntx, tl / pb.ntx, tid, px, py);
   const bool in = px < W && py < H;
   const int64_t p = ((int64_t)b * H + py) * W + px;
   const int np = in ? pb.npix[p] : 0;
-  const SoftPairRec *rec = pb.rec + tile * pb.cap;
-  const T *pr = pb.sprob + tile * pb.cap;
   T prod = (T)1.0;
   for (int s0 = 0; s0 < K; s0 += kReduceSlots) {
     __syncthreads();  // the previous pass is done with s_p
-    constexpr int U = 4;  // record loads in flight per thread
-    for (int i0 = tid; i0 < n; i0 += U * kBlock) {
-      uint32_t sq[U];
-      T pv[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = i0 + u * kBlock;
-        sq[u] = i < n ? __builtin_nontemporal_load((const uint32_t *)(rec + i) + 2) : 0xffffu;
-        pv[u] = i < n ? pr[i] : (T)0;
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int s = (int)(sq[u] & 0xffffu) - s0;  // slot | q << 16 | type << 24
-        if (s >= 0 && s < kReduceSlots) s_p[s][(sq[u] >> 16) & 0xffu] = pv[u];
-      }
+    for (int i = tid; i < n; i += kBlock) {
+      const int ww = (i >= n0) + (i >= n01) + (i >= n012);
+      const int j = i - (ww == 0 ? 0 : ww == 1 ? n0 : ww == 2 ? n01 : n012);
+      const int64_t ri = pool_index(pb, blk + ww * kMaxWaveBlocks, j);
+      const uint32_t sq = ((const uint32_t *)(pb.rec + ri))[2];  // slot | q << 16
+      const int s = (int)(sq & 0xffffu) - s0;
+      if (s >= 0 && s < kReduceSlots) s_p[s][(sq >> 16) & 0xffu] = pb.sprob[ri];
     }
     __syncthreads();
     const int e = min(np - s0, kReduceSlots);
@@ -506,71 +663,51 @@ __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPair
     else
       a.zero1[i - a.nzero0] = (T)0;
   }
-  const int ntl = pb.counters[1];
+  const int ntl = pb.counters[2];
   for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) soft_reduce_tile<T>(a, pb, pb.tiles[ti], s_p);
 }
 
-// Flat over the (tile, 256-record chunk) items: each record's distance type and probability
-// (bit-identical to the reference) and optionally the close lists.  (Reducing a tile in the workgroup that finishes its last chunk needs a device-scope
-// release per item -- an L2 writeback on gfx950 -- and measured 30x slower than kd_soft_reduce.)
-template <typename T, bool LISTS, int R>
+// Flat over the pool: each record's distance type and probability (bit-identical to the
+// reference) and optionally the close lists.
+template <typename T, bool LISTS>
 __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftPairBuf<T> pb) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
-  const int nitems = pb.counters[0];
-  // R items per workgroup pass, their loads issued together: each thread has R independent
-  // item -> record -> corner load chains in flight (the kernel is latency-bound, not ALU-bound)
-  for (int it0 = blockIdx.x * R; it0 < nitems; it0 += gridDim.x * R) {
-    int2 item[R];
-    bool ok[R];
-    SoftPairRec r[R];
-    T v[R][6];
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      item[u] = it0 + u < nitems ? pb.items[it0 + u] : make_int2(0, 0);
-      ok[u] = (int)threadIdx.x < (item[u].y >> 16);
-    }
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-      if (ok[u]) r[u] = pb.rec[(int64_t)item[u].x * pb.cap + (item[u].y & 0xffff) * kBlock +
-                               threadIdx.x];
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-      if (ok[u]) load_corners(fs, (int64_t)r[u].row, v[u]);
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      if (!ok[u]) continue;
-      const int64_t tile = item[u].x;
-      const int i = (item[u].y & 0xffff) * kBlock + threadIdx.x;
-      const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-      const int tx = tl % pb.ntx, ty = tl / pb.ntx;
-      int px, py;
-      tile_pixel(tx, ty, r[u].q, px, py);
-      const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
-      int et = 0;
-      T prob = (T)0;
-      if (!(fs.dbg & 32)) soft_face_dist<T>(x0, y0, v[u], M, a.sigmainv, et, prob);
+  const int64_t nrec = pool_used_records(pb.counters, pb.bs_shift);
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrec;
+       i += (int64_t)gridDim.x * kBlock) {
+    const SoftPairRec r = pb.rec[i];
+    if (r.row < 0) continue;
+    T v[6];
+    load_corners(fs, (int64_t)r.row, v);
+    const int64_t tile = r.tile;
+    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+    int px, py;
+    tile_pixel(tl % pb.ntx, tl / pb.ntx, r.q, px, py);
+    const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
+    int et = 0;
+    T prob = (T)0;
+    soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+    pb.sprob[i] = prob;
+    pb.stype[i] = (uint8_t)et;
+    if (LISTS || a.last) {
       const int64_t gp = ((int64_t)b * H + py) * W + px;
-      pb.sprob[tile * pb.cap + i] = prob;  // record order: coalesced
-      pb.rec[tile * pb.cap + i].type = (uint8_t)et;
-      if (LISTS || a.last) {
-        int64_t lo, hi;
-        view_range(fs, b, lo, hi);
-        if (LISTS) {
-          const int64_t o = gp * K + r[u].slot;
-          a.prob[o] = prob;
-          a.cidx[o] = (int64_t)r[u].row - lo;
-          a.ctype[o] = (uint8_t)(et + 1);
-        }
-        if (a.last && r[u].slot == K - 1) a.last[gp] = (int32_t)((int64_t)r[u].row - lo);
+      int64_t lo, hi;
+      view_range(fs, b, lo, hi);
+      if (LISTS) {
+        const int64_t o = gp * K + r.slot;
+        a.prob[o] = prob;
+        a.cidx[o] = (int64_t)r.row - lo;
+        a.ctype[o] = (uint8_t)(et + 1);
       }
+      if (a.last && r.slot == K - 1) a.last[gp] = (int32_t)((int64_t)r.row - lo);
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------
-// backward: per tile, per face sums in LDS
+// backward
 // ------------------------------------------------------------------------------------------
 // Adds one pair's contribution s_p * h_j to the register sums g[6] of its face's corners.
 template <typename T>
@@ -628,52 +765,54 @@ __device__ __forceinline__ void seg_scan_shfl(int seg, int lane, T g[6]) {
   }
 }
 
-// The coefficients are recomputed here from the record's face corners, distance type and forward
-// probability (soft_pair_coef): the forward's critical path skips them, and this kernel, bound by
-// its load chains and atomics, absorbs the arithmetic (measured free).
+// Flat over the pool's 256-record items, one record per thread: the coefficients are computed
+// from the record's face corners, distance type and forward probability (soft_pair_coef: the
+// forward's critical path skips them; this kernel, bound by its load chains and atomics, absorbs
+// the arithmetic), s_p * h_j is expanded to the face's 6 corner coordinates, summed over the
+// record's run of equal faces inside its wave by a segmented inclusive scan (records are
+// face-major runs; no LDS), and the run's last lane adds the nonzero sums with float atomics.
+// Every record costs the same, so the grid is balanced however the records fall on the tiles.
 template <typename T, int R>
 __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                     int blk, int nblk) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const int lane = threadIdx.x & (kWave - 1);
-  const int nitems = pb.counters[0];
-  // R items per workgroup pass; their load chains (item -> record -> the pixel's gradient and
-  // soft value, the face's corners) are issued together
-  for (int it0 = blk * R; it0 < nitems; it0 += nblk * R) {
-    int2 item[R];
+  const int64_t nrec = pool_used_records(pb.counters, pb.bs_shift);
+  const int64_t nitems = (nrec + kBlock - 1) / kBlock;
+  // R items per workgroup pass; their load chains (record -> the pixel's gradient and soft
+  // value, the face's corners) are issued together
+  for (int64_t it0 = (int64_t)blk * R; it0 < nitems; it0 += (int64_t)nblk * R) {
     bool ok[R];
     SoftPairRec r[R];
     SoftCoef<T> c[R];
     T gs[R], so[R];
+    int et[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      item[u] = it0 + u < nitems ? pb.items[it0 + u] : make_int2(0, 0);
-      ok[u] = (int)threadIdx.x < (item[u].y >> 16);
+      const int64_t ri = (it0 + u) * kBlock + threadIdx.x;
+      ok[u] = ri < nrec;
+      if (ok[u]) {
+        r[u] = pb.rec[ri];
+        ok[u] = r[u].row >= 0;
+      }
     }
 #pragma unroll
     for (int u = 0; u < R; ++u)
       if (ok[u]) {
-        const int64_t ri =
-            (int64_t)item[u].x * pb.cap + (item[u].y & 0xffff) * kBlock + threadIdx.x;
-        r[u] = pb.rec[ri];
-      }
-#pragma unroll
-    for (int u = 0; u < R; ++u)
-      if (ok[u]) {
-        const int64_t tile = item[u].x;
+        const int64_t ri = (it0 + u) * kBlock + threadIdx.x;
+        const int64_t tile = r[u].tile;
         const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
         int px, py;
         tile_pixel(tl % pb.ntx, tl / pb.ntx, r[u].q, px, py);
         const int64_t gp = ((int64_t)b * H + py) * W + px;
         gs[u] = a.grad_soft[gp];
         so[u] = a.soft_in[gp];
-        const int64_t ri =
-            (int64_t)item[u].x * pb.cap + (item[u].y & 0xffff) * kBlock + threadIdx.x;
         T v[6];
         load_corners(fs, (int64_t)r[u].row, v);
         const float M = fs.M;
-        soft_pair_coef<T>((T)px_cx(M, W, px), (T)px_cy(M, H, py), v, r[u].type, pb.sprob[ri], M,
+        et[u] = pb.stype[ri];
+        soft_pair_coef<T>((T)px_cx(M, W, px), (T)px_cy(M, H, py), v, et[u], pb.sprob[ri], M,
                           c[u].h);
       }
 #pragma unroll
@@ -682,12 +821,12 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
       T g[6] = {0, 0, 0, 0, 0, 0};
       if (ok[u]) {
         const double sp = -(double)a.sigmainv * (double)gs[u] * (1.0 - (double)so[u]);
-        soft_add_pair<T>(g, r[u].type, sp, c[u]);
+        soft_add_pair<T>(g, et[u], sp, c[u]);
         key = r[u].row;
       }
       // segmented inclusive scan over the wave's lanes; segments are the runs of equal key (a
-      // face may have several runs in a tile: one per wave sub-list chunk), numbered by the
-      // count of run heads up to the lane
+      // face may have several runs: one per wave sub-list chunk), numbered by the count of run
+      // heads up to the lane
       const int prev_key = __shfl_up(key, 1);
       const uint64_t heads = __ballot(lane == 0 || prev_key != key);
       const int seg = __popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
@@ -703,12 +842,61 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
       }
       const int next_key = __shfl_down(key, 1);
       const bool tail = key >= 0 && (lane == kWave - 1 || next_key != key);
-      if (tail && !(fs.dbg & 128)) {
+      if (tail) {
 #pragma unroll
         for (int q = 0; q < 6; ++q)
           if (g[q] != (T)0) atomicAdd(a.grad_fvi + (int64_t)key * 6 + q, g[q]);
       }
     }
+  }
+}
+
+// The backward of the tiles that streamed their soft mask (pool exhausted): the same walk again,
+// each pixel lane recomputing its pairs (bit-identical probabilities and types) and adding their
+// terms with float atomics.  One workgroup per such tile; a grid that finds none exits at once.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_soft_ovf_bwd(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  __shared__ TileLists L;
+  const int blk = blockIdx.x, nblk = gridDim.x;
+  const FaceSet<T> &fs = a.fs;
+  const int H = fs.H, W = fs.W, K = a.K;
+  const float M = fs.M;
+  const int novf = pb.counters[1];
+  for (int i = blk; i < novf; i += nblk) {
+    const int64_t tile = pb.ovf[i];
+    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+    int64_t lo, hi;
+    view_range(fs, b, lo, hi);
+    const TileGeom t = tile_geom(H, W, tl);
+    const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
+    const bool unc = t.inimg && a.face_idx[p] < 0;
+    const bool wave_unc = __ballot(unc) != 0ull;
+    const double sp =
+        unc ? -(double)a.sigmainv * (double)a.grad_soft[p] * (1.0 - (double)a.soft_in[p]) : 0.0;
+    const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
+    int my_kid = 0;
+    auto stage = [&](int, int64_t) {};
+    auto round = [&](int nsub, int) {
+      if (wave_unc)
+        for (int c = 0; c * kWave < nsub; ++c)
+          soft_chunk_stream(L, nsub, c, unc, K, t, lo, my_kid, [&](int64_t row, int) {
+            T v[6];
+            load_corners(fs, row, v);
+            int et = 0;
+            T prob = (T)0;
+            soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+            SoftCoef<T> cf;
+            soft_pair_coef<T>(x0, y0, v, et, prob, M, cf.h);
+            T g[6] = {0, 0, 0, 0, 0, 0};
+            soft_add_pair<T>(g, et, sp, cf);
+#pragma unroll
+            for (int q = 0; q < 6; ++q)
+              if (g[q] != (T)0) atomicAdd(a.grad_fvi + row * 6 + q, g[q]);
+          });
+    };
+    auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
+    if (__syncthreads_or(unc)) tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg, done);
+    __syncthreads();
   }
 }
 
@@ -735,6 +923,21 @@ __global__ __launch_bounds__(kBlock) void kd_dibr_bwd(SoftArgs<T> a, SoftPairBuf
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
+constexpr unsigned kOvfBlocks = 256;  // grid of the overflow kernels (exit at once when unused)
+
+template <typename T, bool FUSED>
+static void ovf_fwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipStream_t stream) {
+  ProfScope prof(K_SOFT_OVF_FWD, stream);
+  hipLaunchKernelGGL((kd_soft_ovf_fwd<T, FUSED>), dim3(kOvfBlocks), dim3(kBlock), 0, stream, a,
+                     pb);
+}
+
+template <typename T>
+static void ovf_bwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipStream_t stream) {
+  ProfScope prof(K_SOFT_OVF_BWD, stream);
+  hipLaunchKernelGGL((kd_soft_ovf_bwd<T>), dim3(kOvfBlocks), dim3(kBlock), 0, stream, a, pb);
+}
+
 template <typename T>
 int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce,
                       hipStream_t stream) {
@@ -749,6 +952,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
     // 6 workgroups per CU (the 16 KB record-index table); 4 and 8 measured no faster
     hipLaunchKernelGGL((kd_soft_pairs<T, true, 6>), dim3((unsigned)pb.ntiles, fs.B),
                        dim3(kBlock), 0, stream, a, pb);
+    ovf_fwd_launch<T, true>(a, pb, stream);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
     return KD_OK;
@@ -758,21 +962,18 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
     hipLaunchKernelGGL((kd_soft_pairs<T, false>), dim3((unsigned)pb.ntiles, fs.B), dim3(kBlock),
                        0, stream, a, pb);
   }
+  ovf_fwd_launch<T, false>(a, pb, stream);
   {
     ProfScope prof(K_SOFT_MATH, stream);
-    const bool lists = a.prob != nullptr;
     const dim3 grid(kMathBlocks);
-    if (lists)
-      hipLaunchKernelGGL((kd_soft_pair_math<T, true, kMathItems>), grid, dim3(kBlock), 0, stream,
-                         a, pb);
+    if (a.prob)
+      hipLaunchKernelGGL((kd_soft_pair_math<T, true>), grid, dim3(kBlock), 0, stream, a, pb);
     else
-      hipLaunchKernelGGL((kd_soft_pair_math<T, false, kMathItems>), grid, dim3(kBlock), 0,
-                         stream, a, pb);
+      hipLaunchKernelGGL((kd_soft_pair_math<T, false>), grid, dim3(kBlock), 0, stream, a, pb);
   }
   if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
-    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3((a.fs.dbg & 2048) ? kPersistentBlocks : 8192),
-                       dim3(kBlock), 0, stream, a, pb);
+    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(8192), dim3(kBlock), 0, stream, a, pb);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
@@ -795,6 +996,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
                        dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
                        stream, ra, a, pb);
   }
+  ovf_fwd_launch<float, true>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr fwd: %s", hipGetErrorString(e));
   return KD_OK;
@@ -813,7 +1015,7 @@ int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, boo
   a.bb.cull = nullptr;
   SoftPairBuf<T> pb = soft_pair_carve<T>(ws, off, fs.B, fs.H, fs.W, a.K);
   a.bb.clear = pb.counters;
-  a.bb.n_clear = 2;
+  a.bb.n_clear = 3;
   hipError_t e = bin_faces<T>(fs, a.bb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   return soft_pairs_launch<T>(a, pb, grad, reduce, stream);
@@ -828,6 +1030,7 @@ int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t s
     hipLaunchKernelGGL((kd_soft_bwd_items<T, 1>), dim3(kMathBlocks), dim3(kBlock), 0, stream, a,
                        pb);
   }
+  ovf_bwd_launch<T>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
   return KD_OK;
@@ -848,6 +1051,7 @@ int dibr_backward_merged_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, const Raster
     hipLaunchKernelGGL((kd_dibr_bwd<T>), dim3((unsigned)(nr + ns)), dim3(kBlock), 0, stream, a,
                        pb, ra, nr, ns, ntl);
   }
+  ovf_bwd_launch<T>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr bwd: %s", hipGetErrorString(e));
   return KD_OK;

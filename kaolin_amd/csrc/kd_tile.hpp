@@ -141,15 +141,16 @@ struct NeverDone {
 
 // `done()` (evaluated by every thread; must return a workgroup-uniform value, e.g. through
 // __syncthreads_and) lets a caller stop the walk once later faces cannot matter any more.
+// nview: faces of view b (rows [lo, lo + nview)), walked in full when the bin overflowed.
 template <typename Stage, typename Round, typename Done = NeverDone>
-__device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, int64_t N, int b,
+__device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, int nview, int b,
                                             int64_t lo, const TileGeom &t, Stage stage,
                                             Round round, int dbg = 0, Done done = Done()) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 / g.ct) * g.nctx + (t.X0 / g.ct);
-  const int n = t.nbin >= 0 ? t.nbin : bb.totals[(int64_t)b * g.nct() + ct];
-  const int *bin = bb.bins + (int64_t)ct * N + lo;
+  int n;
+  const int *bin = bin_list(bb, b, ct, lo, nview, t.nbin, n);
   int cnt = 0;
   // kPrefetch chunks of bin entries and their spans are loaded up front (two dependent
   // round trips per kPrefetch * 256 entries instead of per 256)
@@ -159,7 +160,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
 #pragma unroll
     for (int u = 0; u < kPrefetch; ++u) {
       const int e = base0 + u * kBlock + tid;
-      fr[u] = e < n ? bin[e] : 0;
+      fr[u] = e < n ? (bin ? bin[e] : e) : 0;
     }
 #pragma unroll
     for (int u = 0; u < kPrefetch; ++u) {

@@ -1,0 +1,220 @@
+"""GPU: the bounded workspace pools and their overflow paths.
+
+The workspace of dibr_rasterization / dibr_soft_mask holds two bounded pools whose layout is a
+pure function of the call's sizes (kd_binning.hpp, kd_soft.hpp): the coarse bins (16 entries per
+face row, handed to the bins by kd_bin_scan) and the soft mask's (pixel, close face) records
+(min(knum, 12) per pixel plus block slack, taken per wave by pass A).  What does not fit takes an
+overflow path -- a bin walks every face of its view, a tile computes its soft mask without
+records (kd_soft_ovf_fwd) and its backward recomputes the pairs (kd_soft_ovf_bwd) -- which may
+change the time, never the results.  kd_set_pool_limits lets a forward use only a fraction of
+each pool, so every path runs here:
+- forward outputs bit-identical to the default run (and to the oracle), gradients equal up to
+  the float atomics' summation order, for dibr_rasterization and dibr_soft_mask (fused one-launch
+  path, the split path at knum > 32, the close-list path);
+- a shape whose previous reservation ([coarse tiles] x [faces] bins, 256 x knum records per
+  tile: 437 GB) could not be allocated on a 288 GB MI355X runs in a 61 GB workspace, and its
+  views equal the same views rendered alone.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import TORCH_DTYPES
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+LIMITS = [(0.0, 0.0), (1.0, 0.0), (0.0, 1.0), (0.3, 0.05)]
+
+
+@pytest.fixture(autouse=True)
+def _native():
+    from kaolin_amd import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+    yield
+    _lib.set_pool_limits(1.0, 1.0)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def _views(n_lon, n_lat, h, B, dt=torch.float32, elevation=0.3, first_view=0, total_views=None):
+    from kaolin_amd import workloads
+    v = workloads.sphere_views(n_lon, n_lat, h, h, B, DEV, dtype=dt, seed=0,
+                               elevation=elevation, first_view=first_view,
+                               total_views=total_views)
+    return v['fvz'], v['fvi'].detach(), v['feats'].contiguous(), v['normals_z']
+
+
+def _grads(shape_feat, shape_soft, dt, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand(shape_feat, generator=g, dtype=torch.float64).to(DEV, dt),
+            torch.rand(shape_soft, generator=g, dtype=torch.float64).to(DEV, dt))
+
+
+def _dibr(h, fvz, fvi0, feats0, nz, limits, knum=30, sig=7000., box=0.02, seed=1):
+    from kaolin_amd import _lib
+    from kaolin_amd.render.mesh import dibr_rasterization
+    _lib.set_pool_limits(*limits)
+    try:
+        fvi = fvi0.clone().requires_grad_(True)
+        feats = feats0.clone().requires_grad_(True)
+        interp, soft, face_idx = dibr_rasterization(h, h, fvz, fvi, feats, nz, sig, box, knum)
+        g1, g2 = _grads(interp.shape, soft.shape, fvi.dtype, seed)
+        torch.autograd.backward([interp, soft], [g1, g2])
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_pool_limits(1.0, 1.0)
+    return interp, soft, face_idx, fvi.grad, feats.grad
+
+
+def _close(a, b, dt):
+    scale = b.abs().max().item()
+    tol = 1e-5 if dt == torch.float32 else 1e-10
+    torch.testing.assert_close(a, b, rtol=tol, atol=tol * 0.1 * scale)
+
+
+@pytest.mark.parametrize('limits', LIMITS)
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_dibr_rasterization_pool_overflow(limits, dname):
+    """C2's mesh and image (uv_sphere(100,51), 256x256), 2 views: every limit gives the default
+    run's outputs bit for bit and its gradients up to summation order; both match the oracle."""
+    dt = TORCH_DTYPES[dname]
+    h = 256
+    fvz, fvi, feats, nz = _views(100, 51, h, 2, dt)
+    ref = _dibr(h, fvz, fvi, feats, nz, (1.0, 1.0))
+    out = _dibr(h, fvz, fvi, feats, nz, limits)
+    for a, b in zip(out[:3], ref[:3]):
+        assert torch.equal(a, b)
+    _close(out[3], ref[3], dt)
+    _close(out[4], ref[4], dt)
+    # and the oracle's soft mask and gradient on the same views
+    valid = N(nz) >= 0
+    _, rf, rw = oracle.rasterize(h, h, N(fvz), N(fvi), N(feats), valid)
+    np.testing.assert_array_equal(N(out[2]), rf)
+    osoft, oprob, ocidx, octype, sfvi = oracle.soft_mask_forward(N(fvi), rf)
+    np.testing.assert_allclose(N(out[1]), osoft, rtol=1e-6, atol=1e-7)
+    g1, g2 = _grads(out[0].shape, out[1].shape, dt)
+    gr, _ = oracle.rasterize_backward(N(g1), rf, rw, N(fvi), N(feats), 1e-8)
+    gs = oracle.soft_mask_backward(N(g2), osoft, rf, oprob, ocidx, octype, sfvi, 7000, 1000.)
+    tol = 1e-4 if dname == 'f32' else 1e-9
+    np.testing.assert_allclose(N(out[3]), gr + gs, rtol=tol,
+                               atol=tol * 0.1 * np.abs(gr + gs).max())
+
+
+@pytest.mark.parametrize('limits', LIMITS)
+@pytest.mark.parametrize('knum', [30, 40])
+@pytest.mark.parametrize('lists', [False, True])
+def test_dibr_soft_mask_pool_overflow(limits, knum, lists):
+    """dibr_soft_mask alone: the one-launch path (knum 30), the split path (knum 40 > 32) and the
+    close-list path, each with the pools limited: soft mask (and lists) bit-identical to the
+    default run, gradient up to summation order."""
+    from kaolin_amd import _lib
+    from kaolin_amd.render.mesh import dibr, dibr_soft_mask, rasterize
+    h = 128
+    fvz, fvi0, feats, nz = _views(60, 31, h, 2)
+    _, face_idx = rasterize(h, h, fvz, fvi0, feats, nz >= 0)
+    _, g = _grads((1,), face_idx.shape, torch.float32, seed=3)
+
+    def run(lim):
+        fvi = fvi0.clone().requires_grad_(True)
+        _lib.set_pool_limits(*lim)
+        try:
+            with dibr.close_lists(lists):
+                soft = dibr_soft_mask(fvi, face_idx, 7000, 0.02, knum)
+                grad = torch.autograd.grad(soft, fvi, g)[0]
+            torch.cuda.synchronize()
+        finally:
+            _lib.set_pool_limits(1.0, 1.0)
+        return soft, grad
+
+    s0, g0 = run((1.0, 1.0))
+    s1, g1 = run(limits)
+    assert torch.equal(s0, s1)
+    _close(g1, g0, torch.float32)
+    osoft, oprob, ocidx, octype, sfvi = oracle.soft_mask_forward(N(fvi0), N(face_idx), 7000, 0.02,
+                                                                 knum)
+    np.testing.assert_allclose(N(s1), osoft, rtol=1e-6, atol=1e-7)
+    ref = oracle.soft_mask_backward(N(g), osoft, N(face_idx), oprob, ocidx, octype, sfvi, 7000,
+                                    1000.)
+    np.testing.assert_allclose(N(g1), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize('limits', [(0.0, 0.0), (0.5, 0.1)])
+def test_close_lists_op_pool_overflow(limits):
+    """The reference op with close-face lists (_C.render.mesh.dibr_soft_mask_forward_fused with
+    lists, the split pipeline) under limited pools: lists equal the oracle's element for
+    element."""
+    from kaolin_amd import _C, _lib
+    from kaolin_amd.render.mesh import rasterize
+    h, K = 96, 30
+    fvz, fvi, feats, nz = _views(40, 21, h, 2, elevation=0.5)
+    _, face_idx = rasterize(h, h, fvz, fvi, feats, nz >= 0)
+    _lib.set_pool_limits(*limits)
+    try:
+        soft, _, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
+            fvi, face_idx, 7000., 0.02, K, 1000., with_lists=True, want_grad=False)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_pool_limits(1.0, 1.0)
+    osoft, oprob, ocidx, octype, _ = oracle.soft_mask_forward(N(fvi), N(face_idx), 7000, 0.02,
+                                                              K)
+    np.testing.assert_array_equal(N(cidx), ocidx)
+    np.testing.assert_array_equal(N(ctype), octype)
+    np.testing.assert_allclose(N(prob), oprob, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+
+
+def _old_reservation(B, H, W, F, K, esize=4):
+    """Bytes the round-1 workspace reserved: two [coarse tiles] x [B F] int32 bin arrays plus
+    256 K records (12 B + the probability) per 16x16 tile (kd_binning.hip / kd_softpair.hip at
+    commit 783b9c0)."""
+    m, ct = max(H, W), 32
+    while (m + ct - 1) // ct > 32:
+        ct *= 2
+    nct = ((W + ct - 1) // ct) * ((H + ct - 1) // ct)
+    n = B * F
+    tiles = B * ((W + 15) // 16) * ((H + 15) // 16)
+    return 2 * nct * n * 4 + tiles * 256 * K * (12 + esize)
+
+
+def test_shape_beyond_the_old_reservation():
+    """16 views of the 50k-face sphere at 4096x4096 with knum 100: the old reservation (437 GB)
+    exceeds the MI355X's 288 GB; the bounded pools need ~61 GB.  Views are independent, so views
+    0 and 9 of the batch must equal the same views rendered alone (outputs bit-identical), and two
+    of their raster rows must equal the oracle."""
+    from kaolin_amd import _lib
+    h, B, K, F = 4096, 16, 100, 50000
+    old = _old_reservation(B, h, h, F, K)
+    new = _lib.load().kd_dibr_workspace_size(B, h, h, F, K, 0)
+    assert old > 288e9 and new < 0.25 * old, (old, new)
+    fvz, fvi, feats, nz = _views(250, 101, h, B)
+    assert fvi.shape[1] == F
+    out = _dibr(h, fvz, fvi, feats, nz, (1.0, 1.0), knum=K)
+    covered = out[2] >= 0
+    assert 0.2 < covered.float().mean().item() < 0.8
+    for v in (0, 9):
+        one = _dibr(h, fvz[v:v + 1], fvi[v:v + 1], feats[v:v + 1], nz[v:v + 1], (1.0, 1.0),
+                    knum=K)
+        for a, b in zip(out[:3], one[:3]):
+            assert torch.equal(a[v:v + 1], b)
+        # two raster rows (through the silhouette band and the middle) against the oracle's
+        # brute-force loops (the soft mask's K-lists at this size would take 22 GB of host
+        # memory: its oracle parity under the same pools is covered at the smaller shapes)
+        col = covered[v].any(dim=1).nonzero()
+        r_top = int(col.min().item())
+        for r0 in (r_top - 3, h // 2):
+            rows = (r0, r0 + 1)
+            valid = N(nz[v:v + 1]) >= 0
+            ri, rf, _ = oracle.rasterize(h, h, N(fvz[v:v + 1]), N(fvi[v:v + 1]),
+                                         N(feats[v:v + 1]), valid, rows=rows)
+            np.testing.assert_array_equal(N(one[2][:, r0:r0 + 1]), rf[:, r0:r0 + 1])
+            np.testing.assert_array_equal(N(one[0][:, r0:r0 + 1]), ri[:, r0:r0 + 1])
+    soft = out[1]
+    assert torch.equal(soft[covered], torch.ones_like(soft[covered]))
+    assert (soft >= 0).all() and (soft < 1).logical_or(covered).all()
+    assert (soft[~covered] > 0).any()
+    assert torch.isfinite(out[3]).all() and torch.isfinite(out[4]).all()
