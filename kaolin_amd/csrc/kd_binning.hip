@@ -20,7 +20,6 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view)
   s += align_up(sizeof(int) * (size_t)B * (size_t)(nchunk > 0 ? nchunk : 1) * g.nct());
   s += align_up(sizeof(int) * (size_t)B * g.nct());
   s += align_up(sizeof(int) * (size_t)B * g.nct());
-  s += align_up(sizeof(int) * (size_t)(B > 0 ? B : 1));
   s += align_up(sizeof(int) * (size_t)kBinEntriesPerFace * (size_t)(N > 0 ? N : 1));
   s += align_up(sizeof(float4) * 2 * (size_t)N);
   s += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
@@ -41,8 +40,6 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   off += align_up(sizeof(int) * (size_t)B * bb.g.nct());
   bb.base = (int *)(base + off);
   off += align_up(sizeof(int) * (size_t)B * bb.g.nct());
-  bb.cursor = (int *)(base + off);
-  off += align_up(sizeof(int) * (size_t)(B > 0 ? B : 1));
   bb.bins = (int *)(base + off);
   bb.xper = kBinEntriesPerFace;
   bb.limit = pool_limit_bins();
@@ -139,7 +136,6 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   const int nct = bb.g.nct();
   for (int c = tid; c < nct; c += kBlock) s_cnt[c] = 0;
   if (bb.clear && b == 0 && chunk == 0 && tid < bb.n_clear) bb.clear[tid] = 0;
-  if (chunk == 0 && tid == 0) bb.cursor[b] = 0;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   __syncthreads();
@@ -185,14 +181,10 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 // One wave per (coarse tile, view, set), four per workgroup: exclusive scan of counts[b][*][c]
 // over the chunks.  Lane l owns the contiguous run of chunks [l*per, l*per + per), held in
 // registers; the run sums are scanned with DPP (wave_incl_scan).  No LDS, no barriers: every
-// wave's loads are in flight at once and the grid is one round on the chip.  Then the
-// workgroup's four bins take their room in the view's region with one atomic on its cursor; a
-// bin past the usable end of the region is marked overflowed (base -1, see kd_binning.hpp).
+// wave's loads are in flight at once and the grid is one round on the chip.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
-  const FaceSet<T> &fs = jobs.fs[blockIdx.z];
   const BinBuffers &bb = jobs.bb[blockIdx.z];
-  __shared__ int s_tot[kBlock / kWave], s_base;
   const int nct = bb.g.nct();
   const int wv = threadIdx.x >> 6;
   const int c = blockIdx.x * (kBlock / kWave) + wv;
@@ -239,24 +231,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
       }
     }
   }
-  if (lane == 0) s_tot[wv] = live ? total : 0;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int sum = 0;
-#pragma unroll
-    for (int k = 0; k < kBlock / kWave; ++k) sum += s_tot[k];
-    s_base = sum > 0 ? atomicAdd(&bb.cursor[b], sum) : 0;
-  }
-  __syncthreads();
-  if (live && lane == 0) {
-    int off = s_base;
-    for (int k = 0; k < wv; ++k) off += s_tot[k];
-    int64_t lo, hi;
-    view_range(fs, b, lo, hi);
-    const int64_t room = (int64_t)((double)bb.limit * (double)bb.xper * (double)(hi - lo));
-    bb.totals[(int64_t)b * nct + c] = total;
-    bb.base[(int64_t)b * nct + c] = (int64_t)off + total <= room ? off : -1;
-  }
+  if (live && lane == 0) bb.totals[(int64_t)b * nct + c] = total;
 }
 
 template <typename T>
@@ -272,6 +247,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
   // each thread holds faces tid and tid + 256.
   constexpr int kWords = kChunk / 32, kPerT = kChunk / kBlock;
   extern __shared__ uint32_t s_mask[];  // [nct][kWords]
+  __shared__ int s_bbase[kMaxCtiles], s_scan[kBlock / kWave];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
   for (int k = tid; k < nct * kWords; k += kBlock) s_mask[k] = 0u;
@@ -283,6 +259,33 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
     const int64_t i = lo + (int64_t)chunk * kChunk + u * kBlock + tid;
     sp[u] = Span{1, 0, 1, 0};
     if (i < hi) sp[u] = bb.spans[i];
+  }
+  {
+    // the view's bins in its region [xper*lo, xper*hi): exclusive scan of the totals over the
+    // coarse tiles (every workgroup of the view computes the same bases; chunk 0 stores them
+    // for the tile kernels); a bin past the usable end of the region overflows (base -1)
+    constexpr int kPer = kMaxCtiles / kBlock;
+    const int *tot = bb.totals + (int64_t)b * nct;
+    int v[kPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int c = tid * kPer + k;
+      v[k] = c < nct ? tot[c] : 0;
+      sum += v[k];
+    }
+    int all;
+    int run = wg_exclusive_scan(sum, s_scan, all);
+    const int64_t room = (int64_t)((double)bb.limit * (double)bb.xper * (double)(hi - lo));
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int c = tid * kPer + k;
+      if (c < nct) {
+        const int bc = (int64_t)run + v[k] <= room ? run : -1;
+        s_bbase[c] = bc;
+        if (chunk == 0) bb.base[(int64_t)b * nct + c] = bc;
+      }
+      run += v[k];
+    }
   }
   __syncthreads();
 #pragma unroll
@@ -297,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
   }
   __syncthreads();
   const int *offs = bb.counts + ((int64_t)b * bb.nchunk + chunk) * nct;
-  const int *bbase = bb.base + (int64_t)b * nct;
+  const int *bbase = s_bbase;
   int *bins = bb.bins + (int64_t)bb.xper * lo;
 #pragma unroll
   for (int u = 0; u < kPerT; ++u) {

@@ -7,21 +7,20 @@
 // order, produced without sorting by a three-pass counting scatter:
 //   1. kd_bin_count   one workgroup per (256-face chunk, view): each face computes its exact
 //                     pixel span (kd::make_span), stores it, and counts per coarse tile in LDS.
-//   2. kd_bin_scan    one wave per (coarse tile, view): exclusive scan over the chunks; each
-//                     workgroup (4 bins of a view) then takes its bins' room from the view's
-//                     region with one atomic.
+//   2. kd_bin_scan    one wave per (coarse tile, view): exclusive scan over the chunks.
 //   3. kd_bin_scatter one workgroup per (chunk, view): the rank of a face inside its chunk for a
 //                     tile is a popcount over an LDS bitmask of the chunk's faces touching that
 //                     tile, so the global position is scan offset + rank: ascending by face.
+//                     Each workgroup scans its view's totals over the coarse tiles to place the
+//                     bins in the view's region (CSR; the chunk-0 workgroup stores the bases).
 // Layout in the workspace (N = rows of the face arrays):
 //   spans  [N]           Span (8 B)
 //   counts [B][nchunk][nct] int32 (turned into exclusive offsets by the scan)
 //   totals [B][nct]      int32
 //   base   [B][nct]      int32 start of bin (b, c) inside view b's region, -1 = overflowed
-//   cursor [B]           int32 allocation cursor of each view's region (kd_bin_scan)
 //   bins   [xper * N]    int32 local face index; view b owns the region [xper*lo, xper*hi) of
-//                        its rows [lo, hi) and kd_bin_scan hands each of its bins a contiguous
-//                        piece of it (one atomic per 4 bins).  A bin that does not fit is marked
+//                        its rows [lo, hi), its bins packed in coarse-tile order (exclusive
+//                        scan of the totals, kd_bin_scatter).  A bin that does not fit is marked
 //                        overflowed: its tiles walk every face of the view (entry e = face e),
 //                        which the exact span filter of the walk turns into the same face list,
 //                        so an overflow costs time, never correctness.
@@ -43,7 +42,6 @@ struct BinBuffers {
   int *counts;
   int *totals;
   int *base;       // [B][nct]: start of bin (b, c) in view b's region, -1 = overflowed
-  int *cursor;     // [B]: region cursors (zeroed by kd_bin_count)
   int *bins;
   int xper;        // region entries per face row
   float limit;     // usable fraction of each region (kd_set_pool_limits; 1 in production)

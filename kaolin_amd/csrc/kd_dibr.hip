@@ -89,7 +89,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   d.rbb.cull_eps = eps;
   d.sbb.cull = nullptr;
   d.sbb.clear = d.pb.counters;
-  d.sbb.n_clear = 3;
+  d.sbb.n_clear = kPairClear;
   hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> ra{rfs, d.rbb, fvz, fvz_fs, fvz_cs, feat, D, eps, interp, face_idx, weights};

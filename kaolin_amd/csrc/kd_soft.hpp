@@ -150,11 +150,10 @@ __device__ __forceinline__ void soft_stage(const FaceSet<T> &fs, T (*geo)[kCap],
 // pair pipeline of the autograd path (kd_softpair.hip)
 // ------------------------------------------------------------------------------------------
 struct SoftPairRec {
-  int32_t row;    // face row (view offset + face index); -1: unused pool entry
-  uint32_t tile;  // view * tiles + fine tile
+  int32_t row;    // face row (view offset + face index)
   uint16_t slot;  // close-face slot of the pixel, 0..K-1
   uint8_t q;      // pixel of the tile (tile_geom thread index)
-  uint8_t pad;
+  uint8_t type;   // distance type 0..5 (set by the pair math, while the line is in L2)
 };
 
 template <typename T>
@@ -162,32 +161,45 @@ struct SoftCoef {
   T h[4];
 };
 
-constexpr int kFuseSlots = 32;      // knum bound of the one-launch soft mask (LDS slot table)
-constexpr int kMaxWaveBlocks = 32;  // pool blocks one wave can hold in a tile (64 K records)
-constexpr int kPoolPairsPerPixel = 12;  // record pool: min(knum, 12) pairs per pixel + slack
+constexpr int kFuseSlots = 32;           // knum bound of the one-launch soft mask (LDS slot table)
+constexpr int kPoolPairsPerPixel = kFuseSlots;  // record pool: min(knum, 32) records per pixel
 
-// The record pool.  Records are written by pass A, one wave's records at a time into pool
-// blocks of bs = 64 * 2^s records (64 * knum records per wave need at most 32 blocks) taken with
-// one device atomic per block run; every taken block ends up holding valid records or row -1
-// (the tail of a wave's last block, the blocks of a tile that overflowed), so the backward runs
-// flat over the taken blocks.  A tile whose wave finds the pool exhausted drops its records and
-// computes its soft mask without them (`ovf` list); its backward recomputes the pairs.
+// One backward / pair-math work item: up to 256 consecutive records of one tile.
+struct PairItem {
+  int64_t start;  // first record
+  int32_t tile;   // view * tiles + fine tile
+  int32_t n;      // records (<= 256)
+};
+
+// The record pool (12 B per pair in fp32: the record and its probability).  A tile reserves,
+// with one device atomic at the start of its soft phase, room for the most records it can
+// produce -- its uncovered pixels x min(knum, faces of its soft coarse bin) -- and pass A fills
+// it in order (face-major runs per wave chunk, an LDS counter); reserved room that stays unused
+// is never touched.  The pair math and the backward find the records through PairItems.  The
+// pool holds min(knum, 32) records per pixel, so with knum <= 32 every tile fits: then each tile
+// simply owns 256 knum records (no atomic; `fixed`).  Otherwise (or
+// under kd_set_pool_limits) a tile whose reservation does not fit computes its soft mask without
+// records (`ovf` list, kd_soft_ovf_fwd) and its backward recomputes the pairs
+// (kd_soft_ovf_bwd).
 template <typename T>
 struct SoftPairBuf {
-  SoftPairRec *rec;   // [cap_blocks * bs]
-  T *sprob;           // [cap_blocks * bs] probability of each record
-  uint8_t *stype;     // [cap_blocks * bs] distance type 0..5 of each record
-  int32_t *npix;      // [P] close faces of each uncovered pixel (split pipeline)
-  int32_t *ntile;     // [tiles] records of each tile (diagnostics)
-  int32_t *ovf;       // [tiles] tiles that computed their soft mask without records
-  int32_t *tblk;      // [tiles][4][kMaxWaveBlocks] each wave's blocks (split pipeline)
-  int32_t *twn;       // [tiles][4] each wave's records (split pipeline)
-  int32_t *tiles;     // [tiles] tiles with records (split pipeline)
-  int32_t *counters;  // [4]: blocks taken, overflow tiles, tiles with records (zeroed by
-                      // kd_bin_count), usable blocks of the forward (written by it)
-  int64_t ntiles, npixels, cap_blocks, lim_blocks;
-  int bs, bs_shift, ntx;
+  SoftPairRec *rec;    // [cap]
+  T *sprob;            // [cap] probability of each record
+  int64_t *tbase;      // [tiles] first record of each tile
+  int32_t *npix;       // [P] close faces of each uncovered pixel (split pipeline)
+  int32_t *ntile;      // [tiles] records of each tile
+  PairItem *items;     // [cap / 256 + tiles]
+  int32_t *tiles;      // [tiles] tiles with records (split pipeline's reduce)
+  int32_t *ovf;        // [tiles] tiles that computed their soft mask without records
+  int32_t *counters;   // [4]: items, tiles with records, overflow tiles, unused; then the 64-bit
+                       // record cursor (all zeroed by kd_bin_count: n_clear = 6)
+  unsigned long long *cursor;
+  int64_t ntiles, npixels, cap, lim;  // lim: records a forward may use (kd_set_pool_limits)
+  int fixed;  // knum <= 32 and the whole pool usable: tile t owns records [t * 256 K, +256 K)
+  int ntx;
 };
+
+constexpr int kPairClear = 6;  // ints of SoftPairBuf::counters (with the cursor) to zero
 
 // bins + pair buffers for B views of F faces, K close faces, element size esize
 size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize);

@@ -6,8 +6,9 @@
 // ~16 pairs each at C3).
 //   kd_soft_pairs<FUSED>  one workgroup per 16x16 tile: walks the tile's ordered bin
 //                      (kd_tile.hpp); pass A picks each uncovered pixel's first K close faces by
-//                      face index and writes (pixel, slot, face) records into the record pool
-//                      (SoftPairBuf, kd_soft.hpp), stopping once every uncovered pixel holds K.
+//                      face index and writes (pixel, slot, face) records into the tile's room
+//                      of the record pool (SoftPairBuf, kd_soft.hpp), stopping once every
+//                      uncovered pixel holds K.
 //                      FUSED (knum <= 32, no close lists): the same workgroup then does the pair
 //                      math over its records (distance type and probability, bit-identical to
 //                      the reference) and the ordered product soft = 1 - prod(1 - p)
@@ -15,17 +16,17 @@
 //                      in one launch.
 //   kd_soft_pair_math, kd_soft_reduce   the same math and product as separate launches, for
 //                      the op form with the reference's close-face lists (and knum > 32).
-//   kd_soft_bwd_items  the backward, flat over the pool's 256-record items, then the tiles that
-//                      overflowed the pool (their pairs recomputed).
+//   kd_soft_bwd_items  the backward, flat over (tile, 256-record) items.
+//   kd_soft_ovf_fwd / kd_soft_ovf_bwd   the tiles whose room did not fit the pool.
 //   kd_dibr_fwd_tiles  dibr_rasterization's forward: per tile, the raster pair pipeline
 //                      (kd_raster_pairs.hpp) and then the FUSED soft mask of the same tile.
 //   kd_dibr_bwd        dibr_rasterization's backward: the raster backward's tiles
 //                      (kd_raster_bwd.hpp) and the soft items in one grid.
-// Pool overflow (a workload with more pairs than the pool's min(knum, 12) per pixel, or
-// kd_set_pool_limits): the tile drops its records and runs the same walk again, each pixel lane
-// computing its pairs' probabilities in slot order and the product directly ("streaming": the
-// reference's per-pixel loop over the tile's face list), so the soft mask is bit-identical; its
-// backward walks the tile again in kd_soft_bwd_items.
+// Pool overflow (tiles reserving more than the pool's min(knum, 24) records per pixel, or
+// kd_set_pool_limits): the tile writes no records; kd_soft_ovf_fwd runs its walk again, each
+// pixel lane computing its pairs' probabilities in slot order and the product directly
+// ("streaming": the reference's per-pixel loop over the tile's face list), so the soft mask is
+// bit-identical; kd_soft_ovf_bwd walks it again for the backward.
 // Backward factorisation: the reference's per-pair gradient (dibr_soft_mask_cuda.cu:281-348) is
 //   dLdz * f_j / M  with  dLdz = -sigmainv * dLdp * (1 - soft) / (1 - p + 1e-7) * p
 // and f_j the geometric factors of the distance type (2(x1 - x0) ... for a vertex, the four
@@ -42,37 +43,27 @@ namespace kd {
 
 constexpr unsigned kMathBlocks = 8192;  // pair-math / backward-item grid
 
-// Pool blocks are 64 << shift records: 64 * knum records of one wave fit kMaxWaveBlocks blocks.
-static int pool_shift(int K) {
-  int s = 0;
-  while ((kMaxWaveBlocks << s) < K) ++s;
-  return s;
-}
-
-static int64_t pool_blocks(int B, int H, int W, int K) {
-  const int64_t bs = (int64_t)kWave << pool_shift(K);
+// Records of the pool: min(knum, kPoolPairsPerPixel) per tile pixel (every tile fits when
+// knum <= 32).
+static int64_t pool_records(int B, int H, int W, int K) {
   const int64_t ntiles = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-  const int64_t P = (int64_t)B * H * W, tiles = (int64_t)B * ntiles;
-  // pairs + on average one partly used block per tile (a tile that does not fit streams)
-  const int64_t recs = P * std::min(K, kPoolPairsPerPixel) + tiles * bs;
-  return (recs + bs - 1) / bs;
+  return (int64_t)B * ntiles * kBlock * std::min(K, kPoolPairsPerPixel);
 }
 
 size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize) {
   const int64_t ntiles = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
   const int64_t tiles = (int64_t)B * ntiles, P = (int64_t)B * H * W;
-  const int64_t recs = pool_blocks(B, H, W, K) << (6 + pool_shift(K));
+  const int64_t recs = pool_records(B, H, W, K);
   size_t s = bin_workspace_bytes(B, H, W, N, F);
   s += align_up(sizeof(SoftPairRec) * (size_t)recs);
   s += align_up((size_t)esize * (size_t)recs);
-  s += align_up((size_t)recs);
+  s += align_up(sizeof(int64_t) * (size_t)tiles);
   s += align_up(sizeof(int32_t) * (size_t)P);
   s += align_up(sizeof(int32_t) * (size_t)tiles);
+  s += align_up(sizeof(PairItem) * (size_t)(recs / kBlock + tiles));
   s += align_up(sizeof(int32_t) * (size_t)tiles);
-  s += align_up(sizeof(int32_t) * 4 * kMaxWaveBlocks * (size_t)tiles);
-  s += align_up(sizeof(int32_t) * 4 * (size_t)tiles);
   s += align_up(sizeof(int32_t) * (size_t)tiles);
-  s += align_up(sizeof(int32_t) * 4);
+  s += align_up(sizeof(int32_t) * 8);
   return s;
 }
 
@@ -81,41 +72,32 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   SoftPairBuf<T> pb;
   pb.ntx = (W + kTile - 1) / kTile;
   pb.ntiles = (int64_t)pb.ntx * ((H + kTile - 1) / kTile);
-  pb.bs_shift = 6 + pool_shift(K);
-  pb.bs = 1 << pb.bs_shift;
-  pb.cap_blocks = pool_blocks(B, H, W, K);
-  pb.lim_blocks = (int64_t)((double)pool_limit_pairs() * (double)pb.cap_blocks);
+  pb.cap = pool_records(B, H, W, K);
+  pb.lim = (int64_t)((double)pool_limit_pairs() * (double)pb.cap);
+  pb.fixed = K <= kPoolPairsPerPixel && pb.lim >= pb.cap;
   const int64_t tiles = (int64_t)B * pb.ntiles, P = (int64_t)B * H * W;
-  const int64_t recs = pb.cap_blocks << pb.bs_shift;
   pb.npixels = P;
   char *base = (char *)ws;
   pb.rec = (SoftPairRec *)(base + off);
-  off += align_up(sizeof(SoftPairRec) * (size_t)recs);
+  off += align_up(sizeof(SoftPairRec) * (size_t)pb.cap);
   pb.sprob = (T *)(base + off);
-  off += align_up(sizeof(T) * (size_t)recs);
-  pb.stype = (uint8_t *)(base + off);
-  off += align_up((size_t)recs);
+  off += align_up(sizeof(T) * (size_t)pb.cap);
+  pb.tbase = (int64_t *)(base + off);
+  off += align_up(sizeof(int64_t) * (size_t)tiles);
   pb.npix = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)P);
   pb.ntile = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
-  pb.ovf = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * (size_t)tiles);
-  pb.tblk = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * 4 * kMaxWaveBlocks * (size_t)tiles);
-  pb.twn = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * 4 * (size_t)tiles);
+  pb.items = (PairItem *)(base + off);
+  off += align_up(sizeof(PairItem) * (size_t)(pb.cap / kBlock + tiles));
   pb.tiles = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
+  pb.ovf = (int32_t *)(base + off);
+  off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.counters = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * 4);
+  pb.cursor = (unsigned long long *)(pb.counters + 4);
+  off += align_up(sizeof(int32_t) * 8);
   return pb;
-}
-
-// Blocks of the pool a backward reads: those the forward took, up to its usable limit.
-__device__ __forceinline__ int64_t pool_used_records(const int32_t *counters, int bs_shift) {
-  const int64_t taken = counters[0], lim = counters[3];
-  return (taken < lim ? taken : lim) << bs_shift;
 }
 
 // pixel of tile-local thread index q (kd_tile.hpp tile_geom layout)
@@ -230,51 +212,15 @@ __device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, i
   return sel;
 }
 
-// One wave's records of the current tile: n records in the pool blocks blk[0 .. nblk) (LDS).
-struct WavePool {
-  int n, nblk;
-  int *blk;
-  bool ovf;
-};
-
-template <typename T>
-__device__ __forceinline__ int64_t pool_index(const SoftPairBuf<T> &pb, const int *blk, int j) {
-  return ((int64_t)blk[j >> pb.bs_shift] << pb.bs_shift) + (j & (pb.bs - 1));
-}
-
-// Room for `tot` more records of this wave (wave-uniform): one device atomic per run of new
-// blocks.  false: the usable pool is exhausted; the part of the failed run inside it is marked
-// unused (the backward reads every taken block).
-template <typename T>
-__device__ __forceinline__ bool wave_reserve(const SoftPairBuf<T> &pb, WavePool &wp, int tot) {
-  const int lane = threadIdx.x & 63;
-  const int need = wp.n + tot - (wp.nblk << pb.bs_shift);
-  if (need <= 0) return true;
-  const int nnew = (need + pb.bs - 1) >> pb.bs_shift;
-  int g0 = 0;
-  if (lane == 0) g0 = atomicAdd(&pb.counters[0], nnew);
-  g0 = __builtin_amdgcn_readfirstlane(g0);
-  if ((int64_t)g0 + nnew > pb.lim_blocks || wp.nblk + nnew > kMaxWaveBlocks) {
-    const int64_t e = min((int64_t)g0 + nnew, pb.lim_blocks) << pb.bs_shift;
-    for (int64_t i = ((int64_t)g0 << pb.bs_shift) + lane; i < e; i += kWave) pb.rec[i].row = -1;
-    return false;
-  }
-  if (lane < nnew) wp.blk[wp.nblk + lane] = g0 + lane;
-  wp.nblk += nnew;
-  return true;
-}
-
 // One 64-face chunk of a wave's sub-list: each uncovered pixel lane takes its chunk_select faces.
 // Records are placed face-major (face j's pixels contiguous, pixels ascending): the transposed
 // selections give each face its record count and offset; each pixel lane then writes its own
 // records (slot = its running close-face count) at offset[j] + rank of the pixel in face j.
-template <typename T>
 __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
                                                    int K, const TileGeom &t, int64_t lo,
-                                                   uint32_t tile, int &my_kid, uint64_t *s_pm,
-                                                   unsigned short *s_off,
-                                                   const SoftPairBuf<T> &pb, WavePool &wp,
-                                                   int *s_ovf,
+                                                   int &my_kid, uint64_t *s_pm,
+                                                   unsigned short *s_off, int *s_nrec,
+                                                   SoftPairRec *rec,
                                                    unsigned short (*s_ridx)[kBlock] = nullptr) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
@@ -284,13 +230,9 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
   const int incl = wave_incl_scan(cnt);
   const int tot = __builtin_amdgcn_readlane(incl, 63);
   if (tot == 0) return;
-  if (!wave_reserve(pb, wp, tot)) {
-    wp.ovf = true;
-    if (lane == 0) *s_ovf = 1;
-    return;
-  }
-  const int base = wp.n;
-  wp.n += tot;
+  int base = 0;
+  if (lane == 0) base = atomicAdd(s_nrec, tot);
+  base = __builtin_amdgcn_readfirstlane(base);
   s_pm[lane] = pm;
   s_off[lane] = (unsigned short)(incl - cnt);
   wave_lds_sync();
@@ -303,13 +245,12 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
     const int kk = L.sub[w][c * kWave + jj];
     SoftPairRec r;
     r.row = (int32_t)(lo + L.f[kk]);
-    r.tile = tile;
     r.slot = (uint16_t)slot++;
     r.q = (uint8_t)tile_q;
-    r.pad = 0;
+    r.type = 0;
     const int ri = base + s_off[jj] + __popcll(s_pm[jj] & below);
-    pb.rec[pool_index(pb, wp.blk, ri)] = r;
-    if (s_ridx) s_ridx[r.slot][tile_q] = (unsigned short)ri;  // (slot, pixel) -> wave record
+    rec[ri] = r;
+    if (s_ridx) s_ridx[r.slot][tile_q] = (unsigned short)ri;  // (slot, pixel) -> record
   }
   my_kid = slot;
   wave_lds_sync();
@@ -339,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
-  const int novf = pb.counters[1];
+  const int novf = pb.counters[2];
   for (int i = blockIdx.x; i < novf; i += gridDim.x) {
     const int64_t tile = pb.ovf[i];
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
@@ -384,17 +325,15 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
 // Records of one tile's pixel set (pass A).  FUSED (knum <= kFuseSlots, no close-face lists):
 // the same workgroup then runs the pair math over its own records and the ordered product of
 // each pixel's slots -- the whole soft mask in one launch.  Pass A notes each (slot, pixel)'s
-// record (its index among the wave's records) in LDS, so the product reads the probabilities
-// in slot order.
+// record in LDS, so the product reads the probabilities in slot order.
 template <bool FUSED>
 struct SoftPairsLDS {
   unsigned short ridx[FUSED ? kFuseSlots : 1][kBlock];
   TileLists L;
   uint64_t pm[4][kWave];
   unsigned short off[4][kWave];
-  int blk[4][kMaxWaveBlocks];
-  int wn[4], box[4];
-  int ovf;
+  int64_t base;
+  int nrec, ibase, box[4];
 };
 
 // Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
@@ -416,15 +355,11 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   if (fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, coarse count) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
-  if (tid == 0 && blockIdx.x == 0 && blockIdx.y == 0)
-    pb.counters[3] = (int32_t)pb.lim_blocks;  // the pool this forward may use (for the readers)
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const bool unc = t.inimg && a.face_idx[p] < 0;
   const bool wave_unc = __ballot(unc) != 0ull;
   const int64_t tile = (int64_t)b * pb.ntiles + tl;
-  WavePool wp{0, 0, S.blk[w], false};
   int my_kid = 0;
-  if (tid == 0) S.ovf = 0;
 
   // faces matter only where they reach an uncovered pixel: the filter boxes of tile_rounds
   // shrink to the uncovered pixels' bounding boxes (exact: a record needs the pixel centre
@@ -433,6 +368,8 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   if (tid == 0) {
     s_box[0] = s_box[2] = 1 << 30;
     s_box[1] = s_box[3] = -1;
+    S.nrec = 0;
+    S.base = -1;
   }
   {
     const uint64_t um = __ballot(unc);
@@ -454,41 +391,60 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     atomicMin(&s_box[2], t.SY0);
     atomicMax(&s_box[3], t.SY1);
   }
+  const int U = __syncthreads_count(unc);
   bool ovf = false;
-  auto stage = [&](int, int64_t) {};  // pass A needs the spans only
-  // once every uncovered pixel holds K close faces, later faces cannot enter
-  auto all_full = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
-  if (__syncthreads_or(unc)) {
+  if (U > 0) {
+    // the tile's room in the pool: its own 256 K records (`fixed`), or, reserved with one device
+    // atomic, min(K, faces of the tile's soft coarse bin) per uncovered pixel; the atomic's
+    // latency overlaps the walk's first loads (records are written after a barrier of
+    // tile_rounds)
+    if (pb.fixed) {
+      if (tid == 0) S.base = tile * kBlock * K;
+    } else if (tid == 0) {
+      const BinGeom &g = a.bb.g;
+      const int ct = (t.Y0 / g.ct) * g.nctx + (t.X0 / g.ct);
+      int nb;
+      bin_list(a.bb, b, ct, lo, nview, nbin, nb);
+      const int64_t room = (int64_t)U * (int64_t)min(K, nb);
+      if (room > 0) {
+        const int64_t b0 = (int64_t)atomicAdd(pb.cursor, (unsigned long long)room);
+        S.base = b0 + room <= pb.lim ? b0 : -2;  // -2: the pool is exhausted
+      }
+    }
     t.FX0 = s_box[0];
     t.FX1 = s_box[1];
     t.FY0 = s_box[2];
     t.FY1 = s_box[3];
+    auto stage = [&](int, int64_t) {};  // pass A needs the spans only
     auto round = [&](int nsub, int) {
       if (wave_unc && !(fs.dbg & 1024))
-        for (int c = 0; c * kWave < nsub && !wp.ovf; ++c)
-          soft_chunk_records<T>(L, nsub, c, unc, K, t, lo, (uint32_t)tile, my_kid, S.pm[w],
-                                S.off[w], pb, wp, &S.ovf, FUSED ? S.ridx : nullptr);
+        for (int c = 0; c * kWave < nsub; ++c)
+          soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], &S.nrec,
+                             pb.rec + S.base, FUSED ? S.ridx : nullptr);
     };
-    // (a wave that found the pool exhausted ends the walk at the next round)
-    auto done = [&]() { return all_full() || S.ovf != 0; };
-    tile_rounds(L, a.bb, nview, b, lo, t, stage, round, fs.dbg, done);
-    ovf = S.ovf != 0;  // tile_rounds ends on a barrier
+    // once every uncovered pixel holds K close faces, later faces cannot enter; a tile without
+    // room in the pool stops at the first barrier
+    auto done = [&]() {
+      return __syncthreads_and(!unc || my_kid >= K) != 0 || S.base == -2;
+    };
+    // (S.base == -2 is visible from tile_rounds' first barrier on, before any record is written)
+    auto round_checked = [&](int nsub, int cnt) {
+      if (S.base >= 0) round(nsub, cnt);
+    };
+    tile_rounds(L, a.bb, nview, b, lo, t, stage, round_checked, fs.dbg, done);
+    __syncthreads();
+    ovf = S.base == -2;
   }
-  if (ovf) {
-    // the pool is exhausted: drop this tile's records (every block its waves took); its soft
-    // mask is computed by kd_soft_ovf_fwd and its backward by kd_soft_ovf_bwd (pb.ovf)
-    for (int i = lane; i < (wp.nblk << pb.bs_shift); i += kWave)
-      pb.rec[pool_index(pb, wp.blk, i)].row = -1;
-    wp.n = 0;
+  if (ovf) {  // no records: kd_soft_ovf_fwd computes the tile's soft mask, kd_soft_ovf_bwd its
+              // backward
     my_kid = 0;
-    if (tid == 0) pb.ovf[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
-  } else {
-    // the unused tail of each wave's last block
-    for (int i = wp.n + lane; i < (wp.nblk << pb.bs_shift); i += kWave)
-      pb.rec[pool_index(pb, wp.blk, i)].row = -1;
+    if (tid == 0) {
+      pb.ovf[atomicAdd(&pb.counters[2], 1)] = (int32_t)tile;
+      S.nrec = 0;
+    }
   }
   if (t.inimg) {
-    if (!FUSED) pb.npix[p] = (unc && !ovf) ? my_kid : 0;  // the split pipeline's reduce
+    if (!FUSED) pb.npix[p] = my_kid;  // the split pipeline's reduce
     if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
     else if (a.soft && my_kid == 0) a.soft[p] = (T)0.0;
     if (a.last && my_kid < K) a.last[p] = -1;
@@ -499,15 +455,23 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
         a.ctype[p * K + s] = 0;
       }
   }
-  if (lane == 0) S.wn[w] = wp.n;
   __syncthreads();
-  const int n0 = S.wn[0], n01 = n0 + S.wn[1], n012 = n01 + S.wn[2], n = n012 + S.wn[3];
-  if (tid == 0) pb.ntile[tile] = n;
-  if (!FUSED && n > 0) {  // where the split pipeline's reduce finds this tile's records
-    if (tid < 4 * kMaxWaveBlocks)
-      pb.tblk[tile * 4 * kMaxWaveBlocks + tid] = S.blk[tid / kMaxWaveBlocks][tid % kMaxWaveBlocks];
-    if (tid < 4) pb.twn[tile * 4 + tid] = S.wn[tid];
-    if (tid == 0) pb.tiles[atomicAdd(&pb.counters[2], 1)] = (int32_t)tile;
+  const int n = S.nrec;
+  const int64_t base = S.base;
+  if (tid == 0) {
+    pb.ntile[tile] = n;
+    pb.tbase[tile] = n > 0 ? base : 0;
+  }
+  if (n > 0) {  // work items of the math and backward passes
+    const int nch = (n + kBlock - 1) / kBlock;
+    if (tid == 0) {
+      S.ibase = atomicAdd(&pb.counters[0], nch);
+      if (!FUSED) pb.tiles[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
+    }
+    __syncthreads();
+    for (int c = tid; c < nch; c += kBlock)
+      pb.items[S.ibase + c] =
+          PairItem{base + (int64_t)c * kBlock, (int32_t)tile, min(kBlock, n - c * kBlock)};
   }
   if constexpr (FUSED) {
     // side job of the launch: the backward's gradient buffers (grid-stride, coalesced)
@@ -521,13 +485,12 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
         a.zero1[i - a.nzero0] = (T)0;
     }
     if (n == 0) return;
-    // pair math over this tile's records: record i of the tile is record j of wave ww
+    // pair math over this tile's records (record order: coalesced reads)
     const int tx = tl % pb.ntx, ty = tl / pb.ntx;
+    const SoftPairRec *rec = pb.rec + base;
+    T *sp = pb.sprob + base;
     for (int i = tid; i < n; i += kBlock) {
-      const int ww = (i >= n0) + (i >= n01) + (i >= n012);
-      const int j = i - (ww == 0 ? 0 : ww == 1 ? n0 : ww == 2 ? n01 : n012);
-      const int64_t ri = pool_index(pb, S.blk[ww], j);
-      const SoftPairRec r = pb.rec[ri];
+      const SoftPairRec r = rec[i];
       T v[6];
       load_corners(fs, (int64_t)r.row, v);
       int px, py;
@@ -536,23 +499,21 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       int et = 0;
       T prob = (T)0;
       soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
-      pb.sprob[ri] = prob;
-      pb.stype[ri] = (uint8_t)et;
+      sp[i] = prob;
+      pb.rec[base + i].type = (uint8_t)et;
       // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
     }
     __syncthreads();  // the workgroup's probabilities are visible to it
     // soft = 1 - prod(1 - p) in slot order (dibr_soft_mask_cuda.cu:174-181, double-promoted)
     if (unc && my_kid > 0) {
-      constexpr int U = 8;
+      constexpr int U8 = 8;
       T prod = (T)1.0;
-      for (int s0 = 0; s0 < my_kid; s0 += U) {
-        T pv[U];
+      for (int s0 = 0; s0 < my_kid; s0 += U8) {
+        T pv[U8];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-          pv[u] = s0 + u < my_kid ? pb.sprob[pool_index(pb, S.blk[w], S.ridx[s0 + u][tid])]
-                                  : (T)0;
+        for (int u = 0; u < U8; ++u) pv[u] = s0 + u < my_kid ? sp[S.ridx[s0 + u][tid]] : (T)0;
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U8; ++u)
           if (s0 + u < my_kid) prod = (T)((double)prod * (1.0 - (double)pv[u]));
       }
       a.soft[p] = (T)(1.0 - (double)prod);
@@ -613,8 +574,8 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
 // the split pipeline: pair math and product as their own launches
 // ------------------------------------------------------------------------------------------
 // soft = 1 - prod(1 - p) over the close faces of the 256 pixels of one tile, in slot order
-// (dibr_soft_mask_cuda.cu:174-181, double-promoted product).  The tile's records are found
-// through its waves' block lists; kReduceSlots slots at a time are placed into an LDS table by
+// (dibr_soft_mask_cuda.cu:174-181, double-promoted product).  kReduceSlots slots at a time of
+// the tile's records are placed into an LDS table by
 // (slot, pixel) and each pixel lane multiplies its slots in order.  Pixels without close faces
 // (and the tiles that streamed) were written by kd_soft_pairs.
 constexpr int kReduceSlots = 32;
@@ -625,9 +586,8 @@ __device__ __forceinline__ void soft_reduce_tile(const SoftArgs<T> &a, const Sof
   const int K = a.K, H = a.fs.H, W = a.fs.W;
   const int tid = threadIdx.x;
   const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-  const int32_t *wn = pb.twn + tile * 4;
-  const int32_t *blk = pb.tblk + tile * 4 * kMaxWaveBlocks;
-  const int n0 = wn[0], n01 = n0 + wn[1], n012 = n01 + wn[2], n = n012 + wn[3];
+  const int n = pb.ntile[tile];
+  const int64_t base = pb.tbase[tile];
   int px, py;
   tile_pixel(tl % pb.ntx, tl / pb.ntx, tid, px, py);
   const bool in = px < W && py < H;
@@ -637,10 +597,8 @@ __device__ __forceinline__ void soft_reduce_tile(const SoftArgs<T> &a, const Sof
   for (int s0 = 0; s0 < K; s0 += kReduceSlots) {
     __syncthreads();  // the previous pass is done with s_p
     for (int i = tid; i < n; i += kBlock) {
-      const int ww = (i >= n0) + (i >= n01) + (i >= n012);
-      const int j = i - (ww == 0 ? 0 : ww == 1 ? n0 : ww == 2 ? n01 : n012);
-      const int64_t ri = pool_index(pb, blk + ww * kMaxWaveBlocks, j);
-      const uint32_t sq = ((const uint32_t *)(pb.rec + ri))[2];  // slot | q << 16
+      const int64_t ri = base + i;
+      const uint32_t sq = ((const uint32_t *)(pb.rec + ri))[1];  // slot | q << 16
       const int s = (int)(sq & 0xffffu) - s0;
       if (s >= 0 && s < kReduceSlots) s_p[s][(sq >> 16) & 0xffu] = pb.sprob[ri];
     }
@@ -663,25 +621,26 @@ __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPair
     else
       a.zero1[i - a.nzero0] = (T)0;
   }
-  const int ntl = pb.counters[2];
+  const int ntl = pb.counters[1];
   for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) soft_reduce_tile<T>(a, pb, pb.tiles[ti], s_p);
 }
 
-// Flat over the pool: each record's distance type and probability (bit-identical to the
-// reference) and optionally the close lists.
+// Flat over the (tile, 256-record) items: each record's distance type and probability
+// (bit-identical to the reference) and optionally the close lists.
 template <typename T, bool LISTS>
 __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftPairBuf<T> pb) {
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
-  const int64_t nrec = pool_used_records(pb.counters, pb.bs_shift);
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nrec;
-       i += (int64_t)gridDim.x * kBlock) {
+  const int nitems = pb.counters[0];
+  for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+    const PairItem item = pb.items[it];
+    if ((int)threadIdx.x >= item.n) continue;
+    const int64_t i = item.start + threadIdx.x;
     const SoftPairRec r = pb.rec[i];
-    if (r.row < 0) continue;
     T v[6];
     load_corners(fs, (int64_t)r.row, v);
-    const int64_t tile = r.tile;
+    const int64_t tile = item.tile;
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
     int px, py;
     tile_pixel(tl % pb.ntx, tl / pb.ntx, r.q, px, py);
@@ -690,7 +649,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
     T prob = (T)0;
     soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
     pb.sprob[i] = prob;
-    pb.stype[i] = (uint8_t)et;
+    pb.rec[i].type = (uint8_t)et;
     if (LISTS || a.last) {
       const int64_t gp = ((int64_t)b * H + py) * W + px;
       int64_t lo, hi;
@@ -765,7 +724,7 @@ __device__ __forceinline__ void seg_scan_shfl(int seg, int lane, T g[6]) {
   }
 }
 
-// Flat over the pool's 256-record items, one record per thread: the coefficients are computed
+// Flat over the (tile, 256-record) items, one record per thread: the coefficients are computed
 // from the record's face corners, distance type and forward probability (soft_pair_coef: the
 // forward's critical path skips them; this kernel, bound by its load chains and atomics, absorbs
 // the arithmetic), s_p * h_j is expanded to the face's 6 corner coordinates, summed over the
@@ -778,30 +737,27 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const int lane = threadIdx.x & (kWave - 1);
-  const int64_t nrec = pool_used_records(pb.counters, pb.bs_shift);
-  const int64_t nitems = (nrec + kBlock - 1) / kBlock;
-  // R items per workgroup pass; their load chains (record -> the pixel's gradient and soft
-  // value, the face's corners) are issued together
-  for (int64_t it0 = (int64_t)blk * R; it0 < nitems; it0 += (int64_t)nblk * R) {
+  const int nitems = pb.counters[0];
+  // R items per workgroup pass; their load chains (item -> record -> the pixel's gradient and
+  // soft value, the face's corners) are issued together
+  for (int it0 = blk * R; it0 < nitems; it0 += nblk * R) {
     bool ok[R];
     SoftPairRec r[R];
     SoftCoef<T> c[R];
     T gs[R], so[R];
     int et[R];
+    PairItem item[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      const int64_t ri = (it0 + u) * kBlock + threadIdx.x;
-      ok[u] = ri < nrec;
-      if (ok[u]) {
-        r[u] = pb.rec[ri];
-        ok[u] = r[u].row >= 0;
-      }
+      item[u] = it0 + u < nitems ? pb.items[it0 + u] : PairItem{0, 0, 0};
+      ok[u] = (int)threadIdx.x < item[u].n;
+      if (ok[u]) r[u] = pb.rec[item[u].start + threadIdx.x];
     }
 #pragma unroll
     for (int u = 0; u < R; ++u)
       if (ok[u]) {
-        const int64_t ri = (it0 + u) * kBlock + threadIdx.x;
-        const int64_t tile = r[u].tile;
+        const int64_t ri = item[u].start + threadIdx.x;
+        const int64_t tile = item[u].tile;
         const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
         int px, py;
         tile_pixel(tl % pb.ntx, tl / pb.ntx, r[u].q, px, py);
@@ -811,7 +767,7 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
         T v[6];
         load_corners(fs, (int64_t)r[u].row, v);
         const float M = fs.M;
-        et[u] = pb.stype[ri];
+        et[u] = r[u].type;
         soft_pair_coef<T>((T)px_cx(M, W, px), (T)px_cy(M, H, py), v, et[u], pb.sprob[ri], M,
                           c[u].h);
       }
@@ -861,7 +817,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_bwd(SoftArgs<T> a, SoftPai
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
-  const int novf = pb.counters[1];
+  const int novf = pb.counters[2];
   for (int i = blk; i < novf; i += nblk) {
     const int64_t tile = pb.ovf[i];
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
@@ -925,6 +881,11 @@ __global__ __launch_bounds__(kBlock) void kd_dibr_bwd(SoftArgs<T> a, SoftPairBuf
 // ------------------------------------------------------------------------------------------
 constexpr unsigned kOvfBlocks = 256;  // grid of the overflow kernels (exit at once when unused)
 
+// Whether a tile can find the pool exhausted: never with knum <= 32 (the pool holds 32 records
+// per pixel) unless a test limits the pool; the overflow kernels are launched only then.  The
+// limits must stay the same from a forward to its backward.
+static bool pool_may_overflow(int K) { return K > kPoolPairsPerPixel || pool_limit_pairs() < 1.f; }
+
 template <typename T, bool FUSED>
 static void ovf_fwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipStream_t stream) {
   ProfScope prof(K_SOFT_OVF_FWD, stream);
@@ -952,7 +913,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
     // 6 workgroups per CU (the 16 KB record-index table); 4 and 8 measured no faster
     hipLaunchKernelGGL((kd_soft_pairs<T, true, 6>), dim3((unsigned)pb.ntiles, fs.B),
                        dim3(kBlock), 0, stream, a, pb);
-    ovf_fwd_launch<T, true>(a, pb, stream);
+    if (pool_may_overflow(a.K)) ovf_fwd_launch<T, true>(a, pb, stream);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
     return KD_OK;
@@ -962,7 +923,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
     hipLaunchKernelGGL((kd_soft_pairs<T, false>), dim3((unsigned)pb.ntiles, fs.B), dim3(kBlock),
                        0, stream, a, pb);
   }
-  ovf_fwd_launch<T, false>(a, pb, stream);
+  if (pool_may_overflow(a.K)) ovf_fwd_launch<T, false>(a, pb, stream);
   {
     ProfScope prof(K_SOFT_MATH, stream);
     const dim3 grid(kMathBlocks);
@@ -996,7 +957,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
                        dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
                        stream, ra, a, pb);
   }
-  ovf_fwd_launch<float, true>(a, pb, stream);
+  if (pool_may_overflow(a.K)) ovf_fwd_launch<float, true>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr fwd: %s", hipGetErrorString(e));
   return KD_OK;
@@ -1015,7 +976,7 @@ int soft_pairs_forward(SoftArgs<T> &a, void *ws, size_t ws_bytes, bool grad, boo
   a.bb.cull = nullptr;
   SoftPairBuf<T> pb = soft_pair_carve<T>(ws, off, fs.B, fs.H, fs.W, a.K);
   a.bb.clear = pb.counters;
-  a.bb.n_clear = 3;
+  a.bb.n_clear = kPairClear;
   hipError_t e = bin_faces<T>(fs, a.bb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   return soft_pairs_launch<T>(a, pb, grad, reduce, stream);
@@ -1030,7 +991,7 @@ int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t s
     hipLaunchKernelGGL((kd_soft_bwd_items<T, 1>), dim3(kMathBlocks), dim3(kBlock), 0, stream, a,
                        pb);
   }
-  ovf_bwd_launch<T>(a, pb, stream);
+  if (pool_may_overflow(a.K)) ovf_bwd_launch<T>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
   return KD_OK;
@@ -1051,7 +1012,7 @@ int dibr_backward_merged_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, const Raster
     hipLaunchKernelGGL((kd_dibr_bwd<T>), dim3((unsigned)(nr + ns)), dim3(kBlock), 0, stream, a,
                        pb, ra, nr, ns, ntl);
   }
-  ovf_bwd_launch<T>(a, pb, stream);
+  if (pool_may_overflow(a.K)) ovf_bwd_launch<T>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr bwd: %s", hipGetErrorString(e));
   return KD_OK;
