@@ -76,18 +76,20 @@ def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4, f
         return F * (9 + 6) * e + V * 3 * e
     if pairs is None:
         return None
-    if kernel == 'kd_soft_pairs' and fused:  # whole soft mask: face_idx + corners in; records,
-        # probabilities, types, counts, soft out
-        return P * (8 + 4 + e) + F * 6 * e + pairs * (12 + e + 1)
-    if kernel == 'kd_soft_pairs':      # face_idx in; records, counts, soft out
-        return P * (8 + 4 + e) + pairs * 12
+    # soft-mask records (kd_soft.hpp SoftPairRec): 8 B {row, slot, pixel, type} + the
+    # probability; work items 16 B per 256 records
+    if kernel == 'kd_soft_pairs' and fused:  # whole soft mask: face_idx + corners in; records
+        # (with their type), probabilities, soft out
+        return P * (8 + e) + F * 6 * e + pairs * (8 + e)
+    if kernel == 'kd_soft_pairs':      # face_idx in; records, per-pixel counts, soft out
+        return P * (8 + 4 + e) + pairs * 8
     if kernel == 'kd_soft_pair_math':  # records in; probabilities, types out
-        return pairs * (12 + e + 1)
+        return pairs * (8 + e + 1)
     if kernel == 'kd_soft_reduce':     # probabilities in, soft out
         return pairs * e
     if kernel == 'kd_soft_bwd_pairs':  # records + probabilities, grad/soft, corners in; face
         # grads added
-        return pairs * (12 + e) + P * 2 * e + F * 6 * e * 3
+        return pairs * (8 + e) + P * 2 * e + F * 6 * e * 3
     if kernel == 'kd_dibr_fwd':        # raster forward + whole soft mask in one launch
         return (algorithmic_bytes('kd_raster_fwd', P, F, Fv, D, K, lists, pairs, V, e) +
                 algorithmic_bytes('kd_soft_pairs', P, F, Fv, D, K, lists, pairs, V, e))

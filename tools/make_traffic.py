@@ -24,6 +24,8 @@ SLOT = {
     'kd::kd_zero2<float>': 'kd_zero',
     'kd::kd_raster_bwd_tile<float, 4>': 'kd_raster_bwd_tile',
     'kd::kd_bin_count<float>': 'kd_bin_count', 'kd::kd_bin_scan': 'kd_bin_scan',
+    'kd::kd_bin_scan<float>': 'kd_bin_scan',
+    'kd::kd_soft_ovf_fwd<float, true>': 'kd_soft_ovf_fwd', 'kd::kd_soft_ovf_bwd<float>': 'kd_soft_ovf_bwd',
     'kd::kd_bin_scatter<float>': 'kd_bin_scatter',
     'kd::kd_dibr_bwd<float>': 'kd_dibr_bwd',
     'kd::kd_dibr_fwd_tiles': 'kd_dibr_fwd',
