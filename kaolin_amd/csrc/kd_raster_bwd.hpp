@@ -94,10 +94,13 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
   T *grad_fvi = ra.grad_fvi;
   T *grad_feat = ra.grad_feat;
   constexpr int SMAX = 6 + 3 * DMAX;
+  // odd row stride (in 4-byte words): a pixel's row write (lanes on different rows, one term)
+  // and a slot's column sums (lanes on one row, consecutive terms) are both bank-conflict free
+  constexpr int SROW = (SMAX * (int)sizeof(T) / 4) % 2 ? SMAX : SMAX + 1;
   constexpr int HT = kBlock;  // slots >= distinct faces of a tile
   __shared__ int s_key[HT];
   __shared__ int s_n[HT];  // pixels per slot (their ranks come from the counter)
-  __shared__ T s_con[kBlock][SMAX + 1];
+  __shared__ T s_con[kBlock][SROW];
   __shared__ short s_off[HT];
   __shared__ int s_list[HT];
   __shared__ int s_cnt[4];
