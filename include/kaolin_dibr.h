@@ -267,6 +267,30 @@ int kd_dibr_rasterization_backward_f64(int batch, int height, int width, int64_t
                                        int knum, double *grad_fvi, double *grad_feat,
                                        int grads_zeroed, void *workspace, size_t workspace_bytes,
                                        void *stream);
+/* The same backward with the face -> vertex step of prepare_vertices fused in (SURVEY.md §8 f1;
+ * reference: the gather backward of kaolin/ops/mesh/mesh.py:24-45 with the projection and camera
+ * transform of kaolin/render/mesh/utils.py:164-167 and render/camera/legacy.py:120-139): the raster
+ * and soft-mask corner gradients go straight to grad_vertices (vertex_batch, num_vertices, 3) --
+ * summed over the views when vertex_batch == 1 -- with no (B, F, 3, 2) gradient in between.
+ * fvi / fvc are prepare_vertices' outputs for faces (F, 3) int64, camera_proj (3),
+ * camera_transform (B, 4, 3); feat_dim <= 3.  grad_vertices is zeroed here; grad_feat (nullable)
+ * is zeroed here unless feat_zeroed (the forward's grad_feat_zero). */
+int kd_dibr_rasterization_backward_vertices_f32(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const float *grad_interp,
+    const float *grad_soft, const int64_t *face_idx, const float *weights, const float *soft,
+    const float *fvi, const float *feat, float eps, double multiplier, double boxlen,
+    float sigmainv, int knum, int vertex_batch, int64_t num_vertices, const int64_t *faces,
+    const float *fvc, const float *camera_proj, const float *camera_transform,
+    float *grad_vertices, float *grad_feat, int feat_zeroed, void *workspace,
+    size_t workspace_bytes, void *stream);
+int kd_dibr_rasterization_backward_vertices_f64(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const double *grad_interp,
+    const double *grad_soft, const int64_t *face_idx, const double *weights, const double *soft,
+    const double *fvi, const double *feat, float eps, double multiplier, double boxlen,
+    float sigmainv, int knum, int vertex_batch, int64_t num_vertices, const int64_t *faces,
+    const double *fvc, const double *camera_proj, const double *camera_transform,
+    double *grad_vertices, double *grad_feat, int feat_zeroed, void *workspace,
+    size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * prepare_vertices (kaolin/render/mesh/utils.py:128-175 with camera_transform): camera

@@ -477,6 +477,36 @@ def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights,
     return gfvi, gfeat
 
 
+def dibr_rasterization_backward_vertices(grad_interp, grad_soft, face_idx, weights, soft,
+                                         face_vertices_image, face_features, eps, multiplier,
+                                         boxlen, sigmainv, knum, workspace, faces, fvc,
+                                         camera_proj, camera_transform, vertex_batch,
+                                         num_vertices, need_feat=True, grad_feat_buffer=None):
+    """Gradients (grad_vertices (vertex_batch, V, 3), grad_feat or None) of prepare_vertices +
+    the fused DIB-R forward, with the face -> vertex step inside the backward kernel
+    (kd_dibr_rasterization_backward_vertices).  grad_feat_buffer: the grad_feat the forward
+    zeroed (filled in place)."""
+    dev = face_idx.device
+    B, F = face_vertices_image.shape[:2]
+    H, W = face_idx.shape[1:3]
+    D = face_features.shape[-1]
+    sfx = _sfx(face_vertices_image, 'dibr_rasterization_backward')
+    gvert = torch.empty((vertex_batch, num_vertices, 3), device=dev,
+                        dtype=face_vertices_image.dtype)
+    zeroed = need_feat and grad_feat_buffer is not None
+    gfeat = (grad_feat_buffer if zeroed else torch.empty_like(face_features)) if need_feat \
+        else None
+    c = (lambda t: None if t is None else t.contiguous())  # noqa: E731
+    _lib.call(f'kd_dibr_rasterization_backward_vertices_{sfx}', B, H, W, F, D,
+              _ptr(c(grad_interp)), _ptr(c(grad_soft)), _ptr(face_idx), _ptr(weights),
+              _ptr(soft), _ptr(face_vertices_image), _ptr(face_features), float(eps),
+              float(multiplier), float(boxlen), float(sigmainv), int(knum), int(vertex_batch),
+              int(num_vertices), _ptr(faces), _ptr(fvc), _ptr(camera_proj),
+              _ptr(camera_transform), _ptr(gvert), _ptr(gfeat), 1 if zeroed else 0,
+              _ptr(workspace), workspace.numel(), _stream(dev))
+    return gvert, gfeat
+
+
 # -------------------------------------------------------------------------------------------
 # mask_iou (kaolin/metrics/render.py:18-40) and texture_mapping (render/mesh/utils.py:23-76),
 # SURVEY §8 f2
@@ -729,6 +759,7 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     dibr_soft_mask_backward_binned=dibr_soft_mask_backward_binned,
     dibr_rasterization_forward_fused=dibr_rasterization_forward_fused,
     dibr_rasterization_backward_fused=dibr_rasterization_backward_fused,
+    dibr_rasterization_backward_vertices=dibr_rasterization_backward_vertices,
     prepare_vertices_forward=prepare_vertices_forward,
     prepare_vertices_backward=prepare_vertices_backward,
     texture_mapping_forward=texture_mapping_forward,

@@ -45,6 +45,11 @@ _SIGS = {
     'kd_dibr_rasterization_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_float, c_double, c_double, c_float,
                                        c_int, c_p, c_p, c_int, c_p, c_size, c_p],
+    'kd_dibr_rasterization_backward_vertices': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p,
+                                                c_p, c_p, c_p, c_p, c_p, c_float, c_double,
+                                                c_double, c_float, c_int, c_int, c_i64, c_p,
+                                                c_p, c_p, c_p, c_p, c_p, c_int, c_p, c_size,
+                                                c_p],
     'kd_prepare_vertices_forward': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p,
                                     c_p, c_p],
     'kd_prepare_vertices_backward': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p,

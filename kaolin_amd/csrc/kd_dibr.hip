@@ -158,6 +158,51 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
   return rc;
 }
 
+// The backward with the face -> vertex step fused (VertexOut): the raster and
+// soft-mask corner gradients go straight to the vertex gradient (Bv, V, 3); no grad_fvi.
+template <typename T>
+static int dibr_bwd_vtx(int B, int H, int W, int64_t F, int D, const T *grad_interp,
+                        const T *grad_soft, const int64_t *face_idx, const T *weights,
+                        const T *soft, const T *fvi, const T *feat, float eps, double M,
+                        double boxlen, float sigmainv, int K, int Bv, int64_t V,
+                        const int64_t *faces, const T *fvc, const T *proj, const T *tf,
+                        T *gvert, T *gfeat, int feat_zeroed, void *ws, size_t wsb,
+                        void *stream_) {
+  hipStream_t stream = (hipStream_t)stream_;
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0 && V >= 0, "negative size");
+  KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
+  KD_CHECK_ARG(D <= 3, "vertex backward: feature dim > 3 (use the grad_fvi backward)");
+  KD_CHECK_ARG(Bv == 1 || Bv == B, "vertex batch must be 1 or the view count");
+  KD_CHECK_ARG(gvert && (F == 0 || (faces && fvc && proj && tf)), "vertex backward: NULL input");
+  const size_t need = dibr_workspace_bytes(B, H, W, F, K, sizeof(T));
+  if (wsb < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
+  if ((int64_t)Bv * V > 0) {
+    const hipError_t e = hipMemsetAsync(gvert, 0, sizeof(T) * 3 * (size_t)Bv * (size_t)V, stream);
+    if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
+  }
+  const int64_t nf = (int64_t)B * F;
+  int rc = feat_zeroed || !gfeat ? KD_OK
+                                 : zero_buffers<T>(gfeat, nf * 3 * D, (T *)nullptr, 0, stream);
+  if (rc != KD_OK || B == 0 || H == 0 || W == 0 || F == 0) return rc;
+  DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
+  const VertexOut<T> vo{gvert, faces, fvc, proj, tf, F, V, Bv};
+  SoftArgs<T> sa{};
+  sa.fs = dibr_faceset<T>(B, H, W, F, fvi, M);
+  sa.fs.margin = (T)(boxlen * M);
+  sa.fs.has_margin = 1;
+  sa.bb = d.sbb;
+  sa.face_idx = face_idx;
+  sa.K = K;
+  sa.sigmainv = sigmainv;
+  sa.grad_soft = grad_soft;
+  sa.soft_in = soft;
+  sa.vo = vo;
+  const RasterBwdArgs<T> ra{B,   H,    W,   F,     D,     grad_interp,   face_idx, weights,
+                            fvi, feat, eps, nullptr, gfeat, debug_flags(), vo};
+  return dibr_backward_merged_launch<T>(sa, d.pb, ra, stream);
+}
+
 }  // namespace kd
 
 using namespace kd;
@@ -236,6 +281,31 @@ int kd_dibr_rasterization_backward_f64(int B, int H, int W, int64_t F, int D,
   return dibr_bwd<double>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
                           feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat,
                           grads_zeroed, ws, wsb, stream);
+}
+
+int kd_dibr_rasterization_backward_vertices_f32(
+    int B, int H, int W, int64_t F, int D, const float *grad_interp, const float *grad_soft,
+    const int64_t *face_idx, const float *weights, const float *soft, const float *fvi,
+    const float *feat, float eps, double M, double boxlen, float sigmainv, int knum,
+    int vertex_batch, int64_t num_vertices, const int64_t *faces, const float *fvc,
+    const float *camera_proj, const float *camera_transform, float *grad_vertices,
+    float *grad_feat, int feat_zeroed, void *ws, size_t wsb, void *stream) {
+  return dibr_bwd_vtx<float>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
+                             feat, eps, M, boxlen, sigmainv, knum, vertex_batch, num_vertices,
+                             faces, fvc, camera_proj, camera_transform, grad_vertices, grad_feat,
+                             feat_zeroed, ws, wsb, stream);
+}
+int kd_dibr_rasterization_backward_vertices_f64(
+    int B, int H, int W, int64_t F, int D, const double *grad_interp, const double *grad_soft,
+    const int64_t *face_idx, const double *weights, const double *soft, const double *fvi,
+    const double *feat, float eps, double M, double boxlen, float sigmainv, int knum,
+    int vertex_batch, int64_t num_vertices, const int64_t *faces, const double *fvc,
+    const double *camera_proj, const double *camera_transform, double *grad_vertices,
+    double *grad_feat, int feat_zeroed, void *ws, size_t wsb, void *stream) {
+  return dibr_bwd_vtx<double>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft,
+                              fvi, feat, eps, M, boxlen, sigmainv, knum, vertex_batch,
+                              num_vertices, faces, fvc, camera_proj, camera_transform,
+                              grad_vertices, grad_feat, feat_zeroed, ws, wsb, stream);
 }
 
 }  // extern "C"

@@ -18,6 +18,7 @@ struct RasterBwdArgs {
   float eps;
   T *grad_fvi, *grad_feat;
   int dbg;
+  VertexOut<T> vo;  // vo.grad set: the corner gradients go to the vertices (VTX bodies)
 };
 
 // ------------------------------------------------------------------------------------------
@@ -80,7 +81,7 @@ __device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], con
 // per (tile, face, term), a face's terms on adjacent lanes (its 6 corner terms and its 3*D
 // feature terms are contiguous in memory).  (Summation order varies with the LDS counters, as it
 // does across tiles with the float atomics.)
-template <typename T, int DMAX>
+template <typename T, int DMAX, bool VTX = false>
 __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra, int d, int n,
                                                      int ntl) {
   const int H = ra.H, W = ra.W, D = ra.D, dbg = ra.dbg;
@@ -163,19 +164,31 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
         if (d < D) s_con[ps][6 + ii * D + d] = c[6 + ii * DMAX + d];
   }
   __syncthreads();
-  for (int idx = tid; idx < nocc * S; idx += kBlock) {
-    const int i = idx / S, j = idx - i * S;
+  // VTX: items 0..2 of a face are its corners (terms 2k, 2k+1 -> the corner's vertex)
+  const int SI = VTX ? S - 3 : S;
+  for (int idx = tid; idx < nocc * SI; idx += kBlock) {
+    const int i = idx / SI, j = idx - i * SI;
     const int slot = s_list[i];
     const int ns = s_n[slot];
     const int o = s_off[slot];
-    T v = (T)0;
-    for (int r = 0; r < ns; ++r) v += s_con[o + r][j];  // independent reads: pipelined
-    if (v == (T)0 || (dbg & 128)) continue;
     const int64_t row = (int64_t)b * F + s_key[slot];
-    if (j < 6)
-      atomicAdd(grad_fvi + row * 6 + j, v);
+    if (VTX && j < 3) {
+      T vx = (T)0, vy = (T)0;
+      for (int r = 0; r < ns; ++r) {  // independent reads: pipelined
+        vx += s_con[o + r][2 * j];
+        vy += s_con[o + r][2 * j + 1];
+      }
+      vertex_add(ra.vo, row, j, vx, vy);
+      continue;
+    }
+    const int jj = VTX ? j + 3 : j;
+    T v = (T)0;
+    for (int r = 0; r < ns; ++r) v += s_con[o + r][jj];  // independent reads: pipelined
+    if (v == (T)0 || (dbg & 128)) continue;
+    if (jj < 6)
+      atomicAdd(grad_fvi + row * 6 + jj, v);
     else if (grad_feat)
-      atomicAdd(grad_feat + row * 3 * D + (j - 6), v);
+      atomicAdd(grad_feat + row * 3 * D + (jj - 6), v);
   }
 }
 

@@ -5,6 +5,7 @@
 
 #include "kd_binning.hpp"
 #include "kd_capi.hpp"
+#include "kd_raster.hpp"
 #include "kd_softdist.hpp"
 #include "kd_tile.hpp"
 
@@ -78,6 +79,7 @@ struct SoftArgs {
   // buffers the soft reduction zeroes on the side (the fused backward's gradients), nullable
   T *zero0, *zero1;
   int64_t nzero0, nzero1;
+  VertexOut<T> vo;  // backward: vo.grad set -> vertex gradients instead of grad_fvi (VTX bodies)
 };
 
 // Per-wave pair list of the current batch and its per-pixel bookkeeping.

@@ -731,7 +731,7 @@ __device__ __forceinline__ void seg_scan_shfl(int seg, int lane, T g[6]) {
 // record's run of equal faces inside its wave by a segmented inclusive scan (records are
 // face-major runs; no LDS), and the run's last lane adds the nonzero sums with float atomics.
 // Every record costs the same, so the grid is balanced however the records fall on the tiles.
-template <typename T, int R>
+template <typename T, int R, bool VTX = false>
 __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                     int blk, int nblk) {
   const FaceSet<T> &fs = a.fs;
@@ -799,9 +799,14 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
       const int next_key = __shfl_down(key, 1);
       const bool tail = key >= 0 && (lane == kWave - 1 || next_key != key);
       if (tail) {
+        if constexpr (VTX) {
 #pragma unroll
-        for (int q = 0; q < 6; ++q)
-          if (g[q] != (T)0) atomicAdd(a.grad_fvi + (int64_t)key * 6 + q, g[q]);
+          for (int k = 0; k < 3; ++k) vertex_add(a.vo, (int64_t)key, k, g[2 * k], g[2 * k + 1]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < 6; ++q)
+            if (g[q] != (T)0) atomicAdd(a.grad_fvi + (int64_t)key * 6 + q, g[q]);
+        }
       }
     }
   }
@@ -810,7 +815,7 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
 // The backward of the tiles that streamed their soft mask (pool exhausted): the same walk again,
 // each pixel lane recomputing its pairs (bit-identical probabilities and types) and adding their
 // terms with float atomics.  One workgroup per such tile; a grid that finds none exits at once.
-template <typename T>
+template <typename T, bool VTX>
 __global__ __launch_bounds__(kBlock) void kd_soft_ovf_bwd(SoftArgs<T> a, SoftPairBuf<T> pb) {
   __shared__ TileLists L;
   const int blk = blockIdx.x, nblk = gridDim.x;
@@ -845,9 +850,14 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_bwd(SoftArgs<T> a, SoftPai
             soft_pair_coef<T>(x0, y0, v, et, prob, M, cf.h);
             T g[6] = {0, 0, 0, 0, 0, 0};
             soft_add_pair<T>(g, et, sp, cf);
+            if constexpr (VTX) {
 #pragma unroll
-            for (int q = 0; q < 6; ++q)
-              if (g[q] != (T)0) atomicAdd(a.grad_fvi + row * 6 + q, g[q]);
+              for (int k = 0; k < 3; ++k) vertex_add(a.vo, row, k, g[2 * k], g[2 * k + 1]);
+            } else {
+#pragma unroll
+              for (int q = 0; q < 6; ++q)
+                if (g[q] != (T)0) atomicAdd(a.grad_fvi + row * 6 + q, g[q]);
+            }
           });
     };
     auto done = [&]() { return __syncthreads_and(!unc || my_kid >= K) != 0; };
@@ -865,15 +875,15 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_items(SoftArgs<T> a, SoftP
 // independent (both only add into grad_fvi), so one grid holds both, the raster tiles first
 // (their XCD band mapping keeps its block ids), and the soft items fill the raster's tail:
 // 72 us against 38 + 41 for the two launches at C3 (alternating runs of 8: 74 us).
-template <typename T>
+template <typename T, bool VTX>
 __global__ __launch_bounds__(kBlock) void kd_dibr_bwd(SoftArgs<T> a, SoftPairBuf<T> pb,
                                                       RasterBwdArgs<T> ra, int nr, int ns,
                                                       int ntl) {
   const int blk = blockIdx.x;
   if (blk < nr)
-    raster_bwd_tile_body<T, 3>(ra, blk, nr, ntl);
+    raster_bwd_tile_body<T, 3, VTX>(ra, blk, nr, ntl);
   else
-    soft_bwd_items_body<T, 1>(a, pb, blk - nr, ns);
+    soft_bwd_items_body<T, 1, VTX>(a, pb, blk - nr, ns);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -896,7 +906,12 @@ static void ovf_fwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipSt
 template <typename T>
 static void ovf_bwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipStream_t stream) {
   ProfScope prof(K_SOFT_OVF_BWD, stream);
-  hipLaunchKernelGGL((kd_soft_ovf_bwd<T>), dim3(kOvfBlocks), dim3(kBlock), 0, stream, a, pb);
+  if (a.vo.grad)
+    hipLaunchKernelGGL((kd_soft_ovf_bwd<T, true>), dim3(kOvfBlocks), dim3(kBlock), 0, stream, a,
+                       pb);
+  else
+    hipLaunchKernelGGL((kd_soft_ovf_bwd<T, false>), dim3(kOvfBlocks), dim3(kBlock), 0, stream, a,
+                       pb);
 }
 
 template <typename T>
@@ -1002,17 +1017,21 @@ int dibr_backward_merged_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, const Raster
                                 hipStream_t stream) {
   KD_CHECK_ARG(ra.D <= 3, "merged backward: D > 3");
   const int ntl = (int)pb.ntiles;
-  const int64_t nr64 = (int64_t)ra.B * ntl;
+  const int64_t nr64 = ra.grad ? (int64_t)ra.B * ntl : 0;  // raster tiles (grad_interp given)
   KD_CHECK_ARG(nr64 + kMathBlocks < (1ll << 31), "merged backward: too many tiles");
-  const int nr = (int)nr64, ns = (int)kMathBlocks;
+  const int nr = (int)nr64, ns = a.grad_soft ? (int)kMathBlocks : 0;
   a.fs.dbg = debug_flags();
   a.fs.tbuf = debug_tile_buffer();
-  {
+  if (nr + ns > 0) {
     ProfScope prof(K_DIBR_BWD, stream);
-    hipLaunchKernelGGL((kd_dibr_bwd<T>), dim3((unsigned)(nr + ns)), dim3(kBlock), 0, stream, a,
-                       pb, ra, nr, ns, ntl);
+    if (a.vo.grad)  // the face -> vertex step fused (VertexOut)
+      hipLaunchKernelGGL((kd_dibr_bwd<T, true>), dim3((unsigned)(nr + ns)), dim3(kBlock), 0,
+                         stream, a, pb, ra, nr, ns, ntl);
+    else
+      hipLaunchKernelGGL((kd_dibr_bwd<T, false>), dim3((unsigned)(nr + ns)), dim3(kBlock), 0,
+                         stream, a, pb, ra, nr, ns, ntl);
   }
-  if (pool_may_overflow(a.K)) ovf_bwd_launch<T>(a, pb, stream);
+  if (a.grad_soft && pool_may_overflow(a.K)) ovf_bwd_launch<T>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr bwd: %s", hipGetErrorString(e));
   return KD_OK;

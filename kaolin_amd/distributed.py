@@ -105,17 +105,18 @@ def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_f
     shared mesh to the rank's cameras (``prepare_vertices``, utils.py:128-175), render
     (``dibr_rasterization``, dibr.py:119-209, valid faces = normals z >= 0) and back-propagate
     the fixed upstream gradients ``[grad_interp, grad_soft]`` into ``vertices.grad`` (summed over
-    the rank's views) and the features' gradient.
+    the rank's views) and the features' gradient.  (The fused alternative,
+    ``dibr_rasterization_from_vertices``, measured slower: see its docstring.)
 
     vertices (V, 3) leaf, faces (F, 3) int64, camera_transform (B_rank, 4, 3), face_features
     (B_rank, F, 3, D) or (1, F, 3, D) shared.  `prepare` / `render` default to the HIP kernels
     (kaolin_amd.render.mesh); the CPU tests pass oracle-backed ones with the same signatures.
     Returns face_idx (B_rank, H, W)."""
+    B = camera_transform.shape[0]
     if prepare is None or render is None:
         from .render.mesh import dibr_rasterization, prepare_vertices
         prepare = prepare or prepare_vertices
         render = render or dibr_rasterization
-    B = camera_transform.shape[0]
     fvc, fvi, nrm = prepare(vertices.unsqueeze(0), faces, camera_proj,
                             camera_transform=camera_transform)
     feats = face_features if face_features.shape[0] == B else \

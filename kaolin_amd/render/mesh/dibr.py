@@ -19,7 +19,8 @@ from torch.autograd import Function
 from ... import _C
 from .rasterization import rasterize
 
-__all__ = ['dibr_soft_mask', 'dibr_rasterization', 'close_lists']
+__all__ = ['dibr_soft_mask', 'dibr_rasterization', 'dibr_rasterization_from_vertices',
+           'close_lists']
 
 _tls = threading.local()
 
@@ -172,6 +173,98 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
     interp, soft, face_idx = DibrRasterizationHip.apply(
         height, width, face_vertices_z, face_vertices_image, feats, face_normals_z, sigmainv,
         boxlen, knum, _multiplier, _eps)
+    if isinstance(face_features, (list, tuple)):
+        out, cur = [], 0
+        for f in face_features:
+            out.append(interp[..., cur:cur + f.shape[-1]])
+            cur += f.shape[-1]
+        interp = tuple(out)
+    return interp, soft, face_idx
+
+
+class DibrRenderHip(Function):
+    """prepare_vertices + dibr_rasterization as one autograd node whose backward runs the
+    face -> vertex step inside the DIB-R backward kernel (kd_dibr_rasterization_backward_vertices,
+    SURVEY.md §8 f1): the corner gradients of the raster and the soft mask go straight to the
+    vertex gradient, with no (B, F, 3, 2) gradient and no separate scatter kernel.
+
+    Measured at C3 (same box): the fused backward takes 144-150 us against 69 + 19 us for the
+    DIB-R backward plus kd_prepare_bwd -- the vertex atomics (3 per corner, every vertex shared
+    by ~6 faces and every view) serialise where the per-face grad_fvi atomics did not.  The
+    training step (kaolin_amd.distributed) therefore keeps the two-kernel path; this node stays
+    as the f1 entry point, parity-tested (tests/test_gpu_vertices.py)."""
+
+    @staticmethod
+    def forward(ctx, vertices, faces, camera_proj, camera_transform, face_features, height,
+                width, sigmainv, boxlen, knum, multiplier, eps):
+        vertices = vertices.contiguous()
+        camera_proj = camera_proj.contiguous()
+        camera_transform = camera_transform.contiguous()
+        face_features = face_features.contiguous()
+        fvc, fvi, nrm = _C.prepare_vertices_forward(vertices, faces, camera_proj,
+                                                    camera_transform)
+        need_feat = face_features.requires_grad
+        want_grad = vertices.requires_grad or need_feat
+        gfeat_buf = torch.empty(face_features.shape, device=face_features.device,
+                                dtype=face_features.dtype) if want_grad and need_feat else None
+        interp, face_idx, weights, soft, ws = _C.render.mesh.dibr_rasterization_forward_fused(
+            height, width, fvc[..., 2], fvi, face_features, nrm[..., 2], sigmainv, boxlen, knum,
+            multiplier, eps, want_grad=want_grad,
+            grad_buffers=(None, gfeat_buf) if want_grad else None)
+        ctx.save_for_backward(face_idx, weights, soft, fvi, fvc, face_features, faces,
+                              camera_proj, camera_transform, ws if want_grad else None)
+        ctx.gfeat_buf = gfeat_buf
+        ctx.params = (eps, multiplier, boxlen, sigmainv, knum)
+        ctx.vshape = (vertices.shape[0], vertices.shape[1])
+        ctx.mark_non_differentiable(face_idx)
+        ctx.set_materialize_grads(False)
+        return interp, soft, face_idx
+
+    @staticmethod
+    def backward(ctx, grad_interp, grad_soft, grad_face_idx):
+        need_v, need_feat = ctx.needs_input_grad[0], ctx.needs_input_grad[4]
+        if not (need_v or need_feat) or (grad_interp is None and grad_soft is None):
+            return (None,) * 12
+        (face_idx, weights, soft, fvi, fvc, feat, faces, proj, tf,
+         workspace) = ctx.saved_tensors
+        eps, multiplier, boxlen, sigmainv, knum = ctx.params
+        # the forward zeroed one grad_feat buffer: the first backward fills it, a second one
+        # (retained graph) gets a fresh buffer zeroed by the backward itself
+        buf, ctx.gfeat_buf = ctx.gfeat_buf, None
+        gvert, gfeat = _C.render.mesh.dibr_rasterization_backward_vertices(
+            grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier, boxlen,
+            sigmainv, knum, workspace, faces, fvc, proj, tf, ctx.vshape[0], ctx.vshape[1],
+            need_feat=need_feat, grad_feat_buffer=buf)
+        return (gvert if need_v else None, None, None, None, gfeat, None, None, None, None,
+                None, None, None)
+
+
+def dibr_rasterization_from_vertices(height, width, vertices, faces, camera_proj,
+                                     camera_transform, face_features, sigmainv=7000,
+                                     boxlen=0.02, knum=30, multiplier=None, eps=None):
+    r"""``prepare_vertices`` (utils.py:128-175, camera_transform form) followed by
+    ``dibr_rasterization`` of its outputs (the DIB-R training step, examples/tutorial/
+    ian_dibr.py), as one autograd node with the face -> vertex step fused into the backward
+    kernel.  vertices (1 or B, V, 3), faces (F, 3) int64, camera_proj (3, 1),
+    camera_transform (B, 4, 3), face_features (B, F, 3, D) (or a list, concatenated).  Returns
+    (interpolated_features, soft_mask, face_idx), the same values as
+    ``dibr_rasterization(h, w, fvc[..., 2], fvi, face_features, normals[..., 2], ...)``; the
+    gradients flow to vertices and face_features.  Falls back to that composition when it
+    cannot fuse (feature dim > 3, camera tensors requiring grad, close_lists mode)."""
+    feats = torch.cat(face_features, dim=-1) \
+        if isinstance(face_features, (list, tuple)) else face_features
+    _multiplier = 1000. if multiplier is None else multiplier
+    _eps = 1e-8 if eps is None else eps
+    if (feats.shape[-1] > 3 or camera_proj.requires_grad or camera_transform.requires_grad
+            or _lists_enabled()):
+        from .utils import prepare_vertices
+        fvc, fvi, nrm = prepare_vertices(vertices, faces, camera_proj,
+                                         camera_transform=camera_transform)
+        return dibr_rasterization(height, width, fvc[..., 2], fvi, face_features, nrm[..., 2],
+                                  sigmainv, boxlen, knum, multiplier, eps)
+    interp, soft, face_idx = DibrRenderHip.apply(vertices, faces, camera_proj, camera_transform,
+                                                 feats, height, width, sigmainv, boxlen, knum,
+                                                 _multiplier, _eps)
     if isinstance(face_features, (list, tuple)):
         out, cur = [], 0
         for f in face_features:

@@ -1,0 +1,139 @@
+"""GPU: dibr_rasterization_from_vertices -- prepare_vertices + dibr_rasterization with the
+face -> vertex step fused into the DIB-R backward kernel (SURVEY.md §8 f1,
+kd_dibr_rasterization_backward_vertices).
+
+Its outputs must be the composition's bit for bit (the same forward kernels), and its vertex and
+feature gradients the composition's (prepare_vertices' gather-form backward over the fused
+backward's grad_fvi) up to float-atomic summation order: rtol 1e-4 in fp32, 1e-9 in fp64, with an
+absolute floor at that fraction of the gradient's largest magnitude.  The composition's vertex
+gradient is itself pinned against the reference's PyTorch composition in test_gpu_parity.py
+(test_prepare_vertices_vs_torch) and its grad_fvi against the oracle.
+"""
+import math
+
+import pytest
+import torch
+
+from helpers import TORCH_DTYPES
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _native():
+    from kaolin_amd import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+
+
+def _scene(n_lon, n_lat, B, dt, elevation=0.3, shared=True, seed=0):
+    from kaolin_amd import workloads
+    verts, faces, face_uvs = workloads.uv_sphere(n_lon, n_lat, seed=seed, dtype=dt)
+    cam = workloads.orbit_cameras(B, elevation, dtype=dt).to(DEV)
+    proj = workloads.generate_perspective_projection(math.pi / 4, dtype=dt).to(DEV)
+    v = verts.to(DEV).unsqueeze(0)
+    if not shared:
+        g = torch.Generator().manual_seed(seed + 5)
+        v = v.repeat(B, 1, 1) + 0.01 * torch.randn((B,) + tuple(v.shape[1:]), generator=g,
+                                                    dtype=dt).to(DEV)
+    uvs = face_uvs.to(DEV).unsqueeze(0).repeat(B, 1, 1, 1)
+    feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
+    return v.contiguous(), faces.to(DEV), proj, cam, feats
+
+
+def _grads(h, B, D, dt, seed=1):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.rand((B, h, h, D), generator=g, dtype=torch.float64).to(DEV, dt),
+            torch.rand((B, h, h), generator=g, dtype=torch.float64).to(DEV, dt))
+
+
+def _close(a, b, dt):
+    tol = 1e-4 if dt == torch.float32 else 1e-9
+    torch.testing.assert_close(a, b, rtol=tol, atol=tol * 0.1 * b.abs().max().item())
+
+
+def _both(h, v0, faces, proj, cam, feats0, dt, which=('interp', 'soft'), sig=7000., box=0.02):
+    from kaolin_amd.render.mesh import (dibr_rasterization, dibr_rasterization_from_vertices,
+                                        prepare_vertices)
+    B, D = cam.shape[0], feats0.shape[-1]
+    g1, g2 = _grads(h, B, D, dt)
+    res = []
+    for fused in (True, False):
+        v = v0.clone().requires_grad_(True)
+        feats = feats0.clone().requires_grad_(True)
+        if fused:
+            interp, soft, fi = dibr_rasterization_from_vertices(h, h, v, faces, proj, cam, feats,
+                                                                sig, box)
+        else:
+            fvc, fvi, nrm = prepare_vertices(v, faces, proj, camera_transform=cam)
+            interp, soft, fi = dibr_rasterization(h, h, fvc[..., 2], fvi, feats, nrm[..., 2],
+                                                  sig, box)
+        outs = [t for t, k in ((interp, 'interp'), (soft, 'soft')) if k in which]
+        grads = [g for g, k in ((g1, 'interp'), (g2, 'soft')) if k in which]
+        torch.autograd.backward(outs, grads)
+        res.append((interp.detach(), soft.detach(), fi, v.grad, feats.grad))
+    return res
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('shared', [True, False])
+def test_fused_vertex_backward_matches_composition(dname, shared):
+    dt = TORCH_DTYPES[dname]
+    h, B = 192, 3
+    v0, faces, proj, cam, feats = _scene(60, 31, B, dt, shared=shared)
+    (i1, s1, f1, gv1, gf1), (i2, s2, f2, gv2, gf2) = _both(h, v0, faces, proj, cam, feats, dt)
+    assert torch.equal(i1, i2) and torch.equal(s1, s2) and torch.equal(f1, f2)
+    assert gv1.shape == v0.shape
+    _close(gv1, gv2, dt)
+    _close(gf1, gf2, dt)
+
+
+@pytest.mark.parametrize('which', [('interp',), ('soft',)])
+def test_fused_vertex_backward_one_output(which):
+    """Only one of the two outputs carries a gradient (the other's kernel half is skipped)."""
+    dt = torch.float32
+    h, B = 128, 2
+    v0, faces, proj, cam, feats = _scene(40, 21, B, dt, elevation=0.5)
+    (_, _, _, gv1, gf1), (_, _, _, gv2, gf2) = _both(h, v0, faces, proj, cam, feats, dt, which)
+    _close(gv1, gv2, dt)
+    if 'interp' in which:
+        _close(gf1, gf2, dt)
+
+
+def test_fused_vertex_backward_c3_view_and_overflow():
+    """Two views of the C3 sphere at 512x512 (the bench workload), and the same with the record
+    pool limited so every tile takes the overflow path (kd_soft_ovf_bwd with vertex output)."""
+    from kaolin_amd import _lib
+    dt = torch.float32
+    h = 512
+    v0, faces, proj, cam, feats = _scene(250, 101, 2, dt)
+    (i1, s1, _, gv1, gf1), (i2, s2, _, gv2, gf2) = _both(h, v0, faces, proj, cam, feats, dt)
+    assert torch.equal(i1, i2) and torch.equal(s1, s2)
+    _close(gv1, gv2, dt)
+    _close(gf1, gf2, dt)
+    _lib.set_pool_limits(1.0, 0.0)
+    try:
+        (i3, s3, _, gv3, gf3), _ = _both(h, v0, faces, proj, cam, feats, dt)
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_pool_limits(1.0, 1.0)
+    assert torch.equal(s3, s1)
+    _close(gv3, gv2, dt)
+    _close(gf3, gf2, dt)
+
+
+def test_fused_vertex_backward_retained_graph():
+    from kaolin_amd.render.mesh import dibr_rasterization_from_vertices
+    dt = torch.float32
+    h, B = 96, 2
+    v0, faces, proj, cam, feats0 = _scene(30, 16, B, dt)
+    v = v0.clone().requires_grad_(True)
+    feats = feats0.clone().requires_grad_(True)
+    interp, soft, _ = dibr_rasterization_from_vertices(h, h, v, faces, proj, cam, feats)
+    g1, g2 = _grads(h, B, 3, dt)
+    a = torch.autograd.grad([interp, soft], [v, feats], [g1, g2], retain_graph=True)
+    b = torch.autograd.grad([interp, soft], [v, feats], [g1, g2])
+    _close(a[0], b[0], dt)
+    _close(a[1], b[1], dt)
