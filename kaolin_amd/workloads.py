@@ -110,8 +110,8 @@ def face_normals(face_vertices, unit=False):
     e1 = face_vertices[:, :, 1] - face_vertices[:, :, 0]
     e2 = face_vertices[:, :, 2] - face_vertices[:, :, 0]
     n = torch.cross(e1, e2, dim=2)
-    if unit:
-        n = torch.nn.functional.normalize(n, dim=2)
+    if unit:  # ops/mesh/trianglemesh.py:333-335 (length + 1e-10, not F.normalize)
+        n = n / (n.norm(dim=2, keepdim=True) + 1e-10)
     return n
 
 
