@@ -3,6 +3,10 @@
 hipcc cross-compiles for gfx950 without a GPU.  Flags that are part of the numerics contract:
   -ffp-contract=off  no FMA contraction (the reference expressions are evaluated as written)
   no -ffast-math, no -fgpu-flush-denormals-to-zero
+and one code-generation guard:
+  -mllvm -disable-promote-alloca-to-lds  the AMDGPU pass that moves small private arrays into LDS
+      (256 lanes x the array) fires or not depending on register pressure; in kd_bin_count it
+      turned the 8-float cull array into 8 KB of LDS traffic per workgroup (30 -> 51 us)
 """
 import concurrent.futures
 import os
@@ -23,6 +27,7 @@ HEADERS = sorted(f for f in os.listdir(CSRC) if f.endswith('.hpp'))  # every sou
 ARCH = os.environ.get('KAOLIN_AMD_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', f'--offload-arch={ARCH}',
+         '-mllvm', '-disable-promote-alloca-to-lds',
          '-Wall', '-Wno-unused-function', '-Wno-unused-result']
 
 

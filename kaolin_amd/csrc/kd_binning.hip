@@ -125,6 +125,7 @@ template <typename T>
 struct BinJobs {
   FaceSet<T> fs[2];
   BinBuffers bb[2];
+  SpanConsts k[2];  // make_span constants of each set (host-computed)
 };
 
 template <typename T>
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
         T v[6], box[4];
         load_corners(fs, i, v);
         face_box(fs, i, v, box);
-        s = make_span<T>(box[0], box[1], box[2], box[3], fs.M, fs.H, fs.W);
+        s = make_span_k<T>(box[0], box[1], box[2], box[3], jobs.k[blockIdx.z]);
         if constexpr (std::is_same<T, float>::value) {
           if (bb.cull && !span_empty(s)) {
             float cc[8];
@@ -166,8 +167,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
       }
       bb.spans[i] = s;
       if (!span_empty(s)) {
-        const int cx0 = s.x0 / bb.g.ct, cx1 = s.x1 / bb.g.ct;
-        const int cy0 = s.y0 / bb.g.ct, cy1 = s.y1 / bb.g.ct;
+        const int cx0 = s.x0 >> bb.g.sh, cx1 = s.x1 >> bb.g.sh;
+        const int cy0 = s.y0 >> bb.g.sh, cy1 = s.y1 >> bb.g.sh;
         for (int cy = cy0; cy <= cy1; ++cy)
           for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&s_cnt[cy * bb.g.nctx + cx], 1);
       }
@@ -235,7 +236,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
 }
 
 template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
+__global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   const FaceSet<T> &fs = jobs.fs[blockIdx.z];
   const BinBuffers &bb = jobs.bb[blockIdx.z];
   if (blockIdx.x == gridDim.x - 1) {  // the extra column: the set's tile dispatch order
@@ -294,8 +295,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
     const int t = u * kBlock + tid;
     const uint32_t bit = 1u << (t & 31);
     const int word = t >> 5;
-    for (int cy = sp[u].y0 / bb.g.ct; cy <= sp[u].y1 / bb.g.ct; ++cy)
-      for (int cx = sp[u].x0 / bb.g.ct; cx <= sp[u].x1 / bb.g.ct; ++cx)
+    for (int cy = sp[u].y0 >> bb.g.sh; cy <= sp[u].y1 >> bb.g.sh; ++cy)
+      for (int cx = sp[u].x0 >> bb.g.sh; cx <= sp[u].x1 >> bb.g.sh; ++cx)
         atomicOr(&s_mask[(cy * bb.g.nctx + cx) * kWords + word], bit);
   }
   __syncthreads();
@@ -309,8 +310,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scatter(BinJobs<T> jobs) {
     const uint32_t bit = 1u << (t & 31);
     const int word = t >> 5;
     const int local = chunk * kChunk + t;
-    for (int cy = sp[u].y0 / bb.g.ct; cy <= sp[u].y1 / bb.g.ct; ++cy)
-      for (int cx = sp[u].x0 / bb.g.ct; cx <= sp[u].x1 / bb.g.ct; ++cx) {
+    for (int cy = sp[u].y0 >> bb.g.sh; cy <= sp[u].y1 >> bb.g.sh; ++cy)
+      for (int cx = sp[u].x0 >> bb.g.sh; cx <= sp[u].x1 >> bb.g.sh; ++cx) {
         const int c = cy * bb.g.nctx + cx;
         const int bc = bbase[c];
         if (bc < 0) continue;  // overflowed: its tiles walk all faces of the view
@@ -448,6 +449,7 @@ hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t str
   BinJobs<T> jobs;
   jobs.fs[0] = jobs.fs[1] = fs;
   jobs.bb[0] = jobs.bb[1] = bb;
+  jobs.k[0] = jobs.k[1] = span_consts(fs.M, fs.H, fs.W);
   return bin_jobs<T>(jobs, 1, stream);
 }
 
@@ -463,6 +465,8 @@ hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSe
   jobs.fs[1] = fs1;
   jobs.bb[0] = bb0;
   jobs.bb[1] = bb1;
+  jobs.k[0] = span_consts(fs0.M, fs0.H, fs0.W);
+  jobs.k[1] = span_consts(fs1.M, fs1.H, fs1.W);
   return bin_jobs<T>(jobs, 2, stream);
 }
 

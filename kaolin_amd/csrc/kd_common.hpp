@@ -199,6 +199,91 @@ __device__ inline Span make_span(T xmin, T ymin, T xmax, T ymax, float M, int H,
   return s;
 }
 
+// The per-call constants of make_span, computed once on the host (IEEE fp32 M / W there is the
+// device's quotient too): the binning kernels compute a span per face.
+struct SpanConsts {
+  float M, sx, sy;  // sx = M / W, sy = M / H (the first factor of px_cx / px_cy)
+  double rsx, rsy;  // 1 / sx, 1 / sy (estimates only)
+  int H, W;
+  int fast;         // sx > 0 and sy > 0: estimate + settle; else binary search (make_span)
+};
+
+inline SpanConsts span_consts(float M, int H, int W) {
+  SpanConsts k;
+  k.M = M;
+  k.H = H;
+  k.W = W;
+  k.sx = W > 0 ? M / (float)W : 0.f;
+  k.sy = H > 0 ? M / (float)H : 0.f;
+  k.fast = k.sx > 0.f && k.sy > 0.f;
+  k.rsx = k.fast ? 1.0 / (double)k.sx : 0.0;
+  k.rsy = k.fast ? 1.0 / (double)k.sy : 0.0;
+  return k;
+}
+
+// First index a in [0, n] with c(a) >= lo for centres c increasing in the index (n if none), from
+// the estimate e (within one index of the answer for finite inputs): one settling step each way,
+// verified; the linear walk runs only if the verification fails (never for finite inputs).
+template <typename T, typename Centre>
+__device__ __forceinline__ int settle_first_ge(T lo, int n, int e, Centre c) {
+  if (e > 0 && (T)c(e - 1) >= lo)
+    --e;
+  else if (e < n && (T)c(e) < lo)
+    ++e;
+  const bool ok = (e == 0 || (T)c(e - 1) < lo) && (e == n || (T)c(e) >= lo);
+  if (__builtin_expect(!ok, 0)) {
+    while (e > 0 && (T)c(e - 1) >= lo) --e;
+    while (e < n && (T)c(e) < lo) ++e;
+  }
+  return e;
+}
+
+// make_span for a positive multiplier with host constants: the same integer span (the double
+// estimates are settled against the exact fp32 centre formula, like span_x / span_y).
+template <typename T>
+__device__ __forceinline__ Span make_span_k(T xmin, T ymin, T xmax, T ymax, const SpanConsts &k) {
+  if (!k.fast) return make_span<T>(xmin, ymin, xmax, ymax, k.M, k.H, k.W);
+  const int W = k.W, H = k.H;
+  const float sx = k.sx, sy = k.sy;
+  auto cx = [&](int i) { return sx * (float)(2 * i + 1 - W); };  // px_cx, increasing in i
+  // rows: cy(h) decreases with h; with g = H - 1 - h, cy = sy * (2 g + 1 - H) increases in g
+  auto cyg = [&](int g) { return sy * (float)(2 * g + 1 - H); };
+  int a = 0, b = W - 1, c = 0, d = H - 1;
+  if (!isnan(xmin)) {  // a = first column with cx >= xmin
+    double t = ((double)xmin * k.rsx + (double)(W - 1)) * 0.5;
+    t = fmin(fmax(t, -1.0), (double)W);
+    a = settle_first_ge<T>(xmin, W, min(max((int)ceil(t), 0), W), cx);
+  }
+  if (!isnan(xmax)) {  // b = last column with cx < xmax = (first with cx >= xmax) - 1
+    double t = ((double)xmax * k.rsx + (double)(W - 1)) * 0.5;
+    t = fmin(fmax(t, -1.0), (double)W);
+    b = settle_first_ge<T>(xmax, W, min(max((int)ceil(t), 0), W), cx) - 1;
+  }
+  if (!isnan(ymax)) {  // c = first row with cy < ymax = H - (first g with cyg >= ymax)
+    double t = ((double)ymax * k.rsy + (double)(H - 1)) * 0.5;
+    t = fmin(fmax(t, -1.0), (double)H);
+    c = H - settle_first_ge<T>(ymax, H, min(max((int)ceil(t), 0), H), cyg);
+  }
+  if (!isnan(ymin)) {  // d = last row with cy >= ymin = H - 1 - (first g with cyg >= ymin)
+    double t = ((double)ymin * k.rsy + (double)(H - 1)) * 0.5;
+    t = fmin(fmax(t, -1.0), (double)H);
+    d = H - 1 - settle_first_ge<T>(ymin, H, min(max((int)ceil(t), 0), H), cyg);
+  }
+  Span s;
+  if (a > b || c > d) {
+    s.x0 = 1;
+    s.x1 = 0;
+    s.y0 = 1;
+    s.y1 = 0;
+  } else {
+    s.x0 = (short)a;
+    s.x1 = (short)b;
+    s.y0 = (short)c;
+    s.y1 = (short)d;
+  }
+  return s;
+}
+
 __device__ __forceinline__ bool span_empty(Span s) { return s.x0 > s.x1 || s.y0 > s.y1; }
 __device__ __forceinline__ bool span_overlaps(Span s, int x0, int x1, int y0, int y1) {
   return !(s.x1 < x0 || s.x0 > x1 || s.y1 < y0 || s.y0 > y1 || span_empty(s));
@@ -315,7 +400,8 @@ __device__ __forceinline__ int wg_compact(bool pred, int *s_cnt, int &total) {
 constexpr int kCoarseTile0 = KD_COARSE_TILE0;  // smallest coarse tile (px); grows to <= 32 per side
 
 struct BinGeom {
-  int ct;        // coarse tile edge in pixels (multiple of kTile)
+  int ct;        // coarse tile edge in pixels (a power of two, multiple of kTile)
+  int sh;        // log2(ct): coarse tile of pixel coordinate x >= 0 is x >> sh
   int nctx, ncty;
   __host__ __device__ int nct() const { return nctx * ncty; }
 };
@@ -326,6 +412,8 @@ __host__ __device__ inline BinGeom bin_geom(int H, int W) {
   while (((m + ct - 1) / ct) > 32) ct *= 2;
   BinGeom g;
   g.ct = ct;
+  g.sh = 0;
+  while ((1 << g.sh) < ct) ++g.sh;
   g.nctx = (W + ct - 1) / ct;
   g.ncty = (H + ct - 1) / ct;
   return g;

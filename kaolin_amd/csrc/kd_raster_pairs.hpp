@@ -220,7 +220,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   if ((s_nan[w] >> lane) & 1ull) {
     // the reference's sequential loop over this pixel's coarse bin (ascending faces)
     const BinGeom &g = a.bb.g;
-    const int ct = (t.py / g.ct) * g.nctx + (t.px / g.ct);
+    const int ct = (t.py >> g.sh) * g.nctx + (t.px >> g.sh);
     int n;
     const int *bin = bin_list(a.bb, b, ct, lo, (int)(hi - lo), -1, n);
     float max_z0 = -INFINITY;

@@ -402,7 +402,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       if (tid == 0) S.base = tile * kBlock * K;
     } else if (tid == 0) {
       const BinGeom &g = a.bb.g;
-      const int ct = (t.Y0 / g.ct) * g.nctx + (t.X0 / g.ct);
+      const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
       int nb;
       bin_list(a.bb, b, ct, lo, nview, nbin, nb);
       const int64_t room = (int64_t)U * (int64_t)min(K, nb);

@@ -148,7 +148,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
                                             Round round, int dbg = 0, Done done = Done()) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const BinGeom &g = bb.g;
-  const int ct = (t.Y0 / g.ct) * g.nctx + (t.X0 / g.ct);
+  const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
   int n;
   const int *bin = bin_list(bb, b, ct, lo, nview, t.nbin, n);
   int cnt = 0;
