@@ -14,11 +14,12 @@
 namespace kd {
 
 // dibr_soft_mask_cuda.cu:100-163: squared distance type (0..5) and probability of one face,
-// bit-identical to the reference (kd_softdist.hpp).
+// bit-identical to the reference (kd_softdist.hpp; fp32: one double reciprocal per edge for its
+// three quotients, quo_f).
 template <typename T>
 __device__ __forceinline__ void soft_face_dist(T x0, T y0, const T v[6], float M, float sigmainv,
                                                int &edgeid, T &prob) {
-  soft_face_dist_ref<T>(x0, y0, v, M, sigmainv, edgeid, prob);
+  soft_face_dist_ref<T, std::is_same<T, float>::value>(x0, y0, v, M, sigmainv, edgeid, prob);
 }
 
 // backward terms of one (pixel, close face) pair, dibr_soft_mask_cuda.cu:281-348; adds to the
