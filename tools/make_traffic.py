@@ -27,7 +27,7 @@ SLOT = {
     'kd::kd_bin_scan<float>': 'kd_bin_scan',
     'kd::kd_soft_ovf_fwd<float, true>': 'kd_soft_ovf_fwd', 'kd::kd_soft_ovf_bwd<float>': 'kd_soft_ovf_bwd',
     'kd::kd_bin_scatter<float>': 'kd_bin_scatter',
-    'kd::kd_dibr_bwd<float>': 'kd_dibr_bwd',
+    'kd::kd_dibr_bwd<float>': 'kd_dibr_bwd', 'kd::kd_dibr_bwd<float, false>': 'kd_dibr_bwd',
     'kd::kd_dibr_fwd_tiles': 'kd_dibr_fwd',
     'kd::kd_dibr_fwd_tiles<false>': 'kd_dibr_fwd',
 }
