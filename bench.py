@@ -144,6 +144,13 @@ class Workload:
         self.F, self.H, self.W, self.D = F, H, W, self.feats.shape[-1]
         g_feat, g_soft = workloads.view_grads(first, n, H, W, self.D, dtype=dt)
         self.g_feat, self.g_soft = g_feat.to(dev), g_soft.to(dev)
+        self.iou = args.iou
+        self.gt = None
+        if self.iou and not self.soup:  # a target silhouette: a disc in the middle of each view
+            yy, xx = torch.meshgrid(torch.arange(H, dtype=dt), torch.arange(W, dtype=dt),
+                                    indexing='ij')
+            disc = (((yy - H / 2) ** 2 + (xx - W / 2) ** 2) < (0.4 * min(H, W)) ** 2).to(dt)
+            self.gt = disc.expand(n, H, W).contiguous().to(dev)
         self.params = [self.fvi, self.feats] if self.soup else [self.vertices, self.feats]
 
     def forward_backward(self):
@@ -155,7 +162,7 @@ class Workload:
             return face_idx
         return distributed.dibr_forward_backward(
             self.vertices, self.faces, self.proj, self.cam, self.feats, self.H, self.W,
-            self.g_feat, self.g_soft, **self.kw)
+            self.g_feat, self.g_soft, gt_mask=self.gt, iou=self.iou or 'fused', **self.kw)
 
     def clear(self):
         for p in self.params:
@@ -249,6 +256,9 @@ def main():
     ap.add_argument('--lists', action='store_true',
                     help='materialise the (B,H,W,K) close-face lists (reference structure)')
     ap.add_argument('--no-graph', action='store_true', help='launch every kernel eagerly')
+    ap.add_argument('--iou', default=None, choices=['fused', 'compose'],
+                    help='the soft mask\'s gradient from the silhouette loss mask_iou(soft, gt) '
+                         '(the training loop\'s), fused into the renderer or as the composition')
     ap.add_argument('--no-weak', action='store_true', help='skip the N > 1 weak-scaling phase')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--pmc', default=None,
@@ -395,6 +405,8 @@ def main():
                                    if world > 1 and not soup else ''),
                    'launch': launch,
                    'close_lists': 'materialised' if args.lists else 'not materialised',
+                   'soft_mask_grad': (f'mask_iou(soft, gt) ({args.iou})' if args.iou
+                                      else 'fixed seeded grad_soft'),
                    'covered_px_per_step': covered, 'front_faces': Fv},
         'roofline': roofline,
         'step_roofline': step_roof,

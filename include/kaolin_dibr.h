@@ -267,6 +267,47 @@ int kd_dibr_rasterization_backward_f64(int batch, int height, int width, int64_t
                                        int knum, double *grad_fvi, double *grad_feat,
                                        int grads_zeroed, void *workspace, size_t workspace_bytes,
                                        void *stream);
+/* dibr_rasterization with the silhouette loss fused in (mask_iou of
+ * kaolin/metrics/render.py:18-40 applied to the soft mask, as in the DIB-R training loop
+ * examples/tutorial/ian_dibr.py:264-265): the forward above, plus
+ *   iou_loss (scalar) = 1 - mean_b(U_b / (D_b + 1e-10)),  U_b = sum(s g), D_b = sum(s + g - s g)
+ * over soft_mask s and gt_mask g (B, H, W), with the per-pixel terms in T, accumulated in fp64
+ * inside the soft mask's tile launch (iou_acc, B x 32 x 2 doubles of partials, scratch) and
+ * finished like
+ * kd_mask_iou_forward_* does; iou_stats = (U_b, D_b) in T, B x 2.  knum <= 32.
+ * The backward adds d iou_loss / d soft_mask -- the arithmetic of kd_mask_iou_backward_*, its
+ * incoming gradient the DEVICE scalar grad_iou_loss (nullable) -- to grad_soft (nullable) per pixel
+ * inside the soft mask's backward: no (B, H, W) gradient of the mask is materialised. */
+int kd_dibr_rasterization_iou_forward_f32(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const float *fvz,
+    int64_t fvz_face_stride, int64_t fvz_corner_stride, const float *fvi, const float *feat,
+    const float *normals_z, int64_t normals_z_stride, double multiplier, float eps,
+    float sigmainv, double boxlen, int knum, const float *gt_mask, float *interp,
+    int64_t *face_idx, float *weights, float *soft, float *iou_loss, float *iou_stats,
+    double *iou_acc, int want_grad, float *grad_fvi_zero, float *grad_feat_zero,
+    void *workspace, size_t workspace_bytes, void *stream);
+int kd_dibr_rasterization_iou_forward_f64(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const double *fvz,
+    int64_t fvz_face_stride, int64_t fvz_corner_stride, const double *fvi, const double *feat,
+    const double *normals_z, int64_t normals_z_stride, double multiplier, float eps,
+    float sigmainv, double boxlen, int knum, const double *gt_mask, double *interp,
+    int64_t *face_idx, double *weights, double *soft, double *iou_loss, double *iou_stats,
+    double *iou_acc, int want_grad, double *grad_fvi_zero, double *grad_feat_zero,
+    void *workspace, size_t workspace_bytes, void *stream);
+int kd_dibr_rasterization_iou_backward_f32(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const float *grad_interp,
+    const float *grad_soft, const float *grad_iou_loss, const float *gt_mask,
+    const float *iou_stats, const int64_t *face_idx, const float *weights, const float *soft,
+    const float *fvi, const float *feat, float eps, double multiplier, double boxlen,
+    float sigmainv, int knum, float *grad_fvi, float *grad_feat, int grads_zeroed,
+    void *workspace, size_t workspace_bytes, void *stream);
+int kd_dibr_rasterization_iou_backward_f64(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const double *grad_interp,
+    const double *grad_soft, const double *grad_iou_loss, const double *gt_mask,
+    const double *iou_stats, const int64_t *face_idx, const double *weights, const double *soft,
+    const double *fvi, const double *feat, float eps, double multiplier, double boxlen,
+    float sigmainv, int knum, double *grad_fvi, double *grad_feat, int grads_zeroed,
+    void *workspace, size_t workspace_bytes, void *stream);
 /* The same backward with the face -> vertex step of prepare_vertices fused in (SURVEY.md §8 f1;
  * reference: the gather backward of kaolin/ops/mesh/mesh.py:24-45 with the projection and camera
  * transform of kaolin/render/mesh/utils.py:164-167 and render/camera/legacy.py:120-139): the raster

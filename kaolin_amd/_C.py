@@ -410,10 +410,13 @@ def _rows_view(t, F, inner):
 
 def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertices_image,
                                      face_features, face_normals_z, sigmainv, boxlen, knum,
-                                     multiplier, eps, want_grad=True, grad_buffers=None):
+                                     multiplier, eps, want_grad=True, grad_buffers=None,
+                                     iou_gt=None):
     """rasterize(valid = normals_z >= 0) + dibr_soft_mask in one launch sequence.  Returns
-    (interp, face_idx, weights, soft, workspace).  grad_buffers = (grad_fvi, grad_feat or None):
-    buffers of the backward that this forward zeroes (see kd_dibr_rasterization_forward)."""
+    (interp, face_idx, weights, soft, workspace), and with iou_gt (B, H, W) also (iou_loss,
+    iou_stats): mask_iou(soft, iou_gt) fused in (kd_dibr_rasterization_iou_forward).
+    grad_buffers = (grad_fvi, grad_feat or None): buffers of the backward that this forward
+    zeroes (see kd_dibr_rasterization_forward)."""
     fn = 'dibr_rasterization'
     dev = _check_same_gpu(fn, face_vertices_z=face_vertices_z,
                           face_vertices_image=face_vertices_image, face_features=face_features,
@@ -442,6 +445,22 @@ def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertic
     nb = int(_lib.load().kd_dibr_workspace_size(B, height, width, F, knum,
                                                 1 if fvi.dtype == torch.float64 else 0))
     ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+    if iou_gt is not None:
+        _check_size(fn, 'gt_mask', iou_gt, (B, height, width))
+        _check_dtype(fn, face_vertices_image, gt_mask=iou_gt)
+        if iou_gt.device != dev:
+            raise RuntimeError(f'{fn}: gt_mask must be on {dev}')
+        gt = iou_gt.contiguous()
+        loss = torch.empty((), **opts)
+        stats = torch.empty((B, 2), **opts)
+        acc = torch.empty((B, 32, 2), device=dev, dtype=torch.float64)  # kIouParts partials
+        _lib.call(f'kd_dibr_rasterization_iou_forward_{sfx}', B, height, width, F, D, _ptr(fvz),
+                  fvz_fs, fvz_cs, _ptr(fvi), _ptr(feat), _ptr(nz), nz_s, float(multiplier),
+                  float(eps), float(sigmainv), float(boxlen), knum, _ptr(gt), _ptr(interp),
+                  _ptr(face_idx), _ptr(weights), _ptr(soft), _ptr(loss), _ptr(stats), _ptr(acc),
+                  1 if want_grad else 0, _ptr(grad_buffers[0]) if grad_buffers else None,
+                  _ptr(grad_buffers[1]) if grad_buffers else None, _ptr(ws), nb, _stream(dev))
+        return interp, face_idx, weights, soft, ws, loss, stats
     _lib.call(f'kd_dibr_rasterization_forward_{sfx}', B, height, width, F, D, _ptr(fvz), fvz_fs,
               fvz_cs, _ptr(fvi), _ptr(feat), _ptr(nz), nz_s, float(multiplier), float(eps),
               float(sigmainv), float(boxlen), knum, _ptr(interp), _ptr(face_idx), _ptr(weights),
@@ -454,9 +473,11 @@ def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertic
 def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights, soft,
                                       face_vertices_image, face_features, eps, multiplier,
                                       boxlen, sigmainv, knum, workspace, need_feat=True,
-                                      grad_buffers=None):
+                                      grad_buffers=None, iou=None):
     """Gradients (grad_fvi, grad_feat or None) of the fused forward, from its workspace;
-    grad_buffers: the (grad_fvi, grad_feat) the forward zeroed, filled in place."""
+    grad_buffers: the (grad_fvi, grad_feat) the forward zeroed, filled in place.  iou =
+    (gt_mask, iou_stats, grad_iou_loss (device scalar)): the fused mask_iou's gradient is added
+    to grad_soft inside the kernel (kd_dibr_rasterization_iou_backward)."""
     dev = face_idx.device
     B, F = face_vertices_image.shape[:2]
     H, W = face_idx.shape[1:3]
@@ -469,6 +490,15 @@ def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights,
         gfvi = torch.empty_like(face_vertices_image)
         gfeat = torch.empty_like(face_features) if need_feat else None
     c = (lambda t: None if t is None else t.contiguous())  # noqa: E731
+    if iou is not None:
+        gt, stats, g_loss = iou
+        _lib.call(f'kd_dibr_rasterization_iou_backward_{sfx}', B, H, W, F, D,
+                  _ptr(c(grad_interp)), _ptr(c(grad_soft)), _ptr(c(g_loss)), _ptr(c(gt)),
+                  _ptr(stats), _ptr(face_idx), _ptr(weights), _ptr(soft),
+                  _ptr(face_vertices_image), _ptr(face_features), float(eps), float(multiplier),
+                  float(boxlen), float(sigmainv), int(knum), _ptr(gfvi), _ptr(gfeat),
+                  1 if zeroed else 0, _ptr(workspace), workspace.numel(), _stream(dev))
+        return gfvi, gfeat
     _lib.call(f'kd_dibr_rasterization_backward_{sfx}', B, H, W, F, D, _ptr(c(grad_interp)),
               _ptr(c(grad_soft)), _ptr(face_idx), _ptr(weights), _ptr(soft),
               _ptr(face_vertices_image), _ptr(face_features), float(eps), float(multiplier),

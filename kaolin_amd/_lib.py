@@ -45,6 +45,14 @@ _SIGS = {
     'kd_dibr_rasterization_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,
                                        c_p, c_p, c_p, c_float, c_double, c_double, c_float,
                                        c_int, c_p, c_p, c_int, c_p, c_size, c_p],
+    'kd_dibr_rasterization_iou_forward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_i64, c_i64,
+                                          c_p, c_p, c_p, c_i64, c_double, c_float, c_float,
+                                          c_double, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                          c_int, c_p, c_p, c_p, c_size, c_p],
+    'kd_dibr_rasterization_iou_backward': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p,
+                                           c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_float, c_double,
+                                           c_double, c_float, c_int, c_p, c_p, c_int, c_p,
+                                           c_size, c_p],
     'kd_dibr_rasterization_backward_vertices': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p,
                                                 c_p, c_p, c_p, c_p, c_p, c_float, c_double,
                                                 c_double, c_float, c_int, c_int, c_i64, c_p,
@@ -144,9 +152,19 @@ def soft_mask_workspace_size(B, H, W, F, knum, double_precision):
 def set_pool_limits(bins=1.0, pairs=1.0):
     """Fractions of the bin and record pools a forward may use (kd_set_pool_limits): a test
     hook that forces the overflow paths; 1, 1 restores the default."""
+    global _pool_limited
     call_plain = load().kd_set_pool_limits(float(bins), float(pairs))
     if call_plain != KD_OK:
         raise RuntimeError(load().kd_last_error().decode(errors='replace'))
+    _pool_limited = float(bins) < 1.0 or float(pairs) < 1.0
+
+
+_pool_limited = False
+
+
+def pool_limits_active():
+    """True while set_pool_limits holds a pool below its full size (the test hook)."""
+    return _pool_limited
 
 
 def profile_enable(on=True):

@@ -51,6 +51,8 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   bb.cull_eps = 0.f;
   bb.clear = nullptr;
   bb.n_clear = 0;
+  bb.clear_b = nullptr;
+  bb.n_clear_b = 0;
   return bb;
 }
 
@@ -136,7 +138,10 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
   for (int c = tid; c < nct; c += kBlock) s_cnt[c] = 0;
-  if (bb.clear && b == 0 && chunk == 0 && tid < bb.n_clear) bb.clear[tid] = 0;
+  if (b == 0 && chunk == 0) {
+    if (bb.clear && tid < bb.n_clear) bb.clear[tid] = 0;
+    for (int i = tid; i < bb.n_clear_b; i += kBlock) bb.clear_b[i] = 0;
+  }
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   __syncthreads();
@@ -406,6 +411,10 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
       const BinBuffers &b = jobs.bb[j];
       if (b.clear && b.n_clear > 0) {
         const hipError_t e = hipMemsetAsync(b.clear, 0, sizeof(int) * b.n_clear, stream);
+        if (e != hipSuccess) return e;
+      }
+      if (b.clear_b && b.n_clear_b > 0) {
+        const hipError_t e = hipMemsetAsync(b.clear_b, 0, sizeof(int) * b.n_clear_b, stream);
         if (e != hipSuccess) return e;
       }
       hipError_t e = hipMemsetAsync(

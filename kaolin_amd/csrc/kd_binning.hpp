@@ -49,6 +49,8 @@ struct BinBuffers {
   float cull_eps;  // the raster eps (cull coefficients only)
   int *clear;      // nullable: n_clear ints zeroed by kd_bin_count (counters of later passes)
   int n_clear;
+  int *clear_b;    // nullable: a second such range (e.g. the fused mask_iou accumulators)
+  int n_clear_b;
   int2 *order;     // [B * fine tiles] (view * tiles + tile, its coarse bin's face count),
                    // heaviest first (tile_order in kd_bin_scatter): the tile kernels' dispatch order
   int nchunk;

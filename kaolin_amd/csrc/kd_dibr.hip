@@ -58,12 +58,28 @@ static FaceSet<T> dibr_faceset(int B, int H, int W, int64_t F, const T *fvi, dou
   return fs;
 }
 
+// mask_iou(soft, gt) fused into dibr_rasterization: inputs / outputs of the
+// forward (gt nullptr: none) and of the backward
+template <typename T>
+struct IouIo {
+  const T *gt;     // (B, H, W) the right-hand mask
+  T *loss;         // () forward
+  T *stats;        // (B, 2) (U_b, D_b) in T: forward out, backward in
+  double *acc;     // (B, kIouParts, 2) fp64 partials, forward
+  const T *grad;   // () device scalar d(outer)/d loss, backward
+};
+
+template <typename T>
+int iou_finish_launch(int B, int nparts, const double *acc, T *stats, T *loss,
+                      hipStream_t stream);
+
 template <typename T>
 static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t fvz_fs,
                     int64_t fvz_cs, const T *fvi, const T *feat, const T *nz, int64_t nz_stride,
                     double M, float eps, float sigmainv, double boxlen, int K, T *interp,
                     int64_t *face_idx, T *weights, T *soft, int want_grad, T *gz_fvi,
-                    T *gz_feat, void *ws, size_t wsb, void *stream_) {
+                    T *gz_feat, void *ws, size_t wsb, void *stream_,
+                    const IouIo<T> &iou = IouIo<T>{}) {
   hipStream_t stream = (hipStream_t)stream_;
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
   KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
@@ -73,10 +89,18 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   const size_t need = dibr_workspace_bytes(B, H, W, F, K, sizeof(T));
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
+  KD_CHECK_ARG(!iou.gt || (iou.loss && iou.stats && iou.acc), "mask_iou: NULL output");
+  KD_CHECK_ARG(!iou.gt || (K <= kFuseSlots && pool_limit_pairs() >= 1.f),
+               "fused mask_iou needs knum <= 32 (the one-launch soft mask)");
   const int64_t nf = (int64_t)B * F;
   if (!want_grad) gz_fvi = gz_feat = nullptr;
-  if (B == 0 || H == 0 || W == 0)
-    return zero_buffers<T>(gz_fvi, nf * 6, gz_feat, gz_feat ? nf * 3 * D : 0, stream);
+  if (B == 0 || H == 0 || W == 0) {
+    const int rc = zero_buffers<T>(gz_fvi, nf * 6, gz_feat, gz_feat ? nf * 3 * D : 0, stream);
+    if (rc != KD_OK || !iou.gt || B == 0) return rc;
+    if (hipMemsetAsync(iou.acc, 0, sizeof(double) * 2 * kIouParts * B, stream) != hipSuccess)
+      return set_error(KD_ERR_LAUNCH, "mask_iou: memset");
+    return iou_finish_launch<T>(B, kIouParts, iou.acc, iou.stats, iou.loss, stream);
+  }
   DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
   // raster: valid faces (normals z >= 0, dibr.py:195), tight boxes; soft: all faces, +-boxlen*M
   FaceSet<T> rfs = dibr_faceset<T>(B, H, W, F, fvi, M);
@@ -90,6 +114,10 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   d.sbb.cull = nullptr;
   d.sbb.clear = d.pb.counters;
   d.sbb.n_clear = kPairClear;
+  if (iou.gt) {  // the IoU accumulators start at zero (kd_bin_count)
+    d.sbb.clear_b = (int *)iou.acc;
+    d.sbb.n_clear_b = 4 * kIouParts * B;
+  }
   hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> ra{rfs, d.rbb, fvz, fvz_fs, fvz_cs, feat, D, eps, interp, face_idx, weights};
@@ -106,12 +134,23 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   sa.nzero0 = gz_fvi ? nf * 6 : 0;
   sa.zero1 = gz_feat;
   sa.nzero1 = gz_feat ? nf * 3 * D : 0;
+  sa.iou_gt = iou.gt;
+  sa.iou_acc = iou.acc;
+  sa.iou_B = B;
+  int rc = KD_OK;
+  bool done = false;
   if constexpr (std::is_same<T, float>::value) {
-    if (dibr_fwd_fusable(ra, sa)) return dibr_fwd_fused_launch(ra, sa, d.pb, stream);
+    if (dibr_fwd_fusable(ra, sa)) {
+      rc = dibr_fwd_fused_launch(ra, sa, d.pb, stream);
+      done = true;
+    }
   }
-  const int rc = raster_launch<T>(ra, stream);
-  if (rc != KD_OK) return rc;
-  return soft_pairs_launch<T>(sa, d.pb, want_grad != 0, true, stream);
+  if (!done) {
+    rc = raster_launch<T>(ra, stream);
+    if (rc == KD_OK) rc = soft_pairs_launch<T>(sa, d.pb, want_grad != 0, true, stream);
+  }
+  if (rc != KD_OK || !iou.gt) return rc;
+  return iou_finish_launch<T>(B, kIouParts, iou.acc, iou.stats, iou.loss, stream);
 }
 
 template <typename T>
@@ -119,7 +158,7 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
                     const T *grad_soft, const int64_t *face_idx, const T *weights, const T *soft,
                     const T *fvi, const T *feat, float eps, double M, double boxlen,
                     float sigmainv, int K, T *gfvi, T *gfeat, int zeroed, void *ws, size_t wsb,
-                    void *stream_) {
+                    void *stream_, const IouIo<T> &iou = IouIo<T>{}) {
   hipStream_t stream = (hipStream_t)stream_;
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
   KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
@@ -130,7 +169,8 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
   const int64_t nf = (int64_t)B * F;
   int rc = zeroed ? KD_OK : zero_buffers<T>(gfvi, nf * 6, gfeat, gfeat ? nf * 3 * D : 0, stream);
   if (rc != KD_OK || B == 0 || H == 0 || W == 0) return rc;
-  if (grad_soft) {
+  KD_CHECK_ARG(!iou.gt || (iou.stats && iou.grad), "mask_iou: NULL stats / gradient");
+  if (grad_soft || iou.gt) {
     DibrBuffers<T> d = dibr_carve<T>(ws, B, H, W, F, K);
     SoftArgs<T> sa{};
     sa.fs = dibr_faceset<T>(B, H, W, F, fvi, M);
@@ -143,6 +183,10 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
     sa.grad_soft = grad_soft;
     sa.soft_in = soft;
     sa.grad_fvi = gfvi;
+    sa.iou_gt = iou.gt;
+    sa.iou_stats = iou.stats;
+    sa.iou_grad = iou.grad;
+    sa.iou_B = B;
     if (grad_interp && D <= 3 && !(debug_flags() & (1 << 24))) {
       // both backwards in one launch (kd_dibr_bwd)
       const RasterBwdArgs<T> ra{B,   H,    W,   F,    D,     grad_interp, face_idx,
@@ -281,6 +325,59 @@ int kd_dibr_rasterization_backward_f64(int B, int H, int W, int64_t F, int D,
   return dibr_bwd<double>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
                           feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat,
                           grads_zeroed, ws, wsb, stream);
+}
+
+int kd_dibr_rasterization_iou_forward_f32(
+    int B, int H, int W, int64_t F, int D, const float *fvz, int64_t fvz_face_stride,
+    int64_t fvz_corner_stride, const float *fvi, const float *feat, const float *normals_z,
+    int64_t normals_z_stride, double M, float eps, float sigmainv, double boxlen, int knum,
+    const float *gt_mask, float *interp, int64_t *face_idx, float *weights, float *soft,
+    float *iou_loss, float *iou_stats, double *iou_acc, int want_grad, float *grad_fvi_zero,
+    float *grad_feat_zero, void *ws, size_t wsb, void *stream) {
+  KD_CHECK_ARG(gt_mask, "mask_iou: gt_mask is NULL");
+  return dibr_fwd<float>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
+                         normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
+                         face_idx, weights, soft, want_grad, grad_fvi_zero, grad_feat_zero, ws,
+                         wsb, stream, IouIo<float>{gt_mask, iou_loss, iou_stats, iou_acc, nullptr});
+}
+int kd_dibr_rasterization_iou_forward_f64(
+    int B, int H, int W, int64_t F, int D, const double *fvz, int64_t fvz_face_stride,
+    int64_t fvz_corner_stride, const double *fvi, const double *feat, const double *normals_z,
+    int64_t normals_z_stride, double M, float eps, float sigmainv, double boxlen, int knum,
+    const double *gt_mask, double *interp, int64_t *face_idx, double *weights, double *soft,
+    double *iou_loss, double *iou_stats, double *iou_acc, int want_grad, double *grad_fvi_zero,
+    double *grad_feat_zero, void *ws, size_t wsb, void *stream) {
+  KD_CHECK_ARG(gt_mask, "mask_iou: gt_mask is NULL");
+  return dibr_fwd<double>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
+                          normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
+                          face_idx, weights, soft, want_grad, grad_fvi_zero, grad_feat_zero, ws,
+                          wsb, stream,
+                          IouIo<double>{gt_mask, iou_loss, iou_stats, iou_acc, nullptr});
+}
+int kd_dibr_rasterization_iou_backward_f32(
+    int B, int H, int W, int64_t F, int D, const float *grad_interp, const float *grad_soft,
+    const float *grad_iou_loss, const float *gt_mask, const float *iou_stats,
+    const int64_t *face_idx, const float *weights, const float *soft, const float *fvi,
+    const float *feat, float eps, double M, double boxlen, float sigmainv, int knum,
+    float *grad_fvi, float *grad_feat, int grads_zeroed, void *ws, size_t wsb, void *stream) {
+  return dibr_bwd<float>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
+                         feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat, grads_zeroed,
+                         ws, wsb, stream,
+                         IouIo<float>{grad_iou_loss ? gt_mask : nullptr, nullptr,
+                                      const_cast<float *>(iou_stats), nullptr, grad_iou_loss});
+}
+int kd_dibr_rasterization_iou_backward_f64(
+    int B, int H, int W, int64_t F, int D, const double *grad_interp, const double *grad_soft,
+    const double *grad_iou_loss, const double *gt_mask, const double *iou_stats,
+    const int64_t *face_idx, const double *weights, const double *soft, const double *fvi,
+    const double *feat, float eps, double M, double boxlen, float sigmainv, int knum,
+    double *grad_fvi, double *grad_feat, int grads_zeroed, void *ws, size_t wsb, void *stream) {
+  return dibr_bwd<double>(B, H, W, F, D, grad_interp, grad_soft, face_idx, weights, soft, fvi,
+                          feat, eps, M, boxlen, sigmainv, knum, grad_fvi, grad_feat, grads_zeroed,
+                          ws, wsb, stream,
+                          IouIo<double>{grad_iou_loss ? gt_mask : nullptr, nullptr,
+                                        const_cast<double *>(iou_stats), nullptr,
+                                        grad_iou_loss});
 }
 
 int kd_dibr_rasterization_backward_vertices_f32(

@@ -166,6 +166,21 @@ size_t iou_workspace_bytes(int B, int64_t P, int esize) {
   return sizeof(double2) * (size_t)B * (size_t)nchunk;
 }
 
+// The loss from per-view (U_b, D_b) partials accumulated elsewhere (the fused DIB-R forward:
+// acc[b][nparts] in fp64): the same finisher as mask_iou's.
+template <typename T>
+int iou_finish_launch(int B, int nparts, const double *acc, T *stats, T *loss,
+                      hipStream_t stream) {
+  hipLaunchKernelGGL(kd_iou_finish<T>, dim3(1), dim3(kBlock), sizeof(double) * B, stream, B,
+                     nparts, (const double2 *)acc, stats, loss, (T *)nullptr);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "mask_iou: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+template int iou_finish_launch<float>(int, int, const double *, float *, float *, hipStream_t);
+template int iou_finish_launch<double>(int, int, const double *, double *, double *,
+                                       hipStream_t);
+
 template <typename T>
 static int iou_forward(int B, int64_t P, const T *lhs, const T *rhs, T *loss, T *stats, T *iou,
                        void *ws, size_t wsb, hipStream_t stream) {

@@ -80,8 +80,37 @@ struct SoftArgs {
   // buffers the soft reduction zeroes on the side (the fused backward's gradients), nullable
   T *zero0, *zero1;
   int64_t nzero0, nzero1;
+  // mask_iou(soft_mask, iou_gt) fused in: the forward adds each view's
+  // (U_b, D_b) = (sum s g, sum (s + g - s g)) into iou_acc (fp64, B x 2); the backward adds
+  // d loss / d soft (kaolin/metrics/render.py:18-40 through autograd, from iou_stats (B x 2, T)
+  // and the device scalar iou_grad) to grad_soft.  iou_gt nullptr: no IoU.
+  const T *iou_gt;
+  double *iou_acc;  // [B][kIouParts] (U, D) partials: a tile adds to partial tile % kIouParts
+  const T *iou_stats;
+  const T *iou_grad;
+  int iou_B;
   VertexOut<T> vo;  // backward: vo.grad set -> vertex gradients instead of grad_fvi (VTX bodies)
 };
+
+// d loss / d soft of the fused backward at pixel gp of view b: the incoming grad_soft (nullable)
+// plus, with iou_gt, mask_iou's gradient w.r.t. its left mask -- kd_iou_bwd's arithmetic
+// (kd_metrics.hip), so the sum is that of rasterize + dibr_soft_mask + mask_iou's autograd.
+template <typename T>
+__device__ __forceinline__ T soft_grad_at(const SoftArgs<T> &a, int b, int64_t gp) {
+  T g = a.grad_soft ? a.grad_soft[gp] : (T)0;
+  if (a.iou_gt) {
+    const T gi = -(*a.iou_grad / (T)a.iou_B);
+    const T U = a.iou_stats[2 * b], Dp = a.iou_stats[2 * b + 1] + (T)1e-10;
+    const T gu = gi / Dp;
+    const T gd = -gi * U / (Dp * Dp);
+    const T gm = gu - gd;
+    const T gl = gm * a.iou_gt[gp] + gd;
+    g = a.grad_soft ? g + gl : gl;
+  }
+  return g;
+}
+
+constexpr int kIouParts = 32;  // fp64 (U, D) partials per view of the fused mask_iou
 
 // Per-wave pair list of the current batch and its per-pixel bookkeeping.
 struct PairBook {

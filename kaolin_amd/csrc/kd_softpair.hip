@@ -326,6 +326,40 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
 // the same workgroup then runs the pair math over its own records and the ordered product of
 // each pixel's slots -- the whole soft mask in one launch.  Pass A notes each (slot, pixel)'s
 // record in LDS, so the product reads the probabilities in slot order.
+// mask_iou fused into the soft mask (SoftArgs::iou_gt): this tile's share of its view's
+// U_b = sum(s g) and D_b = sum(s + g - s g), the per-pixel terms in T as kaolin/metrics/
+// render.py:35-38 forms them (kd_metrics.hip iou_terms), summed in fp64 over the tile and added
+// to one of the view's kIouParts accumulator pairs with one fp64 atomic each.  s_red: 8 doubles
+// of LDS.
+template <typename T>
+__device__ __forceinline__ void iou_tile_terms(const SoftArgs<T> &a, int b, int tl, int64_t p,
+                                               bool in, T s, double *s_red) {
+  if (!a.iou_gt) return;
+  double u = 0.0, d = 0.0;
+  if (in) {
+    const T g = a.iou_gt[p];
+    const T mul = s * g, add = s + g;
+    u = (double)mul;
+    d = (double)(add - mul);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    u += __shfl_xor(u, o);
+    d += __shfl_xor(d, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_red[w] = u;
+    s_red[4 + w] = d;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // partials spread the atomics of a view's tiles over 32 lines
+    double *acc = a.iou_acc + 2 * ((int64_t)b * kIouParts + (tl & (kIouParts - 1)));
+    atomicAdd(acc, s_red[0] + s_red[1] + s_red[2] + s_red[3]);
+    atomicAdd(acc + 1, s_red[4] + s_red[5] + s_red[6] + s_red[7]);
+  }
+}
+
 template <bool FUSED>
 struct SoftPairsLDS {
   unsigned short ridx[FUSED ? kFuseSlots : 1][kBlock];
@@ -334,6 +368,7 @@ struct SoftPairsLDS {
   unsigned short off[4][kWave];
   int64_t base;
   int nrec, ibase, box[4];
+  double iou[8];  // iou_tile_terms
 };
 
 // Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
@@ -443,6 +478,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       S.nrec = 0;
     }
   }
+  T sval = unc ? (T)0.0 : (T)1.0;  // this pixel's soft value (FUSED: the product below)
   if (t.inimg) {
     if (!FUSED) pb.npix[p] = my_kid;  // the split pipeline's reduce
     if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
@@ -484,7 +520,10 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       else
         a.zero1[i - a.nzero0] = (T)0;
     }
-    if (n == 0) return;
+    if (n == 0) {
+      iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
+      return;
+    }
     // pair math over this tile's records (record order: coalesced reads)
     const int tx = tl % pb.ntx, ty = tl / pb.ntx;
     const SoftPairRec *rec = pb.rec + base;
@@ -516,8 +555,10 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
         for (int u = 0; u < U8; ++u)
           if (s0 + u < my_kid) prod = (T)((double)prod * (1.0 - (double)pv[u]));
       }
-      a.soft[p] = (T)(1.0 - (double)prod);
+      sval = (T)(1.0 - (double)prod);
+      a.soft[p] = sval;
     }
+    iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
   }
 }
 
@@ -762,7 +803,7 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
         int px, py;
         tile_pixel(tl % pb.ntx, tl / pb.ntx, r[u].q, px, py);
         const int64_t gp = ((int64_t)b * H + py) * W + px;
-        gs[u] = a.grad_soft[gp];
+        gs[u] = soft_grad_at<T>(a, b, gp);
         so[u] = a.soft_in[gp];
         T v[6];
         load_corners(fs, (int64_t)r[u].row, v);
@@ -833,7 +874,8 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_bwd(SoftArgs<T> a, SoftPai
     const bool unc = t.inimg && a.face_idx[p] < 0;
     const bool wave_unc = __ballot(unc) != 0ull;
     const double sp =
-        unc ? -(double)a.sigmainv * (double)a.grad_soft[p] * (1.0 - (double)a.soft_in[p]) : 0.0;
+        unc ? -(double)a.sigmainv * (double)soft_grad_at<T>(a, b, p) * (1.0 - (double)a.soft_in[p])
+            : 0.0;
     const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
     int my_kid = 0;
     auto stage = [&](int, int64_t) {};
@@ -1019,7 +1061,7 @@ int dibr_backward_merged_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, const Raster
   const int ntl = (int)pb.ntiles;
   const int64_t nr64 = ra.grad ? (int64_t)ra.B * ntl : 0;  // raster tiles (grad_interp given)
   KD_CHECK_ARG(nr64 + kMathBlocks < (1ll << 31), "merged backward: too many tiles");
-  const int nr = (int)nr64, ns = a.grad_soft ? (int)kMathBlocks : 0;
+  const int nr = (int)nr64, ns = (a.grad_soft || a.iou_gt) ? (int)kMathBlocks : 0;
   a.fs.dbg = debug_flags();
   a.fs.tbuf = debug_tile_buffer();
   if (nr + ns > 0) {
@@ -1031,7 +1073,7 @@ int dibr_backward_merged_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, const Raster
       hipLaunchKernelGGL((kd_dibr_bwd<T, false>), dim3((unsigned)(nr + ns)), dim3(kBlock), 0,
                          stream, a, pb, ra, nr, ns, ntl);
   }
-  if (a.grad_soft && pool_may_overflow(a.K)) ovf_bwd_launch<T>(a, pb, stream);
+  if ((a.grad_soft || a.iou_gt) && pool_may_overflow(a.K)) ovf_bwd_launch<T>(a, pb, stream);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr bwd: %s", hipGetErrorString(e));
   return KD_OK;

@@ -100,7 +100,7 @@ class EarlyReduce:
 
 def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_features, height,
                           width, grad_interp, grad_soft, sigmainv=7000., boxlen=0.02, knum=30,
-                          prepare=None, render=None):
+                          prepare=None, render=None, gt_mask=None, iou='fused'):
     """The GPU part of one DIB-R training step on this rank's views: project the
     shared mesh to the rank's cameras (``prepare_vertices``, utils.py:128-175), render
     (``dibr_rasterization``, dibr.py:119-209, valid faces = normals z >= 0) and back-propagate
@@ -111,6 +111,10 @@ def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_f
     vertices (V, 3) leaf, faces (F, 3) int64, camera_transform (B_rank, 4, 3), face_features
     (B_rank, F, 3, D) or (1, F, 3, D) shared.  `prepare` / `render` default to the HIP kernels
     (kaolin_amd.render.mesh); the CPU tests pass oracle-backed ones with the same signatures.
+    With gt_mask (B_rank, H, W) the soft mask's gradient is that of the DIB-R silhouette loss
+    mask_iou(soft_mask, gt_mask) (metrics/render.py:18-40, ian_dibr.py:264-265) instead of
+    grad_soft: fused into the renderer (iou='fused', dibr_rasterization_with_mask_iou) or as the
+    composition dibr_rasterization + mask_iou (iou='compose').
     Returns face_idx (B_rank, H, W)."""
     B = camera_transform.shape[0]
     if prepare is None or render is None:
@@ -121,6 +125,20 @@ def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_f
                             camera_transform=camera_transform)
     feats = face_features if face_features.shape[0] == B else \
         face_features.expand(B, *face_features.shape[1:])
+    if gt_mask is not None:
+        from .render.mesh import dibr_rasterization_with_mask_iou
+        from .metrics.render import mask_iou
+        one = torch.ones((), device=gt_mask.device, dtype=gt_mask.dtype)
+        if iou == 'fused':
+            interp, soft, face_idx, loss = dibr_rasterization_with_mask_iou(
+                height, width, fvc[..., 2], fvi, feats, nrm[..., 2], gt_mask, sigmainv, boxlen,
+                knum)
+        else:
+            interp, soft, face_idx = render(height, width, fvc[..., 2], fvi, feats, nrm[..., 2],
+                                            sigmainv, boxlen, knum)
+            loss = mask_iou(soft, gt_mask)
+        torch.autograd.backward([interp, loss], [grad_interp, one])
+        return face_idx
     interp, soft, face_idx = render(height, width, fvc[..., 2], fvi, feats, nrm[..., 2],
                                     sigmainv, boxlen, knum)
     torch.autograd.backward([interp, soft], [grad_interp, grad_soft])

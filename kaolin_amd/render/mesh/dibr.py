@@ -16,7 +16,7 @@ import threading
 import torch
 from torch.autograd import Function
 
-from ... import _C
+from ... import _C, _lib
 from .rasterization import rasterize
 
 __all__ = ['dibr_soft_mask', 'dibr_rasterization', 'dibr_rasterization_from_vertices',
@@ -272,3 +272,86 @@ def dibr_rasterization_from_vertices(height, width, vertices, faces, camera_proj
             cur += f.shape[-1]
         interp = tuple(out)
     return interp, soft, face_idx
+
+
+class DibrRasterizationIouHip(Function):
+    """dibr_rasterization + mask_iou(soft_mask, gt_mask) fused (kd_dibr_rasterization_iou_*,
+    SURVEY.md §8 f2): the IoU sums are accumulated inside the soft mask's tile launch and the
+    IoU's gradient is formed per pixel inside the soft mask's backward, so neither the standalone
+    IoU kernels nor a (B, H, W) gradient of the mask run."""
+
+    @staticmethod
+    def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features,
+                face_normals_z, gt_mask, sigmainv, boxlen, knum, multiplier, eps):
+        want_grad = face_vertices_image.requires_grad or face_features.requires_grad
+        face_vertices_image = face_vertices_image.contiguous()
+        face_features = face_features.contiguous()
+        gt_mask = gt_mask.contiguous()
+        bufs = None
+        if want_grad:
+            bufs = (torch.empty(face_vertices_image.shape, device=face_vertices_image.device,
+                                dtype=face_vertices_image.dtype),
+                    torch.empty(face_features.shape, device=face_features.device,
+                                dtype=face_features.dtype) if face_features.requires_grad
+                    else None)
+        interp, face_idx, weights, soft, ws, loss, stats = \
+            _C.render.mesh.dibr_rasterization_forward_fused(
+                height, width, face_vertices_z, face_vertices_image, face_features,
+                face_normals_z, sigmainv, boxlen, knum, multiplier, eps, want_grad=want_grad,
+                grad_buffers=bufs, iou_gt=gt_mask)
+        ctx.save_for_backward(face_idx, weights, soft, face_vertices_image, face_features,
+                              ws if want_grad else None, gt_mask, stats)
+        ctx.grad_buffers = bufs
+        ctx.params = (eps, multiplier, boxlen, sigmainv, knum)
+        ctx.mark_non_differentiable(face_idx)
+        ctx.set_materialize_grads(False)
+        return interp, soft, face_idx, loss
+
+    @staticmethod
+    def backward(ctx, grad_interp, grad_soft, grad_face_idx, grad_loss):
+        need_fvi, need_feat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+        none = (None,) * 12
+        if not (need_fvi or need_feat) or (grad_interp is None and grad_soft is None and
+                                           grad_loss is None):
+            return none
+        face_idx, weights, soft, fvi, feat, workspace, gt, stats = ctx.saved_tensors
+        eps, multiplier, boxlen, sigmainv, knum = ctx.params
+        bufs, ctx.grad_buffers = ctx.grad_buffers, None
+        iou = None if grad_loss is None else (gt, stats, grad_loss.reshape(()))
+        gfvi, gfeat = _C.render.mesh.dibr_rasterization_backward_fused(
+            grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier, boxlen,
+            sigmainv, knum, workspace, need_feat=need_feat, grad_buffers=bufs, iou=iou)
+        return (None, None, None, gfvi if need_fvi else None, gfeat, None, None, None, None,
+                None, None, None)
+
+
+def dibr_rasterization_with_mask_iou(height, width, face_vertices_z, face_vertices_image,
+                                     face_features, face_normals_z, gt_mask, sigmainv=7000,
+                                     boxlen=0.02, knum=30, multiplier=None, eps=None):
+    r"""``dibr_rasterization`` (dibr.py:119-209) followed by the DIB-R silhouette loss
+    ``kaolin.metrics.render.mask_iou(soft_mask, gt_mask)`` (metrics/render.py:18-40; the training
+    loop of examples/tutorial/ian_dibr.py:264-265), fused.  gt_mask (B, H, W)
+    of the features' dtype.  Returns (interpolated_features, soft_mask, face_idx, iou_loss), the
+    values of the composition; gradients of any of the outputs flow to face_vertices_image and
+    face_features.  Falls back to the composition where it cannot fuse (knum > 32, close_lists
+    mode, a pool-limit test hook)."""
+    from ...metrics.render import mask_iou
+    _multiplier = 1000. if multiplier is None else multiplier
+    _eps = 1e-8 if eps is None else eps
+    feats = torch.cat(face_features, dim=-1) \
+        if isinstance(face_features, (list, tuple)) else face_features
+    if int(knum) > 32 or _lists_enabled() or _lib.pool_limits_active():
+        interp, soft, face_idx = dibr_rasterization(
+            height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z,
+            sigmainv, boxlen, knum, multiplier, eps)
+        return interp, soft, face_idx, mask_iou(soft, gt_mask)
+    interp, soft, face_idx, loss = DibrRasterizationIouHip.apply(
+        height, width, face_vertices_z, face_vertices_image, feats, face_normals_z, gt_mask,
+        sigmainv, boxlen, knum, _multiplier, _eps)
+    if isinstance(face_features, (list, tuple)):
+        out, cur = [], 0
+        for f in face_features:
+            out.append(interp[..., cur:cur + f.shape[-1]])
+            cur += f.shape[-1]
+        interp = tuple(out)
+    return interp, soft, face_idx, loss
