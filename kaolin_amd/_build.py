@@ -19,6 +19,9 @@ CSRC = os.path.join(PKG, 'csrc')
 LIBDIR = os.path.join(PKG, 'lib')
 LIB = os.path.join(LIBDIR, 'libkaolin_dibr.so')
 OBJDIR = os.path.join(PKG, 'build')
+# the diagnostic variant (-DKD_DIAG=1: device ablation switches, per-tile clocks) for tools/ only
+LIB_DIAG = os.path.join(LIBDIR, 'libkaolin_dibr_diag.so')
+OBJDIR_DIAG = os.path.join(PKG, 'build_diag')
 
 SOURCES = ['kd_capi.cpp', 'kd_binning.hip', 'kd_raster.hip', 'kd_softmask.hip', 'kd_softpair.hip',
            'kd_prepare.hip', 'kd_dibr.hip', 'kd_metrics.hip', 'kd_texture.hip',
@@ -38,38 +41,41 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src):
+def _compile(src, diag=False):
     path = os.path.join(CSRC, src)
-    obj = os.path.join(OBJDIR, src + '.o')
-    deps = [path, os.path.join(ROOT, 'include', 'kaolin_dibr.h')] + \
+    obj = os.path.join(OBJDIR_DIAG if diag else OBJDIR, src + '.o')
+    deps = [path, os.path.join(ROOT, 'include', 'kaolin_dibr.h'), __file__] + \
         [os.path.join(CSRC, h) for h in HEADERS]
     if _stale(obj, deps):
         lang = ['-x', 'hip'] if src.endswith('.cpp') else []
-        cmd = [HIPCC, *FLAGS, *lang, '-c', path, '-o', obj + '.tmp']
+        extra = ['-DKD_DIAG=1'] if diag else []
+        cmd = [HIPCC, *FLAGS, *extra, *lang, '-c', path, '-o', obj + '.tmp']
         subprocess.check_call(cmd)
         os.replace(obj + '.tmp', obj)
     return obj
 
 
-def build(force=False, verbose=True):
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force=False, verbose=True, diag=False):
+    """The production library (diag=False) or the diagnostic one (tools/ only)."""
+    objdir, lib = (OBJDIR_DIAG, LIB_DIAG) if diag else (OBJDIR, LIB)
+    os.makedirs(objdir, exist_ok=True)
     os.makedirs(LIBDIR, exist_ok=True)
     if force:
         for s in SOURCES:
-            o = os.path.join(OBJDIR, s + '.o')
+            o = os.path.join(objdir, s + '.o')
             if os.path.exists(o):
                 os.remove(o)
     with concurrent.futures.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        objs = list(ex.map(_compile, SOURCES))
-    if force or _stale(LIB, objs):
-        tmp = LIB + f'.{os.getpid()}.tmp'
+        objs = list(ex.map(lambda s: _compile(s, diag), SOURCES))
+    if force or _stale(lib, objs):
+        tmp = lib + f'.{os.getpid()}.tmp'
         subprocess.check_call([HIPCC, '-shared', f'--offload-arch={ARCH}', *objs, '-Wl,--no-undefined',
                                '-o', tmp])
-        os.replace(tmp, LIB)
+        os.replace(tmp, lib)
         if verbose:
-            print(f'[kaolin_amd] built {LIB}', file=sys.stderr)
-    return LIB
+            print(f'[kaolin_amd] built {lib}', file=sys.stderr)
+    return lib
 
 
 if __name__ == '__main__':
-    build(force='--force' in sys.argv)
+    build(force='--force' in sys.argv, diag='--diag' in sys.argv)

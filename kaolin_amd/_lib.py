@@ -9,7 +9,9 @@ import re
 import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, 'lib', 'libkaolin_dibr.so')
+# KAOLIN_AMD_DIAG=1 (tools/ only): the diagnostic build with the device ablation switches
+LIB_PATH = os.path.join(_PKG, 'lib', 'libkaolin_dibr_diag.so'
+                        if os.environ.get('KAOLIN_AMD_DIAG') == '1' else 'libkaolin_dibr.so')
 HEADER = os.path.join(os.path.dirname(_PKG), 'include', 'kaolin_dibr.h')
 
 KD_OK = 0

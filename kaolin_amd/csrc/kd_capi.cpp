@@ -19,7 +19,9 @@ std::atomic<long long *> g_tbuf{nullptr};
 std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
 float pool_limit_bins() { return g_lim_bins.load(); }
 float pool_limit_pairs() { return g_lim_pairs.load(); }
-long long *debug_tile_buffer() { return (g_debug.load() & 64) ? g_tbuf.load() : nullptr; }
+long long *debug_tile_buffer() {
+  return (KD_DIAG && (g_debug.load() & 64)) ? g_tbuf.load() : nullptr;
+}
 
 namespace {
 std::atomic<bool> g_prof{false};

@@ -14,7 +14,16 @@
 
 namespace kd {
 
-// Diagnostic ablation switches (kd_debug_set, copied into FaceSet::dbg); 0 in production.
+// Diagnostic build (kaolin_amd/_build.py build(diag=True) -> lib/libkaolin_dibr_diag.so, loaded
+// with KAOLIN_AMD_DIAG=1 by the tools under tools/): the device-side ablation switches and the
+// per-tile clocks exist only there.  In the production library ablate() is constant false and
+// TileClock records nothing, so none of it is in the kernels.
+#ifndef KD_DIAG
+#define KD_DIAG 0
+#endif
+__host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG && (flags & bit); }
+
+// Diagnostic ablation switches (kd_debug_set, copied into FaceSet::dbg; diagnostic build only).
 // Bits: 1 skip the per-pixel face tests of the forward kernels, 2 skip staging face data,
 //       4 skip the per-batch work entirely (bin walk only), 8 fp32 raster: lane-per-pixel
 //       kernel instead of the pair pipeline, 16 / 32 skip the per-pair pass of the fp32
@@ -31,7 +40,7 @@ struct TileClock {
   long long t0;
   int64_t idx;
   __device__ TileClock(long long *b, int slot)
-      : buf(b), t0(b ? wall_clock64() : 0),
+      : buf(KD_DIAG ? b : nullptr), t0(KD_DIAG && b ? wall_clock64() : 0),
         idx((int64_t)slot * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x +
             blockIdx.x) {}
   __device__ ~TileClock() {

@@ -59,7 +59,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
     s_geo[8][k] = zz[2 * a.fvz_cs];
   };
   auto round = [&](int nsub, int) {
-    if (nsub == 0 || (fs.dbg & 1)) return;
+    if (nsub == 0 || ablate(fs.dbg, 1)) return;
     const SubSpans ss = load_subspans(L, nsub);
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
 __global__ __launch_bounds__(kBlock, 6) void kd_raster_fwd_pairs(RasterFwdArgs<float> a) {
   TileClock clk(a.fs.tbuf, 0);
   __shared__ RasterPairsLDS S;
-  if (a.fs.dbg & 16384) return;  // diagnostics: dispatch cost only
+  if (ablate(a.fs.dbg, 16384)) return;  // diagnostics: dispatch cost only
   int b, tl, nbin;
   tile_of_block(a.bb, a.fs.H, a.fs.W, b, tl, nbin, a.fs.dbg);
   raster_pairs_tile(a, b, tl, nbin, S);

@@ -111,7 +111,7 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
   // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (d % 8 is the XCD: callers keep
   // it so), so XCD x gets the contiguous band of tiles [x n/8, (x+1) n/8): neighbouring tiles
   // (which share faces) share one L2
-  if ((n & 7) == 0 && !(dbg & (1 << 17))) d = (d & 7) * (n >> 3) + (d >> 3);
+  if ((n & 7) == 0 && !ablate(dbg, (1 << 17))) d = (d & 7) * (n >> 3) + (d >> 3);
   const int b = d / ntl, tl = d - b * ntl;
   const int px = (tl % ntx) * kTile + (tid & 15);
   const int py = (tl / ntx) * kTile + (tid >> 4);
@@ -184,7 +184,7 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
     const int jj = VTX ? j + 3 : j;
     T v = (T)0;
     for (int r = 0; r < ns; ++r) v += s_con[o + r][jj];  // independent reads: pipelined
-    if (v == (T)0 || (dbg & 128)) continue;
+    if (v == (T)0 || ablate(dbg, 128)) continue;
     if (jj < 6)
       atomicAdd(grad_fvi + row * 6 + jj, v);
     else if (grad_feat)

@@ -132,7 +132,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   };
   // B: the reference's per-pixel test (rasterization_cuda.cu:131-162) over the current batch
   auto test_batch = [&](int total) {
-    if (fs.dbg & 16) return;
+    if (ablate(fs.dbg, 16)) return;
     wave_lds_sync();
     for (int e0 = 0; e0 < total; e0 += kWave) {
       const int e = e0 + lane;
@@ -159,7 +159,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
     wave_lds_sync();
   };
   auto round = [&](int nsub, int) {
-    if (nsub == 0 || (fs.dbg & 1)) return;
+    if (nsub == 0 || ablate(fs.dbg, 1)) return;
     int total = 0;
 #pragma unroll 1
     for (int c = 0; c < 4; ++c) {
@@ -212,7 +212,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   };
   tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
 
-  if (!t.inimg || (fs.dbg & 8192)) return;
+  if (!t.inimg || ablate(fs.dbg, 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const float x0 = px_cx(M, W, t.px), y0 = px_cy(M, H, t.py);
   int best = -1;

@@ -52,7 +52,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
   if (__syncthreads_or(unc)) {
     auto stage = [&](int k, int64_t fi) { soft_stage(fs, s_geo, k, fi); };
     auto flush = [&](int npairs) {  // passes B and C
-      if (fs.dbg & 32) npairs = 0;
+      if (ablate(fs.dbg, 32)) npairs = 0;
       wave_lds_sync();
       for (int e = lane; e < npairs; e += kWave) {
         const int pr = P.pair[w][e];
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_fwd(SoftArgs<T> a) {
       wave_lds_sync();
     };
     auto round = [&](int nsub, int) {
-      if (!umask || nsub == 0 || (fs.dbg & 1)) return;
+      if (!umask || nsub == 0 || ablate(fs.dbg, 1)) return;
       any_sub = true;
       const SubSpans ss = load_subspans(L, nsub);
       soft_pass_a(ss, nsub, P, umask, K, t, my_kid, flush);

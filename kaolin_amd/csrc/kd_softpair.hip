@@ -387,7 +387,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   const int nview = (int)(hi - lo);
   TileGeom t = tile_geom(H, W, tl);
   t.nbin = nbin;
-  if (fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, coarse count) of the slot
+  if (KD_DIAG && fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, bin) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
@@ -452,7 +452,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     t.FY1 = s_box[3];
     auto stage = [&](int, int64_t) {};  // pass A needs the spans only
     auto round = [&](int nsub, int) {
-      if (wave_unc && !(fs.dbg & 1024))
+      if (wave_unc && !ablate(fs.dbg, 1024))
         for (int c = 0; c * kWave < nsub; ++c)
           soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], &S.nrec,
                              pb.rec + S.base, FUSED ? S.ridx : nullptr);
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
   __shared__ SoftPairsLDS<FUSED> S;
   TileClock clk(a.fs.tbuf, 1);
   clk.start_to(2);
-  if (a.fs.dbg & 16384) return;  // diagnostics: dispatch cost only
+  if (ablate(a.fs.dbg, 16384)) return;  // diagnostics: dispatch cost only
   int b, tl, nbin;
   tile_of_block(a.bb, a.fs.H, a.fs.W, b, tl, nbin, a.fs.dbg);
   soft_pairs_tile<T, FUSED>(a, pb, b, tl, nbin, S);
@@ -1010,9 +1010,16 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
-    hipLaunchKernelGGL(a.fs.tbuf ? kd_dibr_fwd_tiles<true> : kd_dibr_fwd_tiles<false>,
-                       dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
-                       stream, ra, a, pb);
+    if constexpr (KD_DIAG) {
+      if (a.fs.tbuf) {
+        hipLaunchKernelGGL(kd_dibr_fwd_tiles<true>, dim3((unsigned)pb.ntiles, ra.fs.B),
+                           dim3(kBlock), 0, stream, ra, a, pb);
+        goto launched;
+      }
+    }
+    hipLaunchKernelGGL(kd_dibr_fwd_tiles<false>, dim3((unsigned)pb.ntiles, ra.fs.B),
+                       dim3(kBlock), 0, stream, ra, a, pb);
+  launched:;
   }
   if (pool_may_overflow(a.K)) ovf_fwd_launch<float, true>(a, pb, stream);
   const hipError_t e = hipGetLastError();

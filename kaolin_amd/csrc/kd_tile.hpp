@@ -47,7 +47,7 @@ __device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W
     // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (d % 8), and the order holds a
     // coarse tile's fine tiles consecutively; within each group of 32 workgroups fine tile j of
     // coarse tile g runs at d = 8 j + g, so the tiles sharing a coarse bin share one L2.
-    if ((d | 31) < n && !(dbg & (1 << 17))) d = (d & ~31) | ((d & 7) << 2) | ((d >> 3) & 3);
+    if ((d | 31) < n && !ablate(dbg, (1 << 17))) d = (d & ~31) | ((d & 7) << 2) | ((d >> 3) & 3);
     const int2 v = bb.order[d];
     b = v.x / ntiles;
     tile = v.x - b * ntiles;
@@ -179,7 +179,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
       // a batch holds at most kCap faces: flush first if this chunk would overflow it
       if (cnt + tot > kCap) {
         __syncthreads();
-        if (!(dbg & 2))
+        if (!ablate(dbg, 2))
           for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
         int nsub = 0;
         for (int k0 = 0; k0 < cnt; k0 += kWave) {
@@ -191,7 +191,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
           nsub += __popcll(m);
         }
         __syncthreads();
-        if (!(dbg & 4)) round(nsub, cnt);
+        if (!ablate(dbg, 4)) round(nsub, cnt);
         __syncthreads();
         cnt = 0;
         if (done()) return;
@@ -205,7 +205,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
   }
   if (cnt > 0) {
     __syncthreads();
-    if (!(dbg & 2))
+    if (!ablate(dbg, 2))
       for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
     int nsub = 0;
     for (int k0 = 0; k0 < cnt; k0 += kWave) {
@@ -217,7 +217,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
       nsub += __popcll(m);
     }
     __syncthreads();
-    if (!(dbg & 4)) round(nsub, cnt);
+    if (!ablate(dbg, 4)) round(nsub, cnt);
     __syncthreads();
   }
 }

@@ -1,5 +1,6 @@
 """A/B of kd_debug_set flags on the bench step time: python tools/ab_bench.py FLAGS_A FLAGS_B [reps]"""
 import os
+os.environ.setdefault('KAOLIN_AMD_DIAG', '1')  # the diagnostic build (ablation flags)
 import subprocess
 import sys
 import json

@@ -1,5 +1,6 @@
 """Ablation timings of the forward kernels (diagnostics; kd_debug_set flags)."""
 import os
+os.environ.setdefault('KAOLIN_AMD_DIAG', '1')  # the diagnostic build (ablation flags)
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

@@ -3,6 +3,7 @@
 # rocprofv3 --pmc pass (SQ counters only) per flag value, eager launches.
 # Usage: tools/pmc_flags.sh FLAGS...   (prints kernel: VALU / SALU / LDS instructions, waves)
 cd /tmp && export TMPDIR=/tmp
+export KAOLIN_AMD_DIAG=1  # the diagnostic build: device ablation switches
 repo="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$repo" || exit 2
 mkdir -p gpurun_out

@@ -2,6 +2,7 @@
 debug flag 1<<26; kd_debug_set flag 64): when do the heavy tiles start and end, and (fused) how
 long is each tile's raster phase?  python tools/soft_timeline.py [config] [extra debug flags]"""
 import os
+os.environ.setdefault('KAOLIN_AMD_DIAG', '1')  # the diagnostic build (ablation flags)
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

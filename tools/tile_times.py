@@ -1,5 +1,6 @@
 """Per-tile durations of the tile kernels (kd_debug_set flag 64): distribution and hot spots."""
 import os
+os.environ.setdefault('KAOLIN_AMD_DIAG', '1')  # the diagnostic build (ablation flags)
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
