@@ -9,7 +9,7 @@ for a in "--config c2" "--config c2 --dtype f64" "--config c3 --dtype f64" \
          "--config c3 --views-per-gpu 2" "--config c3 --views-per-gpu 4" \
          "--config c4 --sigmainv 3000 --boxlen 0.05" "--config c4 --sigmainv 7000 --boxlen 0.02" \
          "--config c4 --sigmainv 17000 --boxlen 0.02" "--config c4 --sigmainv 30000 --boxlen 0.01" \
-         "--config c5" "--config c5soup"; do
+         "--config c5" "--config c5soup" "--config c3 --iou fused" "--config c3 --iou compose"; do
   echo "== $a"
   timeout -k 10 180 python bench.py --no-cpu-baseline $a | grep '^{' >> $out
   tail -c 300 $out; echo
