@@ -427,6 +427,28 @@ int kd_texture_mapping_backward_f64(int batch, int64_t num_samples, int channels
                                     const double *tex, int64_t tex_batch_stride, int mode,
                                     int64_t sample_row, const double *grad_out,
                                     double *grad_tex, double *grad_coords, void *stream);
+/* The same backward with the samples listed per 32 x 32 texel tile: the samples with a nonzero
+ * incoming gradient are listed per tile their taps touch (LDS-aggregated counting pass, scan,
+ * fill), each tile's list is cut into chunks of 1024 entries, and each chunk's taps are summed in
+ * LDS and added to the zeroed texture gradient as row-contiguous atomics.  Independent of the uv
+ * layout (the per-block kernel above has an unbounded texel window at uv seams and poles);
+ * textures of more than 4096 tiles (2048 x 2048) run the per-block kernel.  Same results up to
+ * float summation order.  Workspace: kd_texture_mapping_backward_workspace_size
+ * (shared_texture = tex_batch_stride == 0). */
+size_t kd_texture_mapping_backward_workspace_size(int batch, int64_t num_samples, int tex_height,
+                                                  int tex_width, int shared_texture);
+int kd_texture_mapping_backward_tiled_f32(int batch, int64_t num_samples, int channels,
+                                          int tex_height, int tex_width, const float *coords,
+                                          const float *tex, int64_t tex_batch_stride, int mode,
+                                          const float *grad_out, float *grad_tex,
+                                          float *grad_coords, void *workspace,
+                                          size_t workspace_bytes, void *stream);
+int kd_texture_mapping_backward_tiled_f64(int batch, int64_t num_samples, int channels,
+                                          int tex_height, int tex_width, const double *coords,
+                                          const double *tex, int64_t tex_batch_stride, int mode,
+                                          const double *grad_out, double *grad_tex,
+                                          double *grad_coords, void *workspace,
+                                          size_t workspace_bytes, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * nvdiffrast_fwd compatibility (kaolin/render/mesh/rasterization.py:145-241): from an external

@@ -80,6 +80,8 @@ _SIGS = {
                                          c_p, c_float, c_p, c_p, c_p],
     'kd_texture_mapping_backward': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64, c_int,
                                     c_i64, c_p, c_p, c_p, c_p],
+    'kd_texture_mapping_backward_tiled': [c_int, c_i64, c_int, c_int, c_int, c_p, c_p, c_i64,
+                                          c_int, c_p, c_p, c_p, c_p, c_size, c_p],
 }
 
 
@@ -107,6 +109,9 @@ def load():
             lib.kd_mask_iou_workspace_size.restype = c_size
             lib.kd_deftet_workspace_size.argtypes = [c_int, c_i64, c_int]
             lib.kd_deftet_workspace_size.restype = c_size
+            lib.kd_texture_mapping_backward_workspace_size.argtypes = [c_int, c_i64, c_int, c_int,
+                                                                       c_int]
+            lib.kd_texture_mapping_backward_workspace_size.restype = c_size
             lib.kd_last_error.argtypes = []
             lib.kd_last_error.restype = ctypes.c_char_p
             lib.kd_version.restype = c_int
@@ -149,6 +154,11 @@ def workspace_size(kind, B, H, W, n_total, max_per_view):
 
 def soft_mask_workspace_size(B, H, W, F, knum, double_precision):
     return int(load().kd_soft_mask_workspace_size(B, H, W, F, knum, 1 if double_precision else 0))
+
+
+def texture_backward_workspace_size(B, N, Ht, Wt, shared_texture):
+    return int(load().kd_texture_mapping_backward_workspace_size(B, N, Ht, Wt,
+                                                                 1 if shared_texture else 0))
 
 
 def set_pool_limits(bins=1.0, pairs=1.0):

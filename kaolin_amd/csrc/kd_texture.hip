@@ -20,6 +20,7 @@
 // torch.clamp's backward).
 #include "kd_capi.hpp"
 #include "kd_common.hpp"
+#include "kd_tile.hpp"
 
 namespace kd {
 
@@ -255,6 +256,349 @@ __global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) 
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Texel-tile backward (kd_texture_mapping_backward_tiled): the samples are listed per 32 x 32
+// texel tile, so the texture gradient is summed per tile in LDS and leaves as row-contiguous
+// atomics (the shape the memory-side atomic units take at full rate), whatever the uv layout:
+// the per-sample-block window of kd_tex_bwd grows without bound at uv seams and poles.
+//   kd_tex_tcount  kTexSpan samples per workgroup: the tiles each sample's taps touch (1 to 4)
+//                  counted in LDS, one global atomic per (workgroup, tile) -- counters hit by
+//                  every wave serialise at the memory side; the coordinate gradient.
+//   kd_tex_tscan   one workgroup: exclusive scans of the tile counts and of their kTexChunk
+//                  chunk counts; the chunk table (tile, first entry).
+//   kd_tex_tfill   the same samples again: ranks from the LDS counters, one cursor atomic per
+//                  (workgroup, tile), the sample appended to each touched tile's list.
+//   kd_tex_tacc    persistent: one chunk (<= kTexChunk entries of one tile) at a time, its taps
+//                  summed in LDS, the nonzero sums added to the zeroed gradient.  Chunks of equal
+//                  size keep the magnified tiles (thousands of samples) from serialising; runs
+//                  of adjacent samples in one texel cell are merged in registers first.
+// ------------------------------------------------------------------------------------------
+constexpr int kTexTile = 32;         // texels per tile side
+constexpr int kTexAccC = 4;          // channels per LDS pass of kd_tex_tacc (32 x 33 x 4 x 4 B)
+constexpr int kTexRow = kTexTile + 1;  // LDS row stride of kd_tex_tacc: a column is not one bank
+constexpr int kTexPer = 2;           // samples per thread in kd_tex_tcount / kd_tex_tfill
+constexpr int kTexSpan = kTexPer * kBlock;
+constexpr int kTexChunk = 1024;      // list entries per kd_tex_tacc chunk (4 per thread)
+constexpr int kTexMaxTiles = 4096;   // tiles per texture held in LDS (textures up to 2048 x 2048)
+constexpr int kTexAccGrid = 4096;    // kd_tex_tacc workgroups (persistent over the chunks)
+
+struct TexTiles {
+  int ntx, nty, ntex;  // tiles per row / column, textures (1 when shared)
+  int *count;          // [ntiles + 1]; kd_tex_tscan turns it into entry offsets
+  int *cursor;         // [ntiles]
+  int *nchunk;         // [1]
+  int *chunk_tile;     // [max chunks]
+  int *chunk_e;        // [max chunks] first list entry of the chunk
+  int *list;           // [4 B N] sample indices b * N + n
+};
+
+// tiles (index within the texture) touched by the taps of sample s: 1 to 4
+template <typename T, int MODE>
+__device__ __forceinline__ int tex_sample_tiles(const TexArgs<T> &a, const TexTiles &tt, int64_t s,
+                                                int tiles[4]) {
+  T ix, iy, mx, my, cu, cv;
+  tex_coord<T>(a.coords + 2 * s, ix, iy, mx, my, cu, cv, a.Wt, a.Ht);
+  int x0, y0, x1, y1;
+  if (MODE == KD_TEX_NEAREST) {
+    x0 = x1 = (int)rint(ix);
+    y0 = y1 = (int)rint(iy);
+  } else {
+    x0 = (int)floor(ix);
+    y0 = (int)floor(iy);
+    x1 = min(x0 + 1, a.Wt - 1);
+    y1 = min(y0 + 1, a.Ht - 1);
+  }
+  const int tx0 = x0 / kTexTile, tx1 = x1 / kTexTile, ty0 = y0 / kTexTile, ty1 = y1 / kTexTile;
+  int n = 0;
+  tiles[n++] = ty0 * tt.ntx + tx0;
+  if (tx1 != tx0) tiles[n++] = ty0 * tt.ntx + tx1;
+  if (ty1 != ty0) {
+    tiles[n++] = ty1 * tt.ntx + tx0;
+    if (tx1 != tx0) tiles[n++] = ty1 * tt.ntx + tx1;
+  }
+  return n;
+}
+
+// Adds 1 to ctr[key] (an LDS counter) for every active lane, one atomic per distinct key of the
+// wave; returns the lane's rank among the adders of its key (the counter's old value + its
+// position among the wave's lanes with that key).  Wave-uniform call.
+__device__ __forceinline__ int wave_key_add(bool active, int key, int *ctr) {
+  int pos = 0;
+  uint64_t left = __ballot(active);
+  while (left) {
+    const int leader = __builtin_ctzll(left);
+    const int k = __shfl(key, leader);
+    const uint64_t m = __ballot(active && key == k);
+    int base = 0;
+    if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(ctr + k, __popcll(m));
+    base = __shfl(base, leader);
+    if (active && key == k) pos = base + mbcnt(m);
+    left &= ~m;
+  }
+  return pos;
+}
+
+template <typename T>
+__device__ __forceinline__ bool tex_active(const TexArgs<T> &a, int64_t s) {
+  const T *go = a.grad_out + s * a.C;
+  bool act = false;
+  for (int c = 0; c < a.C; ++c) act |= go[c] != (T)0;
+  return act;
+}
+
+template <typename T, int MODE>
+__device__ __forceinline__ void tex_coord_grad(const TexArgs<T> &a, int b, int64_t s) {
+  T ix, iy, mx, my, cu, cv;
+  tex_coord<T>(a.coords + 2 * s, ix, iy, mx, my, cu, cv, a.Wt, a.Ht);
+  T gix = (T)0, giy = (T)0;
+  if (MODE == KD_TEX_BILINEAR) {
+    const int x0 = (int)floor(ix), y0 = (int)floor(iy);
+    const T ex = (T)(x0 + 1) - ix, wx = ix - (T)x0, ey = (T)(y0 + 1) - iy, wy = iy - (T)y0;
+    const bool vx0 = x0 >= 0 && x0 < a.Wt, vx1 = x0 + 1 >= 0 && x0 + 1 < a.Wt;
+    const bool vy0 = y0 >= 0 && y0 < a.Ht, vy1 = y0 + 1 >= 0 && y0 + 1 < a.Ht;
+    const int64_t plane = (int64_t)a.Ht * a.Wt;
+    const T *t0 = a.tex + (int64_t)b * a.tex_bstride + (int64_t)y0 * a.Wt + x0;
+    const T *go = a.grad_out + s * a.C;
+    for (int c = 0; c < a.C; ++c) {
+      const T g = go[c];
+      const T *tc = t0 + c * plane;
+      if (vy0 && vx0) {
+        const T v = tc[0];
+        gix -= v * ey * g;
+        giy -= v * ex * g;
+      }
+      if (vy0 && vx1) {
+        const T v = tc[1];
+        gix += v * ey * g;
+        giy -= v * wx * g;
+      }
+      if (vy1 && vx0) {
+        const T v = tc[a.Wt];
+        gix -= v * wy * g;
+        giy += v * ex * g;
+      }
+      if (vy1 && vx1) {
+        const T v = tc[a.Wt + 1];
+        gix += v * wy * g;
+        giy += v * wx * g;
+      }
+    }
+  }
+  a.grad_coords[2 * s] = MODE == KD_TEX_BILINEAR && cu != (T)0 ? (mx * gix) * (T)2 : (T)0;
+  a.grad_coords[2 * s + 1] = MODE == KD_TEX_BILINEAR && cv != (T)0 ? -(my * giy) * (T)2 : (T)0;
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void kd_tex_tcount(TexArgs<T> a, TexTiles tt) {
+  __shared__ int s_h[kTexMaxTiles];
+  const int b = blockIdx.y;
+  const int per = tt.nty * tt.ntx;
+  const bool cnt = a.grad_tex != nullptr;
+  if (cnt) {
+    for (int i = threadIdx.x; i < per; i += kBlock) s_h[i] = 0;
+    __syncthreads();
+  }
+  for (int k = 0; k < kTexPer; ++k) {
+    const int64_t n = (int64_t)blockIdx.x * kTexSpan + k * kBlock + threadIdx.x;
+    const bool ok = n < a.N;
+    const int64_t s = (int64_t)b * a.N + (ok ? n : 0);
+    if (cnt) {
+      int tiles[4] = {0, 0, 0, 0};
+      const int nt = ok && tex_active(a, s) ? tex_sample_tiles<T, MODE>(a, tt, s, tiles) : 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) wave_key_add(j < nt, tiles[j], s_h);
+    }
+    if (ok && a.grad_coords) tex_coord_grad<T, MODE>(a, b, s);
+  }
+  if (!cnt) return;
+  __syncthreads();
+  int *gc = tt.count + (int64_t)(a.tex_bstride ? b : 0) * per;
+  for (int i = threadIdx.x; i < per; i += kBlock)
+    if (s_h[i]) atomicAdd(gc + i, s_h[i]);
+}
+
+// one workgroup of 1024 threads: count[0..n) -> exclusive entry offsets (count[n] = total),
+// cursors, and the chunk table
+__global__ __launch_bounds__(1024) void kd_tex_tscan(TexTiles tt, int n) {
+  __shared__ int s_w[2][16];
+  __shared__ int s_carry[2];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid < 2) s_carry[tid] = 0;
+  __syncthreads();
+  for (int i0 = 0; i0 < n; i0 += 1024) {
+    const int i = i0 + tid;
+    const int v = i < n ? tt.count[i] : 0;
+    const int nc = (v + kTexChunk - 1) / kTexChunk;
+    const int incl = wave_incl_scan(v), incl_c = wave_incl_scan(nc);
+    if (lane == 63) {
+      s_w[0][w] = incl;
+      s_w[1][w] = incl_c;
+    }
+    __syncthreads();
+    int off = s_carry[0], off_c = s_carry[1];
+    for (int k = 0; k < w; ++k) {
+      off += s_w[0][k];
+      off_c += s_w[1][k];
+    }
+    const int ex = off + incl - v, ex_c = off_c + incl_c - nc;
+    if (i < n) {
+      tt.count[i] = ex;
+      tt.cursor[i] = ex;
+      for (int j = 0; j < nc; ++j) {
+        tt.chunk_tile[ex_c + j] = i;
+        tt.chunk_e[ex_c + j] = ex + j * kTexChunk;
+      }
+    }
+    __syncthreads();
+    if (tid == 1023) {
+      s_carry[0] = ex + v;
+      s_carry[1] = ex_c + nc;
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    tt.count[n] = s_carry[0];
+    tt.nchunk[0] = s_carry[1];
+  }
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void kd_tex_tfill(TexArgs<T> a, TexTiles tt) {
+  __shared__ int s_h[kTexMaxTiles];
+  __shared__ int s_base[kTexMaxTiles];
+  const int b = blockIdx.y;
+  const int per = tt.nty * tt.ntx;
+  for (int i = threadIdx.x; i < per; i += kBlock) s_h[i] = 0;
+  __syncthreads();
+  int slot[kTexPer][4];  // rank << 12 | tile, or -1
+#pragma unroll
+  for (int k = 0; k < kTexPer; ++k) {
+    const int64_t n = (int64_t)blockIdx.x * kTexSpan + k * kBlock + threadIdx.x;
+    const bool ok = n < a.N;
+    const int64_t s = (int64_t)b * a.N + (ok ? n : 0);
+    int tiles[4] = {0, 0, 0, 0};
+    const int nt = ok && tex_active(a, s) ? tex_sample_tiles<T, MODE>(a, tt, s, tiles) : 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = wave_key_add(j < nt, tiles[j], s_h);
+      slot[k][j] = j < nt ? (r << 12) | tiles[j] : -1;
+    }
+  }
+  __syncthreads();
+  int *gc = tt.cursor + (int64_t)(a.tex_bstride ? b : 0) * per;
+  for (int i = threadIdx.x; i < per; i += kBlock)
+    if (s_h[i]) s_base[i] = atomicAdd(gc + i, s_h[i]);
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kTexPer; ++k) {
+    const int s = (int)((int64_t)b * a.N + (int64_t)blockIdx.x * kTexSpan + k * kBlock +
+                        threadIdx.x);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (slot[k][j] >= 0) tt.list[s_base[slot[k][j] & 4095] + (slot[k][j] >> 12)] = s;
+  }
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(kBlock) void kd_tex_tacc(TexArgs<T> a, TexTiles tt) {
+  __shared__ T s_acc[kTexAccC * kTexTile * kTexRow];
+  const int per = tt.nty * tt.ntx;
+  const int64_t plane = (int64_t)a.Ht * a.Wt;
+  const int nchunk = tt.nchunk[0];
+  constexpr int kE = kTexChunk / kBlock;
+  constexpr int kTaps = MODE == KD_TEX_NEAREST ? 1 : 4;
+  for (int ch = blockIdx.x; ch < nchunk; ch += gridDim.x) {
+    const int tile = tt.chunk_tile[ch];
+    const int e0 = tt.chunk_e[ch], e1 = min(e0 + kTexChunk, tt.count[tile + 1]);
+    const int tb = tile / per, r = tile - tb * per;
+    const int ty = r / tt.ntx, tx = r - ty * tt.ntx;
+    const int X0 = tx * kTexTile, Y0 = ty * kTexTile;
+    T *gt = a.grad_tex + (int64_t)tb * a.tex_bstride;
+    // kE consecutive entries per thread (adjacent samples), all loads issued before any use
+    int64_t s[kE];
+#pragma unroll
+    for (int q = 0; q < kE; ++q) {
+      const int e = e0 + threadIdx.x * kE + q;
+      s[q] = e < e1 ? tt.list[e] : -1;
+    }
+    for (int c0 = 0; c0 < a.C; c0 += kTexAccC) {
+      const int nc = min(kTexAccC, a.C - c0);
+      for (int i = threadIdx.x; i < nc * kTexTile * kTexRow; i += kBlock) s_acc[i] = (T)0;
+      __syncthreads();
+      // A magnified texture gives runs of adjacent samples in one texel cell: their tap sums
+      // are merged in registers and each run costs kTaps x C LDS atomics (the LDS float atomics
+      // are priced per active lane).
+      int cx = INT_MIN, cy = 0;
+      T acc[kTaps][kTexAccC];
+      auto flush = [&]() {
+        if (cx == INT_MIN) return;
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t) {
+          const int x = cx + (t & 1), y = cy + (t >> 1);
+          const int lx = x - X0, ly = y - Y0;
+          if (x < 0 || x >= a.Wt || y < 0 || y >= a.Ht || lx < 0 || lx >= kTexTile || ly < 0 ||
+              ly >= kTexTile)
+            continue;
+#pragma unroll
+          for (int c = 0; c < kTexAccC; ++c)
+            if (c < nc && acc[t][c] != (T)0)
+              atomicAdd(&s_acc[(c * kTexTile + ly) * kTexRow + lx], acc[t][c]);
+        }
+      };
+#pragma unroll
+      for (int q = 0; q < kE; ++q) {
+        if (s[q] < 0) continue;
+        T ix, iy, mx, my, cu, cv;
+        tex_coord<T>(a.coords + 2 * s[q], ix, iy, mx, my, cu, cv, a.Wt, a.Ht);
+        const T *go = a.grad_out + s[q] * a.C + c0;
+        int x0, y0;
+        T w[kTaps];
+        if (MODE == KD_TEX_NEAREST) {
+          x0 = (int)rint(ix);
+          y0 = (int)rint(iy);
+          w[0] = (T)1;
+        } else {
+          x0 = (int)floor(ix);
+          y0 = (int)floor(iy);
+          const T ex = (T)(x0 + 1) - ix, wx = ix - (T)x0, ey = (T)(y0 + 1) - iy,
+                  wy = iy - (T)y0;
+          w[0] = ex * ey;
+          w[kTaps > 1 ? 1 : 0] = wx * ey;
+          w[kTaps > 2 ? 2 : 0] = ex * wy;
+          w[kTaps > 3 ? 3 : 0] = wx * wy;
+        }
+        if (x0 != cx || y0 != cy) {
+          flush();
+          cx = x0;
+          cy = y0;
+#pragma unroll
+          for (int t = 0; t < kTaps; ++t)
+#pragma unroll
+            for (int c = 0; c < kTexAccC; ++c) acc[t][c] = (T)0;
+        }
+#pragma unroll
+        for (int c = 0; c < kTexAccC; ++c) {
+          if (c >= nc) break;
+          const T g = go[c];
+#pragma unroll
+          for (int t = 0; t < kTaps; ++t) acc[t][c] += w[t] * g;
+        }
+      }
+      flush();
+      __syncthreads();
+      // nonzero sums of the tile (rows of 32 texels: two 128-B segments per wave instruction)
+      for (int i = threadIdx.x; i < nc * kTexTile * kTexTile; i += kBlock) {
+        const int c = i / (kTexTile * kTexTile), q = i - c * kTexTile * kTexTile;
+        const T v = s_acc[(c * kTexTile + q / kTexTile) * kTexRow + q % kTexTile];
+        const int y = Y0 + q / kTexTile, x = X0 + q % kTexTile;
+        if (v != (T)0 && x < a.Wt && y < a.Ht)
+          atomicAdd(gt + (int64_t)(c0 + c) * plane + (int64_t)y * a.Wt + x, v);
+      }
+      __syncthreads();
+    }
+  }
+}
+
 template <typename T>
 __global__ void kd_tex_zero(T *p, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
@@ -331,6 +675,80 @@ static int tex_backward(int B, int64_t N, int C, int Ht, int Wt, const T *coords
   return KD_OK;
 }
 
+static int64_t tex_tiles(int B, int Ht, int Wt, int shared) {
+  return (int64_t)(shared ? 1 : B) * ((Ht + kTexTile - 1) / kTexTile) *
+         ((Wt + kTexTile - 1) / kTexTile);
+}
+static int64_t tex_max_chunks(int B, int64_t N, int Ht, int Wt, int shared) {
+  return tex_tiles(B, Ht, Wt, shared) + (4 * (int64_t)B * N + kTexChunk - 1) / kTexChunk;
+}
+
+size_t tex_tiled_workspace_bytes(int B, int64_t N, int Ht, int Wt, int shared) {
+  return sizeof(int) * (size_t)(2 * tex_tiles(B, Ht, Wt, shared) + 2 +
+                                2 * tex_max_chunks(B, N, Ht, Wt, shared) + 4 * (int64_t)B * N);
+}
+
+template <typename T>
+static int tex_backward_tiled(int B, int64_t N, int C, int Ht, int Wt, const T *coords,
+                              const T *tex, int64_t tex_bstride, int mode, const T *grad_out,
+                              T *grad_tex, T *grad_coords, void *ws, size_t wsb,
+                              hipStream_t stream) {
+  int rc = tex_check<T>(B, N, C, Ht, Wt, mode, tex_bstride);
+  if (rc != KD_OK) return rc;
+  KD_CHECK_ARG(grad_out || (!grad_tex && !grad_coords), "texture_mapping: grad_out is NULL");
+  KD_CHECK_ARG((int64_t)B * N < (1ll << 31) / 4, "texture_mapping: too many samples");
+  TexTiles tt;
+  tt.ntx = (Wt + kTexTile - 1) / kTexTile;
+  tt.nty = (Ht + kTexTile - 1) / kTexTile;
+  tt.ntex = tex_bstride ? B : 1;
+  // textures past kTexMaxTiles tiles: the per-sample-block kernel
+  if ((int64_t)tt.ntx * tt.nty > kTexMaxTiles)
+    return tex_backward<T>(B, N, C, Ht, Wt, coords, tex, tex_bstride, mode, 0, grad_out,
+                           grad_tex, grad_coords, stream);
+  const size_t need = tex_tiled_workspace_bytes(B, N, Ht, Wt, tex_bstride == 0);
+  if (grad_tex && (wsb < need || !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
+  const int ntiles = tt.ntex * tt.nty * tt.ntx;
+  const int64_t mc = tex_max_chunks(B, N, Ht, Wt, tex_bstride == 0);
+  tt.count = (int *)ws;
+  tt.cursor = tt.count + ntiles + 1;
+  tt.nchunk = tt.cursor + ntiles;
+  tt.chunk_tile = tt.nchunk + 1;
+  tt.chunk_e = tt.chunk_tile + mc;
+  tt.list = tt.chunk_e + mc;
+  if (grad_tex) {  // the gradient is added into zeros (all Bt textures)
+    const int64_t nt = (int64_t)tt.ntex * C * Ht * Wt;
+    if (nt > 0 && hipMemsetAsync(grad_tex, 0, sizeof(T) * (size_t)nt, stream) != hipSuccess)
+      return set_error(KD_ERR_LAUNCH, "texture_mapping: memset");
+  }
+  if (B == 0 || N == 0 || C == 0 || (!grad_tex && !grad_coords)) return KD_OK;
+  TexArgs<T> a{N, C, Ht, Wt, coords, tex, tex_bstride, nullptr, grad_out, grad_tex, grad_coords};
+  const dim3 grid((unsigned)((N + kTexSpan - 1) / kTexSpan), (unsigned)B);
+  const unsigned gacc = (unsigned)std::min<int64_t>(mc, kTexAccGrid);
+  ProfScope prof(K_TEX_BWD, stream);
+  if (grad_tex && hipMemsetAsync(tt.count, 0, sizeof(int) * (size_t)(ntiles + 1), stream) !=
+                      hipSuccess)
+    return set_error(KD_ERR_LAUNCH, "texture_mapping: memset");
+#define KD_TEX_LAUNCH(M)                                                                   \
+  do {                                                                                     \
+    hipLaunchKernelGGL((kd_tex_tcount<T, M>), grid, dim3(kBlock), 0, stream, a, tt);       \
+    if (grad_tex) {                                                                        \
+      hipLaunchKernelGGL(kd_tex_tscan, dim3(1), dim3(1024), 0, stream, tt, ntiles);        \
+      hipLaunchKernelGGL((kd_tex_tfill<T, M>), grid, dim3(kBlock), 0, stream, a, tt);      \
+      hipLaunchKernelGGL((kd_tex_tacc<T, M>), dim3(gacc), dim3(kBlock), 0, stream, a, tt); \
+    }                                                                                      \
+  } while (0)
+  if (mode == KD_TEX_NEAREST)
+    KD_TEX_LAUNCH(KD_TEX_NEAREST);
+  else
+    KD_TEX_LAUNCH(KD_TEX_BILINEAR);
+#undef KD_TEX_LAUNCH
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    return set_error(KD_ERR_LAUNCH, "texture_mapping bwd: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
 }  // namespace kd
 
 using namespace kd;
@@ -363,6 +781,31 @@ int kd_texture_mapping_backward_f64(int B, int64_t N, int C, int Ht, int Wt,
                                     double *grad_coords, void *stream) {
   return tex_backward<double>(B, N, C, Ht, Wt, coords, tex, tex_batch_stride, mode, sample_row,
                               grad_out, grad_tex, grad_coords, (hipStream_t)stream);
+}
+
+size_t kd_texture_mapping_backward_workspace_size(int B, int64_t N, int Ht, int Wt,
+                                                  int shared_texture) {
+  if (B < 0 || N < 0 || Ht < 1 || Wt < 1) return 0;
+  return tex_tiled_workspace_bytes(B, N, Ht, Wt, shared_texture);
+}
+int kd_texture_mapping_backward_tiled_f32(int B, int64_t N, int C, int Ht, int Wt,
+                                          const float *coords, const float *tex,
+                                          int64_t tex_batch_stride, int mode,
+                                          const float *grad_out, float *grad_tex,
+                                          float *grad_coords, void *ws, size_t wsb,
+                                          void *stream) {
+  return tex_backward_tiled<float>(B, N, C, Ht, Wt, coords, tex, tex_batch_stride, mode, grad_out,
+                                   grad_tex, grad_coords, ws, wsb, (hipStream_t)stream);
+}
+int kd_texture_mapping_backward_tiled_f64(int B, int64_t N, int C, int Ht, int Wt,
+                                          const double *coords, const double *tex,
+                                          int64_t tex_batch_stride, int mode,
+                                          const double *grad_out, double *grad_tex,
+                                          double *grad_coords, void *ws, size_t wsb,
+                                          void *stream) {
+  return tex_backward_tiled<double>(B, N, C, Ht, Wt, coords, tex, tex_batch_stride, mode,
+                                    grad_out, grad_tex, grad_coords, ws, wsb,
+                                    (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -288,3 +288,39 @@ def test_texture_coherent_uvs_vs_torch(k, mode):
         if mode == 'bilinear':
             gtol = dict(rtol=1e-3, atol=1e-3) if k == 'f32' else dict(rtol=1e-9, atol=1e-9)
             np.testing.assert_allclose(N(gu), ru.numpy(), **gtol)
+
+
+@pytest.mark.parametrize('k', ['f32', 'f64'])
+@pytest.mark.parametrize('mode', MODES)
+def test_texture_tiled_heavy_tiles_and_large_texture(k, mode):
+    """The texel-tile backward's chunking: a magnified region where one 32 x 32 texel tile gets
+    ~40k samples (40 chunks of 1024) next to a spread of samples, and a 2080 x 2080 texture
+    (65 x 65 tiles, past the 4096-tile LDS table: the per-block kernel), against the torch
+    composition."""
+    from kaolin_amd.render.mesh import texture_mapping
+    gen = torch.Generator(device='cpu').manual_seed(13)
+    B = 2
+    hot = 0.30 + 0.02 * torch.rand((B, 40000, 2), generator=gen, dtype=torch.float64)
+    spread = torch.rand((B, 9000, 2), generator=gen, dtype=torch.float64)
+    for hw, uv in ((96, torch.cat([hot, spread], 1)), (2080, spread)):
+        tex = torch.rand((B, 3, hw, hw), generator=gen, dtype=torch.float64)
+        go = torch.rand(uv.shape[:2] + (3,), generator=gen, dtype=torch.float64)
+        u, t = uv.to(DEV, DT[k]).requires_grad_(True), tex.to(DEV, DT[k]).requires_grad_(True)
+        gu, gt = torch.autograd.grad(texture_mapping(u, t, mode=mode), [u, t], go.to(DEV, DT[k]))
+        # the reference in the same dtype (f32 uvs round to texels on their own)
+        u2 = uv.to(DEV, DT[k]).requires_grad_(True)
+        t2 = tex.to(DEV, DT[k]).requires_grad_(True)
+        ref = torch_texture_mapping(u2, t2, mode)
+        ru, rt = torch.autograd.grad(ref, [u2, t2], go.to(DEV, DT[k]), allow_unused=True)
+        # f32: bilinear weights come from ix = ((g + 1) W - 1) / 2, whose ulp grows with the
+        # texture width (~1.2e-4 at 2080); torch's kernel may contract it differently
+        scale = float(rt.abs().max())
+        tol = (dict(rtol=1e-4, atol=1e-5 * scale + 8 * hw * 2.0 ** -23) if k == 'f32'
+               else dict(rtol=1e-10, atol=1e-11 * scale))
+        np.testing.assert_allclose(N(gt), N(rt), **tol)
+        if mode == 'bilinear':
+            # the coordinate gradient carries a factor W / 2 (1040 at 2080 texels)
+            su = float(ru.abs().max())
+            gtol = (dict(rtol=1e-3, atol=2e-3 + 1e-4 * su) if k == 'f32'
+                    else dict(rtol=1e-9, atol=1e-9 + 1e-12 * su))
+            np.testing.assert_allclose(N(gu), N(ru), **gtol)
