@@ -124,7 +124,7 @@ def soup(B, F, P, dt, seed, size=1.2, nan_faces=0):
 
 
 @pytest.mark.parametrize('dt', [np.float32, np.float64])
-@pytest.mark.parametrize('knum', [1, 20, 300])
+@pytest.mark.parametrize('knum', [1, 20, 64, 300])
 def test_dense_soup_vs_oracle(dt, knum):
     if knum <= 20:
         px, rr, fvz, fvi, feat = soup(2, 3000, 700, dt, knum, nan_faces=5)
