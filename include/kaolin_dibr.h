@@ -431,7 +431,8 @@ int kd_texture_mapping_backward_f64(int batch, int64_t num_samples, int channels
  * incoming gradient are listed per tile their taps touch (LDS-aggregated counting pass, scan,
  * fill), each tile's list is cut into chunks of 1024 entries, and each chunk's taps are summed in
  * LDS and added to the zeroed texture gradient as row-contiguous atomics.  Independent of the uv
- * layout (the per-block kernel above has an unbounded texel window at uv seams and poles);
+ * layout (the per-block kernel above has an unbounded texel window at uv seams and poles, but is
+ * faster on rendered uvs and is the one texture_mapping runs);
  * textures of more than 4096 tiles (2048 x 2048) run the per-block kernel.  Same results up to
  * float summation order.  Workspace: kd_texture_mapping_backward_workspace_size
  * (shared_texture = tex_batch_stride == 0). */

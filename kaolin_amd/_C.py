@@ -628,13 +628,12 @@ def texture_mapping_backward(grad_out, coords, tex, mode, need_coords=True, need
     gt = None
     if need_tex:
         gt = torch.empty(tex.shape, device=dev, dtype=tex.dtype)
-    # texel-tile backward (kd_texture_mapping_backward_tiled): the samples listed per 32 x 32
-    # texel tile in the workspace, summed per 1024-entry chunk in LDS
-    nb = _lib.texture_backward_workspace_size(B, N, Ht, Wt, bs == 0)
-    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev) if need_tex else None
-    _lib.call(f'kd_texture_mapping_backward_tiled_{sfx}', B, N, C, Ht, Wt, _ptr(coords),
-              _ptr(tex_c), bs, _TEX_MODES[mode], _ptr(go), _ptr(gt), _ptr(gc), _ptr(ws),
-              nb if need_tex else 0, _stream(dev))
+    # per-block backward: dense (B, h, w, 2) coordinates as 16 x 16 sample blocks, runs of
+    # same-cell samples summed across the lanes of a row (DPP), LDS texel sums (kd_tex_bwd);
+    # faster than the texel-tile lists (kd_texture_mapping_backward_tiled) on the C3 render
+    row = coords.shape[2] if coords.dim() == 4 else 0  # dense (B, h, w, 2): 16 x 16 blocks
+    _lib.call(f'kd_texture_mapping_backward_{sfx}', B, N, C, Ht, Wt, _ptr(coords), _ptr(tex_c),
+              bs, _TEX_MODES[mode], row, _ptr(go), _ptr(gt), _ptr(gc), _stream(dev))
     return gc, gt
 
 

@@ -141,6 +141,71 @@ __device__ __forceinline__ int wg_min_max(int lo, int hi, int *s, int &hi_out) {
   return lo;
 }
 
+// DPP within 16-lane rows (row_shr:n = 0x110 + n, row_shl:1 = 0x101); lanes whose source is
+// outside their row read `old`.
+template <int CTRL>
+__device__ __forceinline__ int tex_dpp(int old, int x) {
+  return __builtin_amdgcn_update_dpp(old, x, CTRL, 0xf, 0xf, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float tex_dpp_v(float x) {
+  return __int_as_float(tex_dpp<CTRL>(0, __float_as_int(x)));
+}
+template <int CTRL>
+__device__ __forceinline__ double tex_dpp_v(double x) {
+  const long long u = __double_as_longlong(x);
+  const int lo = tex_dpp<CTRL>(0, (int)u), hi = tex_dpp<CTRL>(0, (int)(u >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// Runs of equal keys along each 16-lane row: take[k] says whether step k (distance 2^k) of the
+// segmented scan adds its source (the flag recurrence of a segmented Hillis-Steele scan, so
+// keys that recur after another key never merge); tail marks each run's last lane.
+__device__ __forceinline__ void tex_runs16(int key, bool take[4], bool &tail) {
+  int prev = tex_dpp<0x111>(INT_MIN, key), next = tex_dpp<0x101>(INT_MIN, key);
+  asm volatile("" : "+v"(prev), "+v"(next));
+  int flag = prev != key;  // run head (a row start reads INT_MIN)
+  take[0] = !flag;
+  int f1 = tex_dpp<0x111>(1, flag);
+  asm volatile("" : "+v"(f1));
+  flag |= f1;
+  take[1] = !flag;
+  int f2 = tex_dpp<0x112>(1, flag);
+  asm volatile("" : "+v"(f2));
+  flag |= f2;
+  take[2] = !flag;
+  int f4 = tex_dpp<0x114>(1, flag);
+  asm volatile("" : "+v"(f4));
+  flag |= f4;
+  take[3] = !flag;
+  tail = next != key;
+}
+
+// One step of the segmented sum.  The DPP read must run on every lane: left as
+// `take ? dpp(x) : 0` the compiler may issue it under the `take` lanes only, and a source lane
+// outside EXEC reads `old` (0) -- partial sums silently dropped.  The empty asm pins the read
+// at this point, where the whole wave is active.
+template <int CTRL, typename T>
+__device__ __forceinline__ T tex_seg_step(bool take, T x) {
+  T o = tex_dpp_v<CTRL>(x);
+  asm volatile("" : "+v"(o));
+  return x + (take ? o : (T)0);
+}
+
+// inclusive segmented sums of v over the runs of tex_runs16 (every lane of the wave active)
+template <typename T, int N>
+__device__ __forceinline__ void tex_seg_sum16(const bool take[4], T v[N]) {
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+    T x = v[t];
+    x = tex_seg_step<0x111>(take[0], x);
+    x = tex_seg_step<0x112>(take[1], x);
+    x = tex_seg_step<0x114>(take[2], x);
+    x = tex_seg_step<0x118>(take[3], x);
+    v[t] = x;
+  }
+}
+
 // Backward.  The texture gradient of a sample block is summed in LDS over the block's texel
 // footprint (neighbouring samples hit the same texels; same-address global atomics serialise in
 // L2) and flushed with one global atomic per touched texel and channel.  A footprint too large for
@@ -175,6 +240,7 @@ __global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) 
     wy = iy - (T)y0;
   }
   constexpr int kExt = MODE == KD_TEX_NEAREST ? 0 : 1;
+  constexpr int kTaps = MODE == KD_TEX_NEAREST ? 1 : 4;
   bool act = false;
   if (ok && gt)
     for (int c = 0; c < a.C; ++c) act |= go[c] != (T)0;
@@ -195,55 +261,65 @@ __global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) 
     else
       atomicAdd(gt + c * plane + (int64_t)y * a.Wt + x, v);
   };
+  // Adjacent samples of a row (the 16 lanes of a DPP row: one row of the 16 x 16 block) often
+  // share their texel cell when the texture is magnified: their tap values are summed over each
+  // run of equal cells by a segmented scan and only the run's last lane adds them (the LDS float
+  // atomics are priced per active lane).
+  bool take[4], tail;
+  tex_runs16(act ? y0 * a.Wt + x0 : -1, take, tail);
   T gix = (T)0, giy = (T)0;
-  if (ok) {
-    const T *tex = a.tex + (int64_t)b * a.tex_bstride;
-    const bool vx0 = x0 >= 0 && x0 < a.Wt, vx1 = x0 + 1 >= 0 && x0 + 1 < a.Wt;
-    const bool vy0 = y0 >= 0 && y0 < a.Ht, vy1 = y0 + 1 >= 0 && y0 + 1 < a.Ht;
-    const T *t0 = tex + (int64_t)y0 * a.Wt + x0;
-    for (int c = 0; c < a.C; ++c) {
-      const T g = go[c];
-      if (act && g != (T)0) {
-        if (MODE == KD_TEX_NEAREST) {
-          add(c, x0, y0, g);
-        } else {
-          add(c, x0, y0, ex * ey * g);
-          add(c, x0 + 1, y0, wx * ey * g);
-          add(c, x0, y0 + 1, ex * wy * g);
-          add(c, x0 + 1, y0 + 1, wx * wy * g);
-        }
+  const T *tex = a.tex + (int64_t)b * a.tex_bstride;
+  const bool vx0 = x0 >= 0 && x0 < a.Wt, vx1 = x0 + 1 >= 0 && x0 + 1 < a.Wt;
+  const bool vy0 = y0 >= 0 && y0 < a.Ht, vy1 = y0 + 1 >= 0 && y0 + 1 < a.Ht;
+  const T *t0 = tex + (int64_t)y0 * a.Wt + x0;
+  for (int c = 0; c < a.C; ++c) {
+    const T g = ok ? go[c] : (T)0;
+    if (gt) {  // uniform
+      T v[kTaps];
+      if (MODE == KD_TEX_NEAREST) {
+        v[0] = act ? g : (T)0;
+      } else {
+        v[0] = act ? ex * ey * g : (T)0;
+        v[kTaps > 1 ? 1 : 0] = act ? wx * ey * g : (T)0;
+        v[kTaps > 2 ? 2 : 0] = act ? ex * wy * g : (T)0;
+        v[kTaps > 3 ? 3 : 0] = act ? wx * wy * g : (T)0;
       }
-      if (MODE == KD_TEX_BILINEAR && a.grad_coords) {
-        const T *tc = t0 + c * plane;
-        if (vy0 && vx0) {
-          const T v = tc[0];
-          gix -= v * ey * g;
-          giy -= v * ex * g;
-        }
-        if (vy0 && vx1) {
-          const T v = tc[1];
-          gix += v * ey * g;
-          giy -= v * wx * g;
-        }
-        if (vy1 && vx0) {
-          const T v = tc[a.Wt];
-          gix -= v * wy * g;
-          giy += v * ex * g;
-        }
-        if (vy1 && vx1) {
-          const T v = tc[a.Wt + 1];
-          gix += v * wy * g;
-          giy += v * wx * g;
-        }
+      tex_seg_sum16<T, kTaps>(take, v);
+      if (tail && act) {
+#pragma unroll
+        for (int t = 0; t < kTaps; ++t)
+          if (v[t] != (T)0) add(c, x0 + (t & 1), y0 + (t >> 1), v[t]);
       }
     }
-    if (a.grad_coords) {
-      // nearest sampling has no coordinate gradient; bilinear: grid gradient -> [-1, 1] coords
-      // (x mx, y my) -> y flip and * 2 -> clamp mask
-      a.grad_coords[2 * s] = MODE == KD_TEX_BILINEAR && cu != (T)0 ? (mx * gix) * (T)2 : (T)0;
-      a.grad_coords[2 * s + 1] =
-          MODE == KD_TEX_BILINEAR && cv != (T)0 ? -(my * giy) * (T)2 : (T)0;
+    if (ok && MODE == KD_TEX_BILINEAR && a.grad_coords) {
+      const T *tc = t0 + c * plane;
+      if (vy0 && vx0) {
+        const T v = tc[0];
+        gix -= v * ey * g;
+        giy -= v * ex * g;
+      }
+      if (vy0 && vx1) {
+        const T v = tc[1];
+        gix += v * ey * g;
+        giy -= v * wx * g;
+      }
+      if (vy1 && vx0) {
+        const T v = tc[a.Wt];
+        gix -= v * wy * g;
+        giy += v * ex * g;
+      }
+      if (vy1 && vx1) {
+        const T v = tc[a.Wt + 1];
+        gix += v * wy * g;
+        giy += v * wx * g;
+      }
     }
+  }
+  if (ok && a.grad_coords) {
+    // nearest sampling has no coordinate gradient; bilinear: grid gradient -> [-1, 1] coords
+    // (x mx, y my) -> y flip and * 2 -> clamp mask
+    a.grad_coords[2 * s] = MODE == KD_TEX_BILINEAR && cu != (T)0 ? (mx * gix) * (T)2 : (T)0;
+    a.grad_coords[2 * s + 1] = MODE == KD_TEX_BILINEAR && cv != (T)0 ? -(my * giy) * (T)2 : (T)0;
   }
   if (!lds) return;
   __syncthreads();

@@ -324,3 +324,38 @@ def test_texture_tiled_heavy_tiles_and_large_texture(k, mode):
             gtol = (dict(rtol=1e-3, atol=2e-3 + 1e-4 * su) if k == 'f32'
                     else dict(rtol=1e-9, atol=1e-9 + 1e-12 * su))
             np.testing.assert_allclose(N(gu), N(ru), **gtol)
+
+
+@pytest.mark.parametrize('k', ['f32', 'f64'])
+@pytest.mark.parametrize('mode', MODES)
+def test_texture_tiled_abi_matches_block(k, mode):
+    """kd_texture_mapping_backward_tiled_* (the texel-tile lists; texture_mapping itself runs the
+    per-block kernel) called through the C ABI against the product's backward: a magnified
+    region of ~40k samples in one tile next to spread samples, per-view and shared textures."""
+    from kaolin_amd import _C, _lib
+    gen = torch.Generator(device='cpu').manual_seed(17)
+    B, C, hw = 2, 3, 96
+    uv = torch.cat([0.30 + 0.02 * torch.rand((B, 40000, 2), generator=gen, dtype=torch.float64),
+                    torch.rand((B, 9000, 2), generator=gen, dtype=torch.float64) * 1.1 - 0.05], 1)
+    go = torch.rand(uv.shape[:2] + (C,), generator=gen, dtype=torch.float64)
+    go[:, ::7] = 0.0  # samples with a zero incoming gradient are not listed
+    for tb in (B, 1):
+        tex = torch.rand((tb, C, hw, hw), generator=gen, dtype=torch.float64).to(DEV, DT[k])
+        u, g_ = uv.to(DEV, DT[k]).contiguous(), go.to(DEV, DT[k]).contiguous()
+        gc_ref, gt_ref = _C.texture_mapping_backward(g_, u, tex, mode)
+        N_ = u.shape[1]
+        bs = 0 if tb == 1 else C * hw * hw
+        nb = _lib.texture_backward_workspace_size(B, N_, hw, hw, tb == 1)
+        ws = torch.empty((nb,), dtype=torch.uint8, device=DEV)
+        gt = torch.empty((tb, C, hw, hw), dtype=DT[k], device=DEV)
+        gc = torch.empty_like(u)
+        _lib.call(f'kd_texture_mapping_backward_tiled_{k}', B, N_, C, hw, hw, u.data_ptr(),
+                  tex.data_ptr(), bs, {'nearest': 0, 'bilinear': 1}[mode], g_.data_ptr(),
+                  gt.data_ptr(), gc.data_ptr(), ws.data_ptr(), nb,
+                  torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        scale = float(gt_ref.abs().max())
+        tol = dict(rtol=1e-4, atol=1e-5 * scale) if k == 'f32' else dict(rtol=1e-10,
+                                                                          atol=1e-11 * scale)
+        np.testing.assert_allclose(N(gt), N(gt_ref), **tol)
+        np.testing.assert_array_equal(N(gc), N(gc_ref))
