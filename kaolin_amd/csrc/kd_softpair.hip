@@ -739,14 +739,19 @@ __device__ __forceinline__ void soft_add_pair(T g[6], int et, double sp, const S
 // record costs the same, so the grid is balanced however the records fall on the tiles.
 // One step of a segmented inclusive wave scan with DPP (no LDS): lanes add the DPP source lane's
 // six sums when it belongs to the same segment (invalid sources read segment -1).
+// The DPP reads are pinned with an empty asm where the whole wave is active: left inside the
+// select, the compiler may issue them under the `take` lanes only, and a source lane outside
+// EXEC reads the `old` operand (0).
 template <int CTRL, int ROWS>
 __device__ __forceinline__ void seg_scan_dpp(int seg, float g[6]) {
-  const int os = __builtin_amdgcn_update_dpp(-1, seg, CTRL, ROWS, 0xf, false);
+  int os = __builtin_amdgcn_update_dpp(-1, seg, CTRL, ROWS, 0xf, false);
+  asm volatile("" : "+v"(os));
   const bool take = os == seg;
 #pragma unroll
   for (int q = 0; q < 6; ++q) {
-    const float o = __int_as_float(
+    float o = __int_as_float(
         __builtin_amdgcn_update_dpp(0, __float_as_int(g[q]), CTRL, ROWS, 0xf, false));
+    asm volatile("" : "+v"(o));
     g[q] += take ? o : 0.f;
   }
 }
