@@ -71,6 +71,31 @@ __device__ __forceinline__ void tex_coord(const T *c, T &ix, T &iy, T &mx, T &my
   iy = tex_source<T>(gy, Ht, my);
 }
 
+// The two horizontal taps (x, x + 1) of one texture row: one 2-element load (element-aligned:
+// the hardware needs dword alignment only) when x + 1 is in the row, else the first alone.
+typedef float kd_f2u __attribute__((ext_vector_type(2), aligned(4)));
+typedef double kd_d2u __attribute__((ext_vector_type(2), aligned(8)));
+__device__ __forceinline__ void tex_pair(const float *p, bool both, float &v0, float &v1) {
+  if (both) {
+    const kd_f2u v = *reinterpret_cast<const kd_f2u *>(p);
+    v0 = v.x;
+    v1 = v.y;
+  } else {
+    v0 = p[0];
+    v1 = 0.f;
+  }
+}
+__device__ __forceinline__ void tex_pair(const double *p, bool both, double &v0, double &v1) {
+  if (both) {
+    const kd_d2u v = *reinterpret_cast<const kd_d2u *>(p);
+    v0 = v.x;
+    v1 = v.y;
+  } else {
+    v0 = p[0];
+    v1 = 0.0;
+  }
+}
+
 template <typename T, int MODE>
 __global__ __launch_bounds__(kBlock) void kd_tex_fwd(TexArgs<T> a) {
   const int b = blockIdx.y;
@@ -95,13 +120,17 @@ __global__ __launch_bounds__(kBlock) void kd_tex_fwd(TexArgs<T> a) {
     const bool vx0 = x0 >= 0 && x0 < a.Wt, vx1 = x1 >= 0 && x1 < a.Wt;
     const bool vy0 = y0 >= 0 && y0 < a.Ht, vy1 = y1 >= 0 && y1 < a.Ht;
     const T *t = tex + (int64_t)y0 * a.Wt + x0;
+    // ix, iy are clipped to the texture: x0, y0 are in range, x1 / y1 at most one past it
     for (int c = 0; c < a.C; ++c) {
       const T *tc = t + c * plane;
+      T nw, ne, sw = (T)0, se = (T)0;
+      tex_pair(tc, vx1, nw, ne);
+      if (vy1) tex_pair(tc + a.Wt, vx1, sw, se);
       T acc = (T)0;
-      if (vy0 && vx0) acc = acc + tc[0] * wnw;
-      if (vy0 && vx1) acc = acc + tc[1] * wne;
-      if (vy1 && vx0) acc = acc + tc[a.Wt] * wsw;
-      if (vy1 && vx1) acc = acc + tc[a.Wt + 1] * wse;
+      if (vy0 && vx0) acc = acc + nw * wnw;
+      if (vy0 && vx1) acc = acc + ne * wne;
+      if (vy1 && vx0) acc = acc + sw * wsw;
+      if (vy1 && vx1) acc = acc + se * wse;
       out[c] = acc;
     }
   }
@@ -292,26 +321,26 @@ __global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) 
       }
     }
     if (ok && MODE == KD_TEX_BILINEAR && a.grad_coords) {
+      // x0, y0 are in range (ix, iy clipped); x0 + 1 / y0 + 1 at most one past it
       const T *tc = t0 + c * plane;
+      T nw, ne, sw = (T)0, se = (T)0;
+      tex_pair(tc, vx1, nw, ne);
+      if (vy1) tex_pair(tc + a.Wt, vx1, sw, se);
       if (vy0 && vx0) {
-        const T v = tc[0];
-        gix -= v * ey * g;
-        giy -= v * ex * g;
+        gix -= nw * ey * g;
+        giy -= nw * ex * g;
       }
       if (vy0 && vx1) {
-        const T v = tc[1];
-        gix += v * ey * g;
-        giy -= v * wx * g;
+        gix += ne * ey * g;
+        giy -= ne * wx * g;
       }
       if (vy1 && vx0) {
-        const T v = tc[a.Wt];
-        gix -= v * wy * g;
-        giy += v * ex * g;
+        gix -= sw * wy * g;
+        giy += sw * ex * g;
       }
       if (vy1 && vx1) {
-        const T v = tc[a.Wt + 1];
-        gix += v * wy * g;
-        giy += v * wx * g;
+        gix += se * wy * g;
+        giy += se * wx * g;
       }
     }
   }
