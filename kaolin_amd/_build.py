@@ -33,6 +33,12 @@ FLAGS = ['-O3', '-std=c++17', '-fPIC', '-ffp-contract=off', f'--offload-arch={AR
          '-mllvm', '-disable-promote-alloca-to-lds',
          '-Wall', '-Wno-unused-function', '-Wno-unused-result']
 
+# per-source flags, each measured on one box against the default scheduler (tools/ab_variant.sh +
+# tools/rocprof_flags.sh, alternating runs): the ILP scheduler takes kd_bin_count from 20.7 to
+# 18.7-19.2 us at C3 and leaves the scan / scatter unchanged; on the tile kernels it changes
+# nothing (kd_dibr_fwd_tiles) or loses (kd_dibr_bwd +2.7 us)
+SOURCE_FLAGS = {'kd_binning.hip': ['-mllvm', '-amdgpu-sched-strategy=max-ilp']}
+
 
 def _stale(target, deps):
     if not os.path.exists(target):
@@ -48,7 +54,7 @@ def _compile(src, diag=False):
         [os.path.join(CSRC, h) for h in HEADERS]
     if _stale(obj, deps):
         lang = ['-x', 'hip'] if src.endswith('.cpp') else []
-        extra = ['-DKD_DIAG=1'] if diag else []
+        extra = (['-DKD_DIAG=1'] if diag else []) + SOURCE_FLAGS.get(src, [])
         cmd = [HIPCC, *FLAGS, *extra, *lang, '-c', path, '-o', obj + '.tmp']
         subprocess.check_call(cmd)
         os.replace(obj + '.tmp', obj)
