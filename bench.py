@@ -38,6 +38,9 @@ from kaolin_amd.render.mesh import dibr, dibr_rasterization  # noqa: E402
 
 METRIC = 'Mpixels/s DIB-R fwd+bwd, 50k-face mesh @512² bs=8, 1/2/4/8 GPU'
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue roof: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles
+# (MI355X_MICROARCH.md issue-cost table: v_add_f32 / v_fma_f32 4 cycles) at the 2.4 GHz peak clock
+VALU_SIMDS, VALU_CYCLES, CLOCK_HZ = 1024, 4, 2.4e9
 
 # name -> (n_lon, n_lat, H, W, global batch, elevation); SURVEY.md §8(d) configs C2-C5
 CONFIGS = {
@@ -236,7 +239,8 @@ def load_pmc(path, config, dtype, lists, views):
     out = {}
     for k, ent in pm.get('kernels', {}).items():
         if 'FETCH_SIZE_KiB' in ent and 'WRITE_SIZE_KiB' in ent:
-            out[k] = round((2 * ent['FETCH_SIZE_KiB'] + ent['WRITE_SIZE_KiB']) * 1024)
+            out[k] = {'traffic': round((2 * ent['FETCH_SIZE_KiB'] + ent['WRITE_SIZE_KiB']) * 1024),
+                      'valu': ent.get('SQ_INSTS_VALU'), 'salu': ent.get('SQ_INSTS_SALU')}
     return out, os.path.relpath(path, ROOT)
 
 
@@ -262,7 +266,7 @@ def main():
     ap.add_argument('--no-weak', action='store_true', help='skip the N > 1 weak-scaling phase')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--pmc', default=None,
-                    help='PMC traffic summary (default profiles/r02/pmc_traffic_<config>.json)')
+                    help='PMC traffic summary (default profiles/r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
 
     # KD_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (ranks share cuda:0;
@@ -332,9 +336,13 @@ def main():
                 torch.cuda.current_stream(dev).cuda_stream))
             del ws
     fused = 'kd_soft_pair_math' not in prof  # the one-launch soft mask (kd_softpair.hip)
-    pmc_path = args.pmc or os.path.join(ROOT, 'profiles', 'r02',
-                                        f'pmc_traffic_{args.config}.json')
-    pmc, pmc_src = load_pmc(pmc_path, args.config, args.dtype, args.lists, n)
+    pmc, pmc_src = {}, None
+    for rnd in ([args.pmc] if args.pmc else ['r03', 'r02']):  # the newest committed summary
+        pmc_path = rnd if args.pmc else os.path.join(ROOT, 'profiles', rnd,
+                                                       f'pmc_traffic_{args.config}.json')
+        pmc, pmc_src = load_pmc(pmc_path, args.config, args.dtype, args.lists, n)
+        if pmc:
+            break
     kernels = {}
     moved = 0
     for name, (ms, cnt) in prof.items():
@@ -348,9 +356,12 @@ def main():
             kernels[name]['GB_s'] = round(ab / (avg_us * 1e-6) / 1e9, 1)
             moved += ab * cnt / args.steps
         if name in pmc:
-            kernels[name]['traffic'] = pmc[name]
+            kernels[name]['traffic'] = pmc[name]['traffic']
             if ab:
-                kernels[name]['traffic_ratio'] = round(pmc[name] / ab, 3)
+                kernels[name]['traffic_ratio'] = round(pmc[name]['traffic'] / ab, 3)
+            if pmc[name]['valu']:
+                kernels[name]['valu_issue_frac'] = round(
+                    pmc[name]['valu'] * VALU_CYCLES / (VALU_SIMDS * CLOCK_HZ) / (avg_us * 1e-6), 3)
     dom = max(prof.items(), key=lambda kv: kv[1][0])[0] if prof else None
     roofline = None
     if dom is not None:
@@ -358,14 +369,28 @@ def main():
         avg_s = ms / cnt / 1e3
         ab = kernels[dom].get('alg_bytes')
         achieved = ab / avg_s / 1e9 if ab else None
-        traffic = pmc.get(dom)
-        roofline = {'kernel': dom, 'bound': 'hbm',
+        traffic = pmc[dom]['traffic'] if dom in pmc else None
+        hbm_frac = None if achieved is None else achieved / HBM_PEAK_GBS
+        valu = None
+        if dom in pmc and pmc[dom]['valu']:
+            issue_s = pmc[dom]['valu'] * VALU_CYCLES / (VALU_SIMDS * CLOCK_HZ)
+            valu = {'insts_per_launch': round(pmc[dom]['valu']),
+                    'salu_insts_per_launch': round(pmc[dom]['salu'] or 0),
+                    'issue_us': round(issue_s * 1e6, 2), 'frac': round(issue_s / avg_s, 4),
+                    'roof': f'{VALU_SIMDS} SIMDs x 1 wave64 VALU instruction per {VALU_CYCLES} '
+                            f'cycles at {CLOCK_HZ / 1e9:g} GHz',
+                    'source': f'{pmc_src}: SQ_INSTS_VALU per launch'}
+        # the bound is the larger of the two roof fractions (the HBM figures stay the
+        # contract's achieved / peak / frac)
+        bound = 'valu' if valu and hbm_frac is not None and valu['frac'] > hbm_frac else 'hbm'
+        roofline = {'kernel': dom, 'bound': bound,
                     'achieved': None if achieved is None else round(achieved, 1),
                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                    'frac': None if achieved is None else round(achieved / HBM_PEAK_GBS, 4),
+                    'frac': None if hbm_frac is None else round(hbm_frac, 4),
                     'traffic': traffic,
                     'traffic_ratio': round(traffic / ab, 3) if traffic and ab else None,
                     'traffic_source': pmc_src and f'{pmc_src}: FETCH_SIZE x 2 + WRITE_SIZE',
+                    'valu_issue': valu,
                     'alg_bytes_per_launch': ab, 'avg_launch_us': round(avg_s * 1e6, 2)}
     ref_bytes = survey_step_bytes(P, Ftot, wl.D, args.knum, esize)
     step_roof = {
@@ -439,7 +464,10 @@ def cpu_baseline(wl, fvz, fvi, nz, runs=5):
     first view, fwd+bwd (all threads); rows 3/8..5/8 of it (one thread)."""
     import numpy as np
     import oracle
-    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or os.cpu_count()
+    # the GPU box gives each GPU a 16-CPU share and sets OMP_NUM_THREADS to it (os.cpu_count()
+    # shows the whole host); without that variable, every CPU this process may run on
+    affinity = len(os.sched_getaffinity(0))
+    threads = int(os.environ.get('OMP_NUM_THREADS', '0')) or affinity
     H, W, kw = wl.H, wl.W, wl.kw
     n = lambda t: np.ascontiguousarray(t[:1].detach().cpu().numpy())  # noqa: E731
     fvz_, fvi_, nz_, ft_ = n(fvz), n(fvi), n(nz), n(wl.feats)
@@ -476,7 +504,12 @@ def cpu_baseline(wl, fvz, fvi, nz, runs=5):
                               'sample': f'rows {r0}..{r1 - 1} of the same view, 1 thread, '
                                         f'median of {runs} after 1 warmup = {med1:.3f} s'},
             'host': {'lscpu_model': _cpu_model(), 'nproc': os.cpu_count(),
-                     'omp_num_threads': os.environ.get('OMP_NUM_THREADS')}}
+                     'affinity_cpus': affinity,
+                     'omp_num_threads': os.environ.get('OMP_NUM_THREADS')},
+            'cores_reason': ('OMP_NUM_THREADS: the GPU box\'s CPU share per GPU (the pool sets it '
+                             'to 16; nproc shows every CPU of the host, which other GPUs\' jobs '
+                             'share)') if os.environ.get('OMP_NUM_THREADS') else
+                            'every CPU in this process\'s affinity mask'}
 
 
 if __name__ == '__main__':

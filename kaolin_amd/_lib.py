@@ -179,6 +179,12 @@ def pool_limits_active():
     return _pool_limited
 
 
+def split_soft_mask_forced():
+    """True when a diagnostic flag (KD_DEBUG_FLAGS bit 4096) forces the split soft-mask
+    pipeline, which the fused mask_iou cannot use."""
+    return bool(int(os.environ.get('KD_DEBUG_FLAGS', '0'), 0) & 4096)
+
+
 def profile_enable(on=True):
     """Record HIP events around every library launch (see kd_profile_enable)."""
     load().kd_profile_enable(1 if on else 0)

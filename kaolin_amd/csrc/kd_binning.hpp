@@ -81,6 +81,7 @@ __device__ __forceinline__ const int *bin_list(const BinBuffers &bb, int b, int 
 // hook that forces the overflow paths).  The workspace layout never depends on them.
 float pool_limit_bins();
 float pool_limit_pairs();
+bool pool_limits_ever_set();  // kd_set_pool_limits has held a pool below 1 in this process
 
 size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view);
 // Carves the buffers from `ws` starting at *offset (advanced past them).

@@ -19,6 +19,8 @@ std::atomic<long long *> g_tbuf{nullptr};
 std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
 float pool_limit_bins() { return g_lim_bins.load(); }
 float pool_limit_pairs() { return g_lim_pairs.load(); }
+std::atomic<bool> g_lim_ever{false};
+bool pool_limits_ever_set() { return g_lim_ever.load(); }
 long long *debug_tile_buffer() {
   return (KD_DIAG && (g_debug.load() & 64)) ? g_tbuf.load() : nullptr;
 }
@@ -85,6 +87,7 @@ int kd_set_pool_limits(double bins, double pairs) {
     return kd::set_error(KD_ERR_INVALID_ARGUMENT, "pool limits must be in [0, 1]");
   kd::g_lim_bins.store((float)bins);
   kd::g_lim_pairs.store((float)pairs);
+  if (bins < 1.0 || pairs < 1.0) kd::g_lim_ever.store(true);
   return KD_OK;
 }
 

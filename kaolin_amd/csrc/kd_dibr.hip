@@ -90,7 +90,8 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   KD_CHECK_ARG(!iou.gt || (iou.loss && iou.stats && iou.acc), "mask_iou: NULL output");
-  KD_CHECK_ARG(!iou.gt || (K <= kFuseSlots && pool_limit_pairs() >= 1.f),
+  KD_CHECK_ARG(!iou.gt || (K <= kFuseSlots && pool_limit_pairs() >= 1.f &&
+                            !(debug_flags() & 4096)),
                "fused mask_iou needs knum <= 32 (the one-launch soft mask)");
   const int64_t nf = (int64_t)B * F;
   if (!want_grad) gz_fvi = gz_feat = nullptr;

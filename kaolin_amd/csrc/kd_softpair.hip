@@ -22,7 +22,7 @@
 //                      (kd_raster_pairs.hpp) and then the FUSED soft mask of the same tile.
 //   kd_dibr_bwd        dibr_rasterization's backward: the raster backward's tiles
 //                      (kd_raster_bwd.hpp) and the soft items in one grid.
-// Pool overflow (tiles reserving more than the pool's min(knum, 24) records per pixel, or
+// Pool overflow (tiles reserving more than the pool's min(knum, 32) records per pixel, or
 // kd_set_pool_limits): the tile writes no records; kd_soft_ovf_fwd runs its walk again, each
 // pixel lane computing its pairs' probabilities in slot order and the product directly
 // ("streaming": the reference's per-pixel loop over the tile's face list), so the soft mask is
@@ -939,9 +939,13 @@ __global__ __launch_bounds__(kBlock) void kd_dibr_bwd(SoftArgs<T> a, SoftPairBuf
 constexpr unsigned kOvfBlocks = 256;  // grid of the overflow kernels (exit at once when unused)
 
 // Whether a tile can find the pool exhausted: never with knum <= 32 (the pool holds 32 records
-// per pixel) unless a test limits the pool; the overflow kernels are launched only then.  The
-// limits must stay the same from a forward to its backward.
-static bool pool_may_overflow(int K) { return K > kPoolPairsPerPixel || pool_limit_pairs() < 1.f; }
+// per pixel) unless a test limits the pool; the overflow kernels are launched only then.  Once a
+// limit has been set in this process (pool_limits_ever_set, the test hook), they are launched
+// for every later call too -- they exit at once when no tile overflowed -- so a backward that
+// runs after the limits were restored (a retained graph) still sees its forward's overflows.
+static bool pool_may_overflow(int K) {
+  return K > kPoolPairsPerPixel || pool_limit_pairs() < 1.f || pool_limits_ever_set();
+}
 
 template <typename T, bool FUSED>
 static void ovf_fwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipStream_t stream) {

@@ -70,24 +70,45 @@ def allreduce_grads_(tensors, group=None):
 class EarlyReduce:
     """Overlap for shared parameters whose gradients are final before the end of the backward
     (e.g. a texture, whose gradient comes out of texture_mapping's backward before the DIB-R
-    backward runs): a post-accumulate hook starts their all-reduce asynchronously as soon as
-    autograd has written it, so the collective runs on RCCL's stream while the rest of the
-    backward runs on the compute stream.  ``wait()`` joins them.  The vertex gradient (the last
+    backward runs): a post-accumulate hook marks a parameter ready as soon as autograd has
+    written its gradient, and the asynchronous all-reduces are issued in the FIXED order of
+    `params` (a parameter starts once it and every parameter before it are ready), so every rank
+    issues the same collectives in the same order whatever order its hooks fire in; the
+    collectives run on RCCL's stream while the rest of the backward runs on the compute stream.
+    ``wait()`` issues whatever is left -- a parameter this rank produced no gradient for (e.g. a
+    rank holding no views) contributes zeros -- and joins them.  The vertex gradient (the last
     one produced) is reduced by the caller."""
 
     def __init__(self, params, group=None):
         self.group = group
+        self.params = list(params)
         self.works = []
         self.handles = []
+        self.ready = [False] * len(self.params)
+        self.next = 0
         if _distributed(group):
-            for p in params:
-                self.handles.append(p.register_post_accumulate_grad_hook(self._hook))
+            for i, p in enumerate(self.params):
+                self.handles.append(p.register_post_accumulate_grad_hook(
+                    lambda _p, i=i: self._hook(i)))
 
-    def _hook(self, p):
+    def _issue(self, i):
+        p = self.params[i]
+        if p.grad is None:
+            p.grad = torch.zeros_like(p)
         self.works.append(dist.all_reduce(p.grad, op=dist.ReduceOp.SUM, group=self.group,
                                           async_op=True))
 
+    def _hook(self, i):
+        self.ready[i] = True
+        while self.next < len(self.params) and self.ready[self.next]:
+            self._issue(self.next)
+            self.next += 1
+
     def wait(self):
+        if self.handles:
+            while self.next < len(self.params):
+                self._issue(self.next)
+                self.next += 1
         for w in self.works:
             w.wait()
         self.works = []
@@ -96,6 +117,57 @@ class EarlyReduce:
         for h in self.handles:
             h.remove()
         self.handles = []
+
+
+class GradBucket:
+    """The step's exchange: the shared parameters' gradients summed over the ranks as ONE flat
+    all-reduce.  The flat buffer is allocated once; ``pack()`` copies the gradients into it (on
+    the current stream: inside a captured HIP graph these copies are graph nodes), ``reduce()``
+    runs the collective (RCCL over xGMI with backend "nccl") and ``unpack()`` copies the sums
+    back.  A single contiguous gradient is reduced in place (no copies).  Parameters without a
+    gradient on this rank contribute zeros, so every rank issues the same collective."""
+
+    def __init__(self, params, group=None):
+        self.params = list(params)
+        self.group = group
+        self.flat = None
+
+    def _grads(self):
+        for p in self.params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        return [p.grad for p in self.params]
+
+    def pack(self):
+        if not self.params or not _distributed(self.group):
+            return
+        gs = self._grads()
+        if len(gs) == 1 and gs[0].is_contiguous():
+            return
+        n = sum(g.numel() for g in gs)
+        if self.flat is None or self.flat.numel() != n or self.flat.device != gs[0].device:
+            self.flat = torch.empty(n, device=gs[0].device, dtype=gs[0].dtype)
+        off = 0
+        for g in gs:
+            self.flat[off:off + g.numel()].copy_(g.reshape(-1))
+            off += g.numel()
+
+    def reduce(self):
+        if not self.params or not _distributed(self.group):
+            return
+        gs = self._grads()
+        if len(gs) == 1 and gs[0].is_contiguous():
+            dist.all_reduce(gs[0], op=dist.ReduceOp.SUM, group=self.group)
+            return
+        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
+        off = 0
+        for g in gs:
+            g.copy_(self.flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
+
+    def __call__(self):
+        self.pack()
+        self.reduce()
 
 
 def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_features, height,
@@ -158,8 +230,8 @@ def dibr_step(vertices, faces, camera_proj, camera_transform, face_features, hei
         face_idx = dibr_forward_backward(vertices, faces, camera_proj, camera_transform,
                                          face_features, height, width, grad_interp, grad_soft,
                                          sigmainv, boxlen, knum, prepare, render)
-        late = [vertices.grad] + [p.grad for p in shared if not early.handles]
-        allreduce_grads_(late, group)
+        late = [vertices] + [p for p in shared if not early.handles]
+        GradBucket(late, group)()
         early.wait()
     finally:
         early.remove()
@@ -168,28 +240,35 @@ def dibr_step(vertices, faces, camera_proj, camera_transform, face_features, hei
 
 class GraphedStep:
     """``dibr_step`` with its GPU part captured once in a HIP graph (torch.cuda.CUDAGraph over
-    the library's stream-ordered launches) and replayed; the all-reduce of the shared gradients
-    stays an eager RCCL call after the replay.  Inputs and the .grad tensors are static: the
-    replay overwrites the gradients in place (they are None at capture, so the captured backward
-    assigns instead of accumulating).  `warmup` eager steps on a side stream come first (they
-    also build the per-topology vertex->face table, a one-time host copy)."""
+    the library's stream-ordered launches) and replayed; the step's exchange (``GradBucket``: the
+    shared gradients packed into one flat buffer -- the packing copies are captured in the graph
+    -- and one all-reduce) stays an eager RCCL call after the replay.  Inputs and the .grad
+    tensors are static: the replay overwrites the gradients in place (they are None at capture,
+    so the captured backward assigns instead of accumulating).  `warmup` eager steps on a side
+    stream come first (they also build the per-topology vertex->face table, a one-time host
+    copy).  Every replay restarts the library's device state (pool counters, the record cursor,
+    the zeroed-on-the-side gradient buffers) inside the graph: tests/test_gpu_graphed_step.py
+    compares replays with eager steps."""
 
     def __init__(self, params, fn, params_to_reduce=None, group=None, warmup=3):
         self.params = list(params)  # every parameter whose .grad the step writes
         self.reduce = self.params if params_to_reduce is None else list(params_to_reduce)
         self.fn = fn
         self.group = group
+        self.bucket = GradBucket(self.reduce, group)
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._clear()
                 fn()
+                self.bucket.pack()
         torch.cuda.current_stream().wait_stream(s)
         self._clear()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = fn()
+            self.bucket.pack()
 
     def _clear(self):
         for p in self.params:
@@ -197,5 +276,5 @@ class GraphedStep:
 
     def __call__(self):
         self.graph.replay()
-        allreduce_grads_([p.grad for p in self.reduce], self.group)
+        self.bucket.reduce()
         return self.out

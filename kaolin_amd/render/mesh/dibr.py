@@ -340,7 +340,8 @@ def dibr_rasterization_with_mask_iou(height, width, face_vertices_z, face_vertic
     _eps = 1e-8 if eps is None else eps
     feats = torch.cat(face_features, dim=-1) \
         if isinstance(face_features, (list, tuple)) else face_features
-    if int(knum) > 32 or _lists_enabled() or _lib.pool_limits_active():
+    if (int(knum) > 32 or _lists_enabled() or _lib.pool_limits_active() or
+            gt_mask.requires_grad or _lib.split_soft_mask_forced()):
         interp, soft, face_idx = dibr_rasterization(
             height, width, face_vertices_z, face_vertices_image, face_features, face_normals_z,
             sigmainv, boxlen, knum, multiplier, eps)

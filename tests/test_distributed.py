@@ -150,3 +150,86 @@ def test_allreduce_noop_without_process_group():
     t = torch.arange(6.)
     out = distributed.allreduce_grads_([t, None])
     assert len(out) == 1 and torch.equal(t, torch.arange(6.))
+
+
+# --------------------------------------------------------------------------------------------
+# the exchange of GraphedStep / dibr_step (GradBucket) and the ordered early reduction
+# --------------------------------------------------------------------------------------------
+def _bucket_worker(rank, world, port, q):
+    """GradBucket over two shared parameters, one of which has no gradient on rank 1 (a rank
+    that produced none contributes zeros); pack() then reduce(), the two calls GraphedStep makes
+    (pack inside the captured graph, reduce after the replay)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        r, wsz, _ = distributed.init_from_env('gloo')
+        a = torch.zeros(3, 4, requires_grad=True)
+        b = torch.zeros(5, requires_grad=True)
+        a.grad = torch.arange(12.).reshape(3, 4) * (r + 1)
+        if r == 0:
+            b.grad = torch.full((5,), 2.5)
+        bucket = distributed.GradBucket([a, b])
+        bucket.pack()
+        bucket.reduce()
+        # a second step reuses the flat buffer
+        a.grad.fill_(1.)
+        b.grad.fill_(float(r))
+        bucket()
+        q.put((r, a.grad.numpy().copy(), b.grad.numpy().copy()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, 'error', repr(e)))
+
+
+def _early_worker(rank, world, port, q):
+    """EarlyReduce with two shared parameters whose gradients are produced in OPPOSITE orders on
+    the two ranks (separate backward calls): the all-reduces must still pair up."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        r, wsz, _ = distributed.init_from_env('gloo')
+        p0 = torch.zeros(4, requires_grad=True)
+        p1 = torch.zeros(7, requires_grad=True)
+        early = distributed.EarlyReduce([p0, p1])
+        x0 = torch.arange(4.) + 10 * r
+        x1 = torch.arange(7.) - 3 * r
+        order = [(p0, x0), (p1, x1)] if r == 0 else [(p1, x1), (p0, x0)]
+        for p, x in order:
+            (p * x).sum().backward()
+        early.wait()
+        early.remove()
+        q.put((r, p0.grad.numpy().copy(), p1.grad.numpy().copy()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, 'error', repr(e)))
+
+
+def _run_world(target, world=2):
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    errs = [r for r in res if isinstance(r[1], str)]
+    assert not errs, errs
+    return sorted(res, key=lambda r: r[0])
+
+
+def test_grad_bucket_world2():
+    res = _run_world(_bucket_worker)
+    for _, ga, gb in res:
+        np.testing.assert_array_equal(ga, np.ones((3, 4)) * 2)
+        np.testing.assert_array_equal(gb, np.full(5, 1.0))
+
+
+def test_early_reduce_fixed_order_world2():
+    res = _run_world(_early_worker)
+    for _, g0, g1 in res:
+        np.testing.assert_array_equal(g0, 2 * np.arange(4.) + 10)
+        np.testing.assert_array_equal(g1, 2 * np.arange(7.) - 3)

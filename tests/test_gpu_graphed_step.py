@@ -1,0 +1,99 @@
+"""GPU: the timed region of bench.py -- ``distributed.GraphedStep`` (the DIB-R training step
+captured once in a HIP graph and replayed) -- against the eager step and the oracle.
+
+Every replay must restart the library's device state: the pool counters and the record cursor
+(zeroed by kd_bin_count, kd_binning.hip), the gradient buffers the forward zeroes on the side
+(kd_softpair.hip soft_pairs_tile), the IoU accumulators.  So three consecutive replays must each
+give the eager step's face_idx (bit-exact), and its vertex and feature gradients up to the float
+atomics' summation order; view 0 of a replay is also checked against the oracle's brute-force
+loops (face index, interpolated features, feature gradient).
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _native():
+    from kaolin_amd import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+
+
+def _setup(n_lon, n_lat, h, B, iou):
+    from kaolin_amd import workloads
+    verts, faces, face_uvs = workloads.uv_sphere(n_lon, n_lat, seed=0)
+    vertices = verts.to(DEV).requires_grad_(True)
+    faces = faces.to(DEV)
+    cam = workloads.orbit_cameras(B, 0.3).to(DEV)
+    proj = workloads.generate_perspective_projection(math.pi / 4).to(DEV)
+    uvs = face_uvs.to(DEV).unsqueeze(0).repeat(B, 1, 1, 1)
+    feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
+    feats.requires_grad_(True)
+    g_feat, g_soft = workloads.view_grads(0, B, h, h, 3)
+    gt = None
+    if iou:
+        yy, xx = torch.meshgrid(torch.arange(h, dtype=torch.float32),
+                                torch.arange(h, dtype=torch.float32), indexing='ij')
+        gt = (((yy - h / 2) ** 2 + (xx - h / 2) ** 2) < (0.4 * h) ** 2).float()
+        gt = gt.expand(B, h, h).contiguous().to(DEV)
+    return dict(vertices=vertices, faces=faces, cam=cam, proj=proj, feats=feats,
+                g_feat=g_feat.to(DEV), g_soft=g_soft.to(DEV), gt=gt, h=h)
+
+
+def _fn(s):
+    from kaolin_amd import distributed
+    return lambda: distributed.dibr_forward_backward(
+        s['vertices'], s['faces'], s['proj'], s['cam'], s['feats'], s['h'], s['h'], s['g_feat'],
+        s['g_soft'], gt_mask=s['gt'], iou='fused')
+
+
+def _eager(s):
+    s['vertices'].grad = None
+    s['feats'].grad = None
+    fidx = _fn(s)()
+    torch.cuda.synchronize()
+    return fidx.clone(), s['vertices'].grad.clone(), s['feats'].grad.clone()
+
+
+@pytest.mark.parametrize('cfg', [(100, 51, 256, 4), (250, 101, 512, 2)], ids=['c2', 'c3x2'])
+@pytest.mark.parametrize('iou', [False, True], ids=['grad_soft', 'mask_iou'])
+def test_graphed_step_replays_match_eager(cfg, iou):
+    from kaolin_amd import distributed
+    n_lon, n_lat, h, B = cfg
+    s = _setup(n_lon, n_lat, h, B, iou)
+    e_fidx, e_gv, e_gf = _eager(s)
+    gs = distributed.GraphedStep([s['vertices'], s['feats']], _fn(s),
+                                 params_to_reduce=[s['vertices']])
+    for rep in range(3):
+        # poison the outputs so a replay that skipped work cannot pass
+        s['vertices'].grad.fill_(float('nan'))
+        s['feats'].grad.fill_(float('nan'))
+        gs.out.fill_(-7)
+        fidx = gs()
+        torch.cuda.synchronize()
+        assert torch.equal(fidx, e_fidx), rep
+        for x, y in ((s['vertices'].grad, e_gv), (s['feats'].grad, e_gf)):
+            scale = y.abs().max().item()
+            assert scale > 0
+            torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * scale)
+    # view 0 of the last replay against the oracle
+    from kaolin_amd.render.mesh import prepare_vertices
+    with torch.no_grad():
+        fvc, fvi, nrm = prepare_vertices(s['vertices'].detach().unsqueeze(0), s['faces'],
+                                         s['proj'], camera_transform=s['cam'])
+    N = lambda t: np.ascontiguousarray(t[:1].detach().cpu().numpy())  # noqa: E731
+    feats0 = N(s['feats'])
+    ri, rf, rw = oracle.rasterize(h, h, N(fvc[..., 2]), N(fvi), feats0, N(nrm[..., 2]) >= 0)
+    np.testing.assert_array_equal(N(gs.out), rf)
+    _, gfeat = oracle.rasterize_backward(N(s['g_feat']), rf, rw, N(fvi), feats0, 1e-8)
+    np.testing.assert_allclose(N(s['feats'].grad), gfeat, rtol=1e-4,
+                               atol=1e-5 * np.abs(gfeat).max())

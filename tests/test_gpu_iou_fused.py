@@ -113,3 +113,32 @@ def test_fused_iou_fallback_and_retained_graph():
     g1, = torch.autograd.grad(loss, x, retain_graph=True)
     g2, = torch.autograd.grad(loss, x)
     np.testing.assert_allclose(N(g1), N(g2), rtol=1e-5, atol=1e-6 * float(N(g1.abs().max())))
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_gt_mask_requiring_grad_gets_its_gradient(dname):
+    """mask_iou differentiates its right-hand mask too (metrics/render.py:18-40): a gt_mask that
+    requires grad must receive d loss / d gt (the fused kernels produce none, so the composition
+    runs) -- equal to the composition's, and the renderer's gradients unchanged."""
+    from kaolin_amd.metrics.render import mask_iou
+    from kaolin_amd.render.mesh import dibr_rasterization, dibr_rasterization_with_mask_iou
+    dt = TORCH_DTYPES[dname]
+    h = 64
+    fvz, fvi0, feats, nz = _views(30, 16, h, 2, dt)
+    _, _, fidx = dibr_rasterization(h, h, fvz, fvi0, feats, nz)
+    gt0 = _gt(fidx, dt)
+    res = []
+    for fused in (True, False):
+        fvi = fvi0.clone().requires_grad_(True)
+        gt = gt0.clone().requires_grad_(True)
+        if fused:
+            _, soft, _, loss = dibr_rasterization_with_mask_iou(h, h, fvz, fvi, feats, nz, gt)
+        else:
+            _, soft, _ = dibr_rasterization(h, h, fvz, fvi, feats, nz)
+            loss = mask_iou(soft, gt)
+        loss.backward()
+        assert gt.grad is not None and gt.grad.abs().max() > 0
+        res.append((loss.detach(), fvi.grad, gt.grad))
+    tol = dict(rtol=1e-5, atol=1e-7) if dname == 'f32' else dict(rtol=1e-12, atol=1e-14)
+    for a, b in zip(res[0], res[1]):
+        torch.testing.assert_close(a, b, **tol)

@@ -43,6 +43,9 @@ def main(summary, out, config, dtype='f32', views=8, lists=False):
         kern[slot] = {'device_kernel': name,
                       'hbm_bytes_per_launch': round(m['hbm_bytes_fetch_x2']),
                       'FETCH_SIZE_KiB': m['FETCH_SIZE'], 'WRITE_SIZE_KiB': m['WRITE_SIZE']}
+        for c in ('SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_WAVES', 'GRBM_GUI_ACTIVE'):
+            if c in m:  # per launch (bench.py: VALU issue fraction)
+                kern[slot][c] = m[c]
     json.dump({'config': config, 'dtype': dtype, 'views_per_gpu': views, 'lists': lists,
                'source': summary, 'traffic': 'FETCH_SIZE x 2 + WRITE_SIZE (KiB x 1024)',
                'kernels': kern}, open(out, 'w'), indent=1)

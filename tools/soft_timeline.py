@@ -13,8 +13,10 @@ import bench  # noqa: E402
 from kaolin_amd import _lib, workloads  # noqa: E402
 from kaolin_amd.render.mesh import dibr_rasterization  # noqa: E402
 
-cfg = sys.argv[1] if len(sys.argv) > 1 else 'c3'
+cfg = sys.argv[1] if len(sys.argv) > 1 else 'c3'   # 'c3' or 'c3:1' (views override)
+cfg, _, nv = cfg.partition(':')
 n_lon, n_lat, H, W, B, elev = bench.CONFIGS[cfg]
+B = int(nv) if nv else B
 dev = torch.device('cuda')
 v = workloads.sphere_views(n_lon, n_lat, H, W, B, dev, elevation=elev)
 fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['normals_z']
@@ -63,7 +65,7 @@ for q in range(10):
           f'{heavy.sum():4d}  heavy unc {u_slot[sl][heavy].mean() if heavy.any() else 0:6.1f} '
           f'heavy nbin {nbin[sl][heavy].mean() if heavy.any() else 0:7.1f}')
 if t[3].any():  # per-slot table for offline study: slot, tile, raster / soft bin counts, unc, us
-    out = os.path.join('gpurun_out', f'timeline_{cfg}.csv')
+    out = os.path.join('gpurun_out', f'timeline_{cfg}_{B}.csv')
     os.makedirs('gpurun_out', exist_ok=True)
     with open(out, 'w') as fh:
         fh.write('slot,tile,raster_nbin,soft_nbin,unc,start,raster_us,soft_us\n')
