@@ -1,5 +1,6 @@
 // kd_binning.hip -- see kd_binning.hpp for the algorithm.
 #include "kd_binning.hpp"
+#include "kd_cull.hpp"
 #include "kd_tile.hpp"
 
 #include "kd_capi.hpp"
@@ -12,9 +13,10 @@ static int64_t fine_tiles(int H, int W) {
   return (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
 }
 
-size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view) {
-  const BinGeom g = bin_geom(H, W);
-  const int64_t nchunk = (max_per_view + kChunk - 1) / kChunk;
+size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view, int ct0) {
+  const BinGeom g = bin_geom(H, W, ct0);
+  const int chunk = bin_chunk(B, max_per_view);
+  const int64_t nchunk = (max_per_view + chunk - 1) / chunk;
   size_t s = 0;
   s += align_up(sizeof(Span) * (size_t)N);
   s += align_up(sizeof(int) * (size_t)B * (size_t)(nchunk > 0 ? nchunk : 1) * g.nct());
@@ -27,10 +29,11 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view)
 }
 
 BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
-                     int64_t max_per_view) {
+                     int64_t max_per_view, int ct0) {
   BinBuffers bb;
-  bb.g = bin_geom(H, W);
-  bb.nchunk = (int)((max_per_view + kChunk - 1) / kChunk);
+  bb.g = bin_geom(H, W, ct0);
+  bb.chunk = bin_chunk(B, max_per_view);
+  bb.nchunk = (int)((max_per_view + bb.chunk - 1) / bb.chunk);
   char *base = (char *)ws;
   bb.spans = (Span *)(base + off);
   off += align_up(sizeof(Span) * (size_t)N);
@@ -56,71 +59,11 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   return bb;
 }
 
-// Edge-culling coefficients of one face for the fp32 pair raster (kd_raster.hip).
-//
-// With the reference's fp32 centres x0, y0 and the scaled corners, w0 is computed as
-// fl(fl(bex*cey) - fl(bey*cex)) over rounded edges; its exact counterpart is affine,
-//   W0 = A0 + B0 x0 + C0 y0,  A0 = bx cy - by cx,  B0 = by - cy,  C0 = cx - bx  (cyclic for 1, 2),
-// and |w_i - W_i| <= tau = 2^-20 E^2 with E = max|corner| + |M| (4.02u(|P1|+|P2|) <= 8.04u E^2,
-// u = 2^-24).  The three W_i sum to N = A0 + A1 + A2 (twice the signed area) at every pixel;
-// when |N| > 6 tau the computed eps-normalised norm has the sign s of N, so a pixel with
-// s W_i < -2 tau for some i has w_i / norm < 0 and is rejected by the reference
-// (rasterization_cuda.cu:145; |w_i| > tau and |eps| <= E^2 keep the quotient finite and away
-// from -0) -- culling it cannot change the result.  Keep iff s W_i >= -2 tau
-// is, for s B_i > 0 (< 0), x0 >= (<=) X*(y0); in tile-local pixel units
-// in pixel units relative to the face's own span (column span.x0, row span.y0),
-//   p*(y0) = P0 + P1 (y0 - y0ref),  y0ref = centre of row span.y0,
-// and the raster keeps columns >= ceil(max_lo - 1/64) and <= floor(min_hi + 1/64).  The 1/64 px
-// slack covers the fp32 evaluation there (|P0| <= 2^14, |P1 d| <= 2^13 over the span's rows,
-// a handful of roundings of at most 2^-10 each), the centre rounding (u W / 2 <= 2^-10 for
-// W <= 2^15) and the double-precision coefficients (terms bounded by 2^40 px: < 2^-12).  Edges outside these bounds, degenerate
-// or non-finite faces and non-positive pixel steps cull nothing (slots stay -inf / +inf).
-// out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}
+// Edge-culling coefficients of one face for the fp32 pair raster: kd_cull.hpp (the rule and its
+// proof; host-compilable for tools/cull_check.cpp).
 __device__ void raster_cull_coefs(const float v[6], float M, int H, int W, Span sp, float eps,
                                   float out[8]) {
-  out[0] = out[2] = -INFINITY;
-  out[4] = out[6] = INFINITY;
-  out[1] = out[3] = out[5] = out[7] = 0.f;
-  const double ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
-  const double vm = fmax(fmax(fmax(fabs(ax), fabs(ay)), fmax(fabs(bx), fabs(by))),
-                         fmax(fabs(cx), fabs(cy)));
-  const float sxf = M / (float)W, syf = M / (float)H;
-  if (!(vm < 0x1p59) || !(sxf > 0.f) || !(syf > 0.f) || W > 32768 || H > 32768) return;
-  const double E = vm + 1.001 * fabs((double)M);
-  const double tau = 0x1p-20 * E * E;
-  const double A[3] = {bx * cy - by * cx, cx * ay - cy * ax, ax * by - ay * bx};
-  const double Bc[3] = {by - cy, cy - ay, ay - by};
-  const double Cc[3] = {cx - bx, ax - cx, bx - ax};
-  const double N = A[0] + A[1] + A[2];
-  if (!(fabs(N) > 6.0 * tau) || !(fabs((double)eps) <= E * E)) return;
-  const double s = N > 0.0 ? 1.0 : -1.0;
-  const double sx = sxf, sy = syf;
-  const double y0ref = (double)px_cy(M, H, sp.y0);
-  const double drows = 2.0 * sy * (double)(sp.y1 - sp.y0 + 1);  // >= |y0 - y0ref| on the span
-  bool has_lo = false, has_hi = false;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double sB = s * Bc[i];
-    if (sB == 0.0) continue;
-    const double inv = 1.0 / (2.0 * sB * sx);
-    const double P1 = -s * Cc[i] * inv;
-    const double t = -2.0 * tau - s * (A[i] + Cc[i] * y0ref);
-    if (!(fabs(P1) * drows <= 0x1p13) ||
-        !((fabs(A[i]) + fabs(Cc[i] * y0ref) + 2.0 * tau) * fabs(inv) <= 0x1p40))
-      continue;
-    double P0 = t * inv + 0.5 * (double)(W - 1) - (double)sp.x0;
-    P0 = fmin(fmax(P0, -0x1p14), 0x1p14);
-    // the exact signs of the B_i cannot all agree (B0 + B1 + B2 = 0): at most two per side
-    if (sB > 0.0) {
-      out[has_lo ? 2 : 0] = (float)P0;
-      out[has_lo ? 3 : 1] = (float)P1;
-      has_lo = true;
-    } else {
-      out[has_hi ? 6 : 4] = (float)P0;
-      out[has_hi ? 7 : 5] = (float)P1;
-      has_hi = true;
-    }
-  }
+  raster_cull_coefs_at(v, M, H, W, sp.x0, sp.y0, sp.y1, eps, out);
 }
 
 template <typename T>
@@ -130,7 +73,7 @@ struct BinJobs {
   SpanConsts k[2];  // make_span constants of each set (host-computed)
 };
 
-template <typename T>
+template <typename T, int PER>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   const FaceSet<T> &fs = jobs.fs[blockIdx.z];
   const BinBuffers &bb = jobs.bb[blockIdx.z];
@@ -146,8 +89,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   view_range(fs, b, lo, hi);
   __syncthreads();
 #pragma unroll
-  for (int u = 0; u < kChunk / kBlock; ++u) {
-    const int64_t i = lo + (int64_t)chunk * kChunk + u * kBlock + tid;
+  for (int u = 0; u < PER; ++u) {
+    const int64_t i = lo + (int64_t)chunk * (PER * kBlock) + u * kBlock + tid;
     if (i < hi) {
       Span s;
       const bool ok = (!fs.valid || fs.valid[i]) && (!fs.nz || fs.nz[i * fs.nz_stride] >= (T)0);
@@ -240,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
   if (live && lane == 0) bb.totals[(int64_t)b * nct + c] = total;
 }
 
-template <typename T>
+template <typename T, int PER>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   const FaceSet<T> &fs = jobs.fs[blockIdx.z];
   const BinBuffers &bb = jobs.bb[blockIdx.z];
@@ -249,9 +192,9 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
       tile_order(bb, fs.B, (fs.W + kTile - 1) / kTile, (fs.H + kTile - 1) / kTile);
     return;
   }
-  // kChunk-bit membership mask per coarse tile: bit t set <=> face (chunk*kChunk + t) touches it;
-  // each thread holds faces tid and tid + 256.
-  constexpr int kWords = kChunk / 32, kPerT = kChunk / kBlock;
+  // chunk-bit membership mask per coarse tile: bit t set <=> face (chunk * chunk size + t) touches
+  // it; each thread holds faces tid (and tid + 256).
+  constexpr int kWords = PER * kBlock / 32, kPerT = PER;
   extern __shared__ uint32_t s_mask[];  // [nct][kWords]
   __shared__ int s_bbase[kMaxCtiles], s_scan[kBlock / kWave];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
@@ -262,7 +205,7 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   Span sp[kPerT];
 #pragma unroll
   for (int u = 0; u < kPerT; ++u) {
-    const int64_t i = lo + (int64_t)chunk * kChunk + u * kBlock + tid;
+    const int64_t i = lo + (int64_t)chunk * (PER * kBlock) + u * kBlock + tid;
     sp[u] = Span{1, 0, 1, 0};
     if (i < hi) sp[u] = bb.spans[i];
   }
@@ -314,7 +257,7 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
     const int t = u * kBlock + tid;
     const uint32_t bit = 1u << (t & 31);
     const int word = t >> 5;
-    const int local = chunk * kChunk + t;
+    const int local = chunk * (PER * kBlock) + t;
     for (int cy = sp[u].y0 >> bb.g.sh; cy <= sp[u].y1 >> bb.g.sh; ++cy)
       for (int cx = sp[u].x0 >> bb.g.sh; cx <= sp[u].x1 >> bb.g.sh; ++cx) {
         const int c = cy * bb.g.nctx + cx;
@@ -428,27 +371,35 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
   }
   const dim3 grid_c(bb.nchunk, fs.B, njobs);
   const dim3 grid_t((bb.g.nct() + kBlock / kWave - 1) / (kBlock / kWave), fs.B, njobs);
+  const bool two = bb.chunk == 2 * kBlock;
   {
     ProfScope prof(K_BIN_COUNT, stream);
-    hipLaunchKernelGGL(kd_bin_count<T>, grid_c, dim3(kBlock), 0, stream, jobs);
+    if (two)
+      hipLaunchKernelGGL((kd_bin_count<T, 2>), grid_c, dim3(kBlock), 0, stream, jobs);
+    else
+      hipLaunchKernelGGL((kd_bin_count<T, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
   }
   {
     ProfScope prof(K_BIN_SCAN, stream);
     hipLaunchKernelGGL(kd_bin_scan<T>, grid_t, dim3(kBlock), 0, stream, jobs);
   }
   {  // + one column of workgroups for the tile order (kd_bin_scatter, tile_order)
-    // kChunk-bit masks per coarse tile: up to 64 KB of dynamic LDS at 1024 coarse tiles (a
+    // chunk-bit masks per coarse tile: up to 64 KB of dynamic LDS at 1024 coarse tiles (a
     // gfx950 workgroup may hold up to 160 KB; past 64 KB it has to be asked for)
-    const size_t dyn = sizeof(uint32_t) * (kChunk / 32) * (size_t)bb.g.nct();
+    const size_t dyn = sizeof(uint32_t) * (bb.chunk / 32) * (size_t)bb.g.nct();
+    const void *fn = two ? (const void *)kd_bin_scatter<T, 2> : (const void *)kd_bin_scatter<T, 1>;
     if (dyn > 48 * 1024) {
-      const hipError_t ea = hipFuncSetAttribute((const void *)kd_bin_scatter<T>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                (int)dyn);
+      const hipError_t ea =
+          hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn);
       if (ea != hipSuccess) return ea;
     }
     ProfScope prof(K_BIN_SCATTER, stream);
-    hipLaunchKernelGGL(kd_bin_scatter<T>, dim3(bb.nchunk + 1, fs.B, njobs), dim3(kBlock),
-                       sizeof(uint32_t) * (kChunk / 32) * bb.g.nct(), stream, jobs);
+    if (two)
+      hipLaunchKernelGGL((kd_bin_scatter<T, 2>), dim3(bb.nchunk + 1, fs.B, njobs), dim3(kBlock),
+                         dyn, stream, jobs);
+    else
+      hipLaunchKernelGGL((kd_bin_scatter<T, 1>), dim3(bb.nchunk + 1, fs.B, njobs), dim3(kBlock),
+                         dyn, stream, jobs);
   }
   return hipGetLastError();
 }

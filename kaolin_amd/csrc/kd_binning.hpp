@@ -54,6 +54,7 @@ struct BinBuffers {
   int2 *order;     // [B * fine tiles] (view * tiles + tile, its coarse bin's face count),
                    // heaviest first (tile_order in kd_bin_scatter): the tile kernels' dispatch order
   int nchunk;
+  int chunk;       // faces per chunk (bin_chunk: 256 or 512)
   BinGeom g;
 };
 
@@ -83,10 +84,11 @@ float pool_limit_bins();
 float pool_limit_pairs();
 bool pool_limits_ever_set();  // kd_set_pool_limits has held a pool below 1 in this process
 
-size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view);
+size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view,
+                           int ct0 = kCoarseTile0);
 // Carves the buffers from `ws` starting at *offset (advanced past them).
 BinBuffers bin_carve(void *ws, size_t &offset, int B, int H, int W, int64_t N,
-                     int64_t max_per_view);
+                     int64_t max_per_view, int ct0 = kCoarseTile0);
 
 template <typename T>
 hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t stream);

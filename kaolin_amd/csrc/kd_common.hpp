@@ -29,6 +29,9 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       kernel instead of the pair pipeline, 16 / 32 skip the per-pair pass of the fp32
 //       raster / soft mask, 64 record per-tile durations into the kd_debug_buffer array,
 //       8192 skip the fp32 raster's per-pixel epilogue (winner reload, output writes),
+//       32 also skips the fused soft mask's pair math (kd_softpair.hip soft_pairs_tile),
+//       1 << 27 (production too) disables the small-batch forward (kd_soft.hpp dibr_small_batch),
+//       1 << 28 (production too) the balanced (item-dealing) fused forward tiles,
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
 int debug_flags();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
@@ -57,7 +60,11 @@ struct TileClock {
 constexpr int kWave = 64;
 constexpr int kBlock = 256;      // 4 waves
 constexpr int kTile = 16;        // fine tile: 16x16 pixels per workgroup, 8x8 per wave
-constexpr int kChunk = 512;      // faces per binning workgroup (two per thread)
+constexpr int kChunk = 512;      // faces per binning workgroup (two per thread) ...
+// ... or one per thread when the batch is small, so the binning grids still fill the chip
+__host__ __device__ inline int bin_chunk(int B, int64_t max_per_view) {
+  return (int64_t)B * ((max_per_view + kChunk - 1) / kChunk) < 256 ? kChunk / 2 : kChunk;
+}
 constexpr int kMaxCtiles = 1024; // coarse tiles per view (LDS bound of the binning kernels)
 
 // ------------------------------------------------------------------------------------------
@@ -415,9 +422,11 @@ struct BinGeom {
   __host__ __device__ int nct() const { return nctx * ncty; }
 };
 
-__host__ __device__ inline BinGeom bin_geom(int H, int W) {
+// ct0: the smallest coarse tile (kCoarseTile0, or kTile for the small-batch forward of
+// kd_dibr.hip, whose workgroups cover 8x8 pixels and walk 16-pixel coarse bins)
+__host__ __device__ inline BinGeom bin_geom(int H, int W, int ct0 = kCoarseTile0) {
   int m = H > W ? H : W;
-  int ct = kCoarseTile0;
+  int ct = ct0;
   while (((m + ct - 1) / ct) > 32) ct *= 2;
   BinGeom g;
   g.ct = ct;

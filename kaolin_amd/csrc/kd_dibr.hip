@@ -23,7 +23,9 @@ namespace kd {
 
 size_t dibr_workspace_bytes(int B, int H, int W, int64_t F, int K, int esize) {
   const int64_t N = (int64_t)B * F;
-  return bin_workspace_bytes(B, H, W, N, F) + soft_pair_workspace_bytes(B, H, W, N, F, K, esize);
+  const int ct0 = dibr_ct0(B, H, W, esize);
+  return bin_workspace_bytes(B, H, W, N, F, ct0) +
+         soft_pair_workspace_bytes(B, H, W, N, F, K, esize, ct0);
 }
 
 template <typename T>
@@ -36,10 +38,11 @@ struct DibrBuffers {
 template <typename T>
 static DibrBuffers<T> dibr_carve(void *ws, int B, int H, int W, int64_t F, int K) {
   const int64_t N = (int64_t)B * F;
+  const int ct0 = dibr_ct0(B, H, W, sizeof(T));
   DibrBuffers<T> d;
   size_t off = 0;
-  d.rbb = bin_carve(ws, off, B, H, W, N, F);
-  d.sbb = bin_carve(ws, off, B, H, W, N, F);  // soft_pair_workspace_bytes starts with these bins
+  d.rbb = bin_carve(ws, off, B, H, W, N, F, ct0);
+  d.sbb = bin_carve(ws, off, B, H, W, N, F, ct0);  // soft_pair_workspace_bytes starts with these
   d.pb = soft_pair_carve<T>(ws, off, B, H, W, K);
   return d;
 }
@@ -263,17 +266,21 @@ int64_t kd_dibr_pair_count(const void *ws, int B, int H, int W, int64_t F, int k
                            int double_precision, void *stream) {
   if (!ws || B <= 0 || H <= 0 || W <= 0 || knum < 1) return 0;
   void *w = const_cast<void *>(ws);
-  const int32_t *ntile = double_precision ? dibr_carve<double>(w, B, H, W, F, knum).pb.ntile
-                                          : dibr_carve<float>(w, B, H, W, F, knum).pb.ntile;
-  const int64_t tiles =
-      (int64_t)B * ((W + kTile - 1) / kTile) * (int64_t)((H + kTile - 1) / kTile);
-  std::vector<int32_t> nt((size_t)tiles);
+  // the records are those of the work items (every fused form writes them)
+  const int32_t *counters = double_precision ? dibr_carve<double>(w, B, H, W, F, knum).pb.counters
+                                             : dibr_carve<float>(w, B, H, W, F, knum).pb.counters;
+  const PairItem *items = double_precision ? dibr_carve<double>(w, B, H, W, F, knum).pb.items
+                                           : dibr_carve<float>(w, B, H, W, F, knum).pb.items;
   if (hipStreamSynchronize((hipStream_t)stream) != hipSuccess) return -1;
-  if (hipMemcpy(nt.data(), ntile, sizeof(int32_t) * nt.size(), hipMemcpyDeviceToHost) !=
-      hipSuccess)
+  int32_t nitems = 0;
+  if (hipMemcpy(&nitems, counters, sizeof(int32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  std::vector<PairItem> it((size_t)std::max(nitems, 0));
+  if (nitems > 0 && hipMemcpy(it.data(), items, sizeof(PairItem) * it.size(),
+                              hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   int64_t n = 0;
-  for (int64_t i = 0; i < tiles; ++i) n += nt[i];
+  for (const PairItem &x : it) n += x.n;
   return n;
 }
 

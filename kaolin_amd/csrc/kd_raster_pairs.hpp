@@ -92,8 +92,18 @@ struct RasterPairsLDS {
 
 // Tile tl of view b (nbin: faces of its coarse bin, or -1).  Each thread owns pixel
 // (t.px, t.py) of tile_geom(H, W, tl) and writes its outputs.
+// BAL (balanced): the (sub-tile, 64-face chunk) items of every batch -- the four sub-lists' chunks
+// -- are dealt to the four waves in turn, so a sub-tile whose list is long (the pole, a dense
+// silhouette) is tested by all four waves; the pairs carry their sub-tile and the winners meet in
+// its LDS key row.  Without BAL each wave tests its own sub-tile's chunks.
+// ST (small-batch mode, kd_dibr_fwd_st): the workgroup covers quadrant `quad` of the tile only
+// (tile_geom_st); its four waves share the quadrant's 64 pixels and its one list (every wave built
+// the same sub-list), the chunks dealt as with BAL, and wave 0 writes the outputs.
+template <bool ST = false, bool BAL = false>
 __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a, int b, int tl,
-                                                  int nbin, RasterPairsLDS &S) {
+                                                  int nbin, RasterPairsLDS &S, int quad = 0) {
+  constexpr bool kItems = ST || BAL;  // chunks dealt to the waves as (sub-tile, chunk) items
+  constexpr int NS = ST ? 1 : 4;       // sub-lists of the workgroup
   TileLists &L = S.L;
   auto &s_geo = S.geo;
   auto &s_cull = S.cull;
@@ -106,11 +116,14 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  TileGeom t = tile_geom(H, W, tl);
+  TileGeom t = ST ? tile_geom_st(H, W, tl, quad) : tile_geom(H, W, tl);
   t.nbin = nbin;
+  const int kw = ST ? 0 : w;  // LDS key row of this wave's pixels
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
-  s_key[w][lane] = 0ull;
-  if (lane == 0) s_nan[w] = 0ull;
+  if (!ST || w == 0) {  // (the walk's first barrier orders these before any pass B)
+    s_key[kw][lane] = 0ull;
+    if (lane == 0) s_nan[kw] = 0ull;
+  }
   // this wave's row centres relative to its first row
   const float ysub = px_cy(M, H, t.WY0);
   float drow[8];
@@ -130,6 +143,9 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
     s_cull[0][k] = a.bb.cull[2 * fi];
     s_cull[1][k] = a.bb.cull[2 * fi + 1];
   };
+  // the pixel origin of sub-list s (items mode)
+  auto sub_x0 = [&](int s) { return NS == 1 ? t.WX0 : t.X0 + (s & 1) * 8; };
+  auto sub_y0 = [&](int s) { return NS == 1 ? t.WY0 : t.Y0 + (s >> 1) * 8; };
   // B: the reference's per-pixel test (rasterization_cuda.cu:131-162) over the current batch
   auto test_batch = [&](int total) {
     if (ablate(fs.dbg, 16)) return;
@@ -138,20 +154,24 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
       const int e = e0 + lane;
       if (e < total) {
         const int pr = s_pair[w][e];
-        const int q = pr >> 8, k = L.sub[w][pr & 255];
-        const float x0 = sx * (float)(2 * (t.WX0 + (q & 7)) + 1 - W);
-        const float y0 = sy * (float)(H - 2 * (t.WY0 + (q >> 3)) - 1);
+        // pair: (sub-list << 14) | (pixel << 8) | entry (items mode); (pixel << 8) | entry
+        const int ps = kItems ? (NS == 1 ? 0 : pr >> 14) : w;
+        const int q = (pr >> 8) & 63, k = L.sub[ps][pr & 255];
+        const int ox = kItems ? sub_x0(ps) : t.WX0, oy = kItems ? sub_y0(ps) : t.WY0;
+        const int krow = kItems ? ps : kw;
+        const float x0 = sx * (float)(2 * (ox + (q & 7)) + 1 - W);
+        const float y0 = sy * (float)(H - 2 * (oy + (q >> 3)) - 1);
         float w0, w1, w2, z0;
         if (raster_face_test<float, false>(x0, y0, s_geo[0][k], s_geo[1][k], s_geo[2][k],
                                            s_geo[3][k], s_geo[4][k], s_geo[5][k], s_geo[6][k],
                                            s_geo[7][k], s_geo[8][k], a.eps, w0, w1, w2, z0)) {
           if (isnan(z0)) {
-            atomicOr(&s_nan[w], 1ull << q);
+            atomicOr(&s_nan[krow], 1ull << q);
           } else if (z0 != -INFINITY) {
             const unsigned long long key =
                 ((unsigned long long)ordered_f32(z0) << 32) |
                 (unsigned long long)(0xffffffffu - (uint32_t)L.f[k]);
-            atomicMax(&s_key[w][q], key);
+            atomicMax(&s_key[krow][q], key);
           }
         }
       }
@@ -159,27 +179,53 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
     wave_lds_sync();
   };
   auto round = [&](int nsub, int) {
-    if (nsub == 0 || ablate(fs.dbg, 1)) return;
+    if (ablate(fs.dbg, 1)) return;
+    if (!kItems && nsub == 0) return;
     int total = 0;
+    // items mode: item i = (sub-list s, chunk c) in sub-list order, wave w takes i = w, w + 4, ...
+    int nci[4] = {0, 0, 0, 0}, nitems = 0;
+    if (kItems) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        nci[s] = (L.nsub[s] + kWave - 1) / kWave;
+        nitems += nci[s];
+      }
+    }
 #pragma unroll 1
-    for (int c = 0; c < 4; ++c) {
-      if (c * kWave >= nsub) break;
+    for (int it = kItems ? w : 0; kItems ? it < nitems : it < 4; it += kItems ? 4 : 1) {
+      int s = w, c = it;
+      if (kItems) {
+        s = 0;  // (unrolled: nci stays in registers)
+#pragma unroll
+        for (int q = 0; q < NS - 1; ++q)
+          if (s == q && c >= nci[q]) {
+            c -= nci[q];
+            s = q + 1;
+          }
+      } else if (c * kWave >= nsub) {
+        break;
+      }
+      const int ls = NS == 1 ? 0 : s;  // the sub-list (ST: every wave built the same one)
+      const int ns = kItems ? L.nsub[ls] : nsub;
+      const int ox = kItems ? sub_x0(s) : t.WX0, oy = kItems ? sub_y0(s) : t.WY0;
+      const float ysb = kItems ? px_cy(M, H, oy) : ysub;
       // A: lane = face (chunk entry c*64 + lane): culled row intervals -> 64-bit pixel mask
       const int j = c * kWave + lane;
       uint64_t fm = 0ull;
-      if (j < nsub) {
-        const int k = L.sub[w][j];
+      if (j < ns) {
+        const int k = L.sub[ls][j];
         const Span sp = L.span[k];
-        const int rx0 = max(sp.x0 - t.WX0, 0), rx1 = min(sp.x1 - t.WX0, 7);
-        const int ry0 = max(sp.y0 - t.WY0, 0), ry1 = min(sp.y1 - t.WY0, 7);
+        const int rx0 = max(sp.x0 - ox, 0), rx1 = min(sp.x1 - ox, 7);
+        const int ry0 = max(sp.y0 - oy, 0), ry1 = min(sp.y1 - oy, 7);
         // face frame -> this sub-tile: columns shift by WX0 - span.x0, rows by the centre offset
-        const float xo = (float)(t.WX0 - sp.x0);
-        const float dref = ysub - px_cy(M, H, sp.y0);
+        const float xo = (float)(ox - sp.x0);
+        const float dref = ysb - px_cy(M, H, sp.y0);
         const float4 cl = s_cull[0][k], ch = s_cull[1][k];
         const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          const float d = drow[r] + dref;
+          // (items mode: the item's sub-tile's row offsets)
+          const float d = (kItems ? px_cy(M, H, oy + r) - ysb : drow[r]) + dref;
           const float plo = fmaxf(fmaf(cl.y, d, l0), fmaf(cl.w, d, l2)) - kSlack;
           const float phi = fminf(fmaf(ch.y, d, h0), fmaf(ch.w, d, h2)) + kSlack;
           const int xs = max((int)ceilf(__builtin_amdgcn_fmed3f(plo, -1.f, 9.f)), rx0);
@@ -195,7 +241,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
       const int incl = wave_incl_scan(cnt);
       int end_tot = total + __builtin_amdgcn_readlane(incl, 63);
       int pos = total + incl - cnt;
-      const int qbits = (lane << 8) | (c << 6);
+      const int qbits = (kItems && NS > 1 ? (s << 14) : 0) | (lane << 8) | (c << 6);
       while (true) {
         while (m && pos < kRasterPairCap) {
           s_pair[w][pos++] = (unsigned short)(qbits | (int)__builtin_ctzll(m));
@@ -212,12 +258,12 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   };
   tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
 
-  if (!t.inimg || ablate(fs.dbg, 8192)) return;
+  if (!t.inimg || (ST && w != 0) || ablate(fs.dbg, 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const float x0 = px_cx(M, W, t.px), y0 = px_cy(M, H, t.py);
   int best = -1;
   float bw0 = 0.f, bw1 = 0.f, bw2 = 0.f;
-  if ((s_nan[w] >> lane) & 1ull) {
+  if ((s_nan[kw] >> lane) & 1ull) {
     // the reference's sequential loop over this pixel's coarse bin (ascending faces)
     const BinGeom &g = a.bb.g;
     const int ct = (t.py >> g.sh) * g.nctx + (t.px >> g.sh);
@@ -241,8 +287,8 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
       bw1 = w1;
       bw2 = w2;
     }
-  } else if (s_key[w][lane] != 0ull) {
-    best = (int)(0xffffffffu - (uint32_t)(s_key[w][lane] & 0xffffffffull));
+  } else if (s_key[kw][lane] != 0ull) {
+    best = (int)(0xffffffffu - (uint32_t)(s_key[kw][lane] & 0xffffffffull));
     float v[6];
     load_corners(fs, lo + best, v);
     const float *zz = a.fvz + (lo + best) * a.fvz_fs;

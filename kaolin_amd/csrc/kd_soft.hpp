@@ -220,10 +220,11 @@ struct SoftPairBuf {
   int64_t *tbase;      // [tiles] first record of each tile
   int32_t *npix;       // [P] close faces of each uncovered pixel (split pipeline)
   int32_t *ntile;      // [tiles] records of each tile
-  PairItem *items;     // [cap / 256 + tiles]
+  PairItem *items;     // [cap / 256 + 4 tiles]
   int32_t *tiles;      // [tiles] tiles with records (split pipeline's reduce)
-  int32_t *ovf;        // [tiles] tiles that computed their soft mask without records
-  int32_t *counters;   // [4]: items, tiles with records, overflow tiles, unused; then the 64-bit
+  int32_t *ovf;        // [4 tiles] tiles (small batch: 4 tile + quadrant) that computed their soft mask without records
+  int32_t *counters;   // [4]: items, tiles with records, overflow tiles, small-batch flag (1: the
+                       // forward ran kd_dibr_fwd_st, overflow entries are 4 tile + quadrant); then the 64-bit
                        // record cursor (all zeroed by kd_bin_count: n_clear = 6)
   unsigned long long *cursor;
   int64_t ntiles, npixels, cap, lim;  // lim: records a forward may use (kd_set_pool_limits)
@@ -234,7 +235,8 @@ struct SoftPairBuf {
 constexpr int kPairClear = 6;  // ints of SoftPairBuf::counters (with the cursor) to zero
 
 // bins + pair buffers for B views of F faces, K close faces, element size esize
-size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize);
+size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize,
+                                 int ct0 = kCoarseTile0);
 // pair buffers carved from a workspace after the soft mask's bins
 template <typename T>
 SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K);
@@ -246,6 +248,18 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
 // the backward over the records of soft_pairs_launch(grad = true), adding into a.grad_fvi
 template <typename T>
 int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream);
+// Small-batch mode of dibr_rasterization (fp32): few enough 16x16 tiles that the tile grid is
+// about one round of workgroup slots -- the forward then runs one workgroup per 8x8 quadrant over
+// 16-pixel coarse bins (kd_dibr_fwd_st).  A function of the call's sizes only, so the forward and
+// the backward carve the same workspace.
+constexpr int64_t kSmallBatchTiles = 2048;  // B x 16x16 tiles
+inline bool dibr_small_batch(int B, int H, int W, int esize) {
+  const int64_t tiles = (int64_t)B * ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+  return esize == 4 && tiles > 0 && tiles <= kSmallBatchTiles && !(debug_flags() & (1 << 27));
+}
+inline int dibr_ct0(int B, int H, int W, int esize) {
+  return dibr_small_batch(B, H, W, esize) ? kTile : kCoarseTile0;
+}
 // The raster forward (fp32 pair pipeline) and the fused soft mask in one launch, when both apply.
 template <typename T>
 struct RasterFwdArgs;

@@ -161,6 +161,76 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_atomic(
   }
 }
 
+// The same backward over given close lists, read in memory order: per 256-pixel block, the
+// uncovered pixels whose first slot holds a face are compacted in LDS; then each half-wave (K <=
+// 32) or wave (K > 32, 64 slots at a time) takes one listed pixel's row of K slots -- consecutive
+// lanes, consecutive elements -- and its lanes up to the row's first -1 (a ballot: the
+// reference's loop stops there, dibr_soft_mask_cuda.cu:273-276) add their pair's terms.  The
+// lane-per-pixel form read each row with one lane (K strided loads per pixel).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
+    int B, int H, int W, int64_t F, int K, const T *__restrict__ grad_soft,
+    const T *__restrict__ soft, const int64_t *__restrict__ face_idx, const T *__restrict__ prob,
+    const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
+    const T *__restrict__ fvi, float sigmainv, float M, T *grad_fvi) {
+  __shared__ int64_t s_pix[kBlock];
+  __shared__ int s_cnt[kBlock / kWave];
+  const int64_t P = (int64_t)H * W;
+  const int64_t total = (int64_t)B * P;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  auto pair = [&](int64_t p, int s) {  // one (pixel, slot) entry holding face >= 0
+    const int64_t e = p * K + s;
+    const int64_t f = cidx[e];
+    const int64_t b = p / P;
+    const int64_t rem = p - b * P;
+    const int h = (int)(rem / W), x = (int)(rem - (int64_t)h * W);
+    const int64_t sf = b * F + f;
+    T v[6];
+#pragma unroll
+    for (int c = 0; c < 6; ++c) v[c] = fvi[sf * 6 + c];
+    T g[6] = {0, 0, 0, 0, 0, 0};
+    soft_bwd_terms<T>((T)px_cx(M, W, x), (T)px_cy(M, H, h), v, (int)ctype[e] - 1, prob[e],
+                      grad_soft[p], soft[p], sigmainv, M, g);
+#pragma unroll
+    for (int c = 0; c < 6; ++c)
+      if (g[c] != (T)0) atomicAdd(grad_fvi + sf * 6 + c, g[c]);
+  };
+  for (int64_t p0 = (int64_t)blockIdx.x * kBlock; p0 < total; p0 += (int64_t)gridDim.x * kBlock) {
+    const int64_t p = p0 + threadIdx.x;
+    const bool live = p < total && face_idx[p] < 0 && cidx[p * K] >= 0;
+    int n;
+    const int pos = wg_compact(live, s_cnt, n);
+    if (live) s_pix[pos] = p;
+    __syncthreads();
+    if (K <= 32) {  // two rows per wave step (half-waves), rows dealt to the waves in turn
+      const int half = lane >> 5, s = lane & 31;
+      for (int i0 = 2 * w; i0 < n; i0 += 2 * (kBlock / kWave)) {
+        const int i = i0 + half;
+        const int64_t pp = i < n ? s_pix[i] : 0;
+        const bool in = i < n && s < K;
+        const bool stop = !in || cidx[pp * K + s] < 0;
+        const uint64_t sm = __ballot(stop);
+        const uint32_t hm = (uint32_t)(sm >> (32 * half));  // this half's stops
+        const int first = hm ? __builtin_ctz(hm) : 32;
+        if (in && s < first) pair(pp, s);
+      }
+    } else {  // one row per wave, 64 slots at a time until its first -1
+      for (int i = w; i < n; i += kBlock / kWave) {
+        const int64_t pp = s_pix[i];
+        for (int s0 = 0; s0 < K; s0 += kWave) {
+          const int s = s0 + lane;
+          const bool stop = s >= K || cidx[pp * K + s] < 0;
+          const uint64_t sm = __ballot(stop);
+          const int first = sm ? __builtin_ctzll(sm) : kWave;
+          if (lane < first) pair(pp, s);
+          if (sm) break;
+        }
+      }
+    }
+    __syncthreads();  // s_pix is reused by the next block of pixels
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
@@ -208,9 +278,15 @@ int soft_backward(int B, int H, int W, int64_t F, int K, const T *grad_soft, con
   if (total > 0 && nf > 0 && K > 0) {
     const int64_t blocks = (total + kBlock - 1) / kBlock;
     ProfScope prof(K_SOFT_BWD_ATOMIC, stream);
-    hipLaunchKernelGGL(kd_soft_bwd_atomic<T>, dim3((unsigned)(blocks < 65536 ? blocks : 65536)),
-                       dim3(kBlock), 0, stream, B, H, W, F, K, grad_soft, soft, face_idx, prob,
-                       cidx, ctype, fvi, sigmainv, M, grad_fvi);
+    const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
+    if (debug_flags() & (1 << 29))  // diagnostics: the lane-per-pixel form
+      hipLaunchKernelGGL(kd_soft_bwd_atomic<T>, dim3(grid), dim3(kBlock), 0, stream, B, H, W, F,
+                         K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
+                         grad_fvi);
+    else
+      hipLaunchKernelGGL(kd_soft_bwd_lists<T>, dim3(grid), dim3(kBlock), 0, stream, B, H, W, F,
+                         K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
+                         grad_fvi);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));

@@ -50,19 +50,22 @@ static int64_t pool_records(int B, int H, int W, int K) {
   return (int64_t)B * ntiles * kBlock * std::min(K, kPoolPairsPerPixel);
 }
 
-size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize) {
+size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int K, int esize,
+                                 int ct0) {
   const int64_t ntiles = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
   const int64_t tiles = (int64_t)B * ntiles, P = (int64_t)B * H * W;
   const int64_t recs = pool_records(B, H, W, K);
-  size_t s = bin_workspace_bytes(B, H, W, N, F);
+  size_t s = bin_workspace_bytes(B, H, W, N, F, ct0);
   s += align_up(sizeof(SoftPairRec) * (size_t)recs);
   s += align_up((size_t)esize * (size_t)recs);
   s += align_up(sizeof(int64_t) * (size_t)tiles);
   s += align_up(sizeof(int32_t) * (size_t)P);
   s += align_up(sizeof(int32_t) * (size_t)tiles);
-  s += align_up(sizeof(PairItem) * (size_t)(recs / kBlock + tiles));
+  // items: a workgroup's n records take ceil(n / 256) items; the small-batch forward runs four
+  // workgroups per tile.  Overflow entries: up to one per (tile, quadrant).
+  s += align_up(sizeof(PairItem) * (size_t)(recs / kBlock + 4 * tiles));
   s += align_up(sizeof(int32_t) * (size_t)tiles);
-  s += align_up(sizeof(int32_t) * (size_t)tiles);
+  s += align_up(sizeof(int32_t) * (size_t)(4 * tiles));
   s += align_up(sizeof(int32_t) * 8);
   return s;
 }
@@ -89,11 +92,11 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   pb.ntile = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.items = (PairItem *)(base + off);
-  off += align_up(sizeof(PairItem) * (size_t)(pb.cap / kBlock + tiles));
+  off += align_up(sizeof(PairItem) * (size_t)(pb.cap / kBlock + 4 * tiles));
   pb.tiles = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.ovf = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * (size_t)tiles);
+  off += align_up(sizeof(int32_t) * (size_t)(4 * tiles));
   pb.counters = (int32_t *)(base + off);
   pb.cursor = (unsigned long long *)(pb.counters + 4);
   off += align_up(sizeof(int32_t) * 8);
@@ -190,15 +193,18 @@ __device__ __forceinline__ uint64_t lowest_bits(uint64_t m, int need) {
 // The faces of one 64-face chunk of a wave's sub-list (lane j = chunk entry j) this pixel lane
 // takes: the first K - kid whose exact enlarged span holds its centre (ascending face index =
 // ascending entry, dibr_soft_mask_cuda.cu:95 and :165-171).
-__device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, int c, bool unc,
-                                                 int K, const TileGeom &t, int kid) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+// The faces of chunk c of sub-list s (lane j = entry c*64 + j) whose exact enlarged span holds
+// this pixel lane's centre (pixel (ox + (lane & 7), oy + (lane >> 3))).  Every lane of the wave
+// must call it (its ballots gather the chunk's faces from all lanes).
+__device__ __forceinline__ uint64_t chunk_hits(const TileLists &L, int s, int nsub, int c, int ox,
+                                               int oy) {
+  const int lane = threadIdx.x & 63;
   const int qx = lane & 7, qy = lane >> 3;
   const int j = c * kWave + lane;
   const bool has = j < nsub;
-  const int k = has ? L.sub[w][j] : 0;
+  const int k = has ? L.sub[s][j] : 0;
   const Span sp = has ? L.span[k] : Span{1, -1, 1, -1};
-  const int x0 = sp.x0 - t.WX0, x1 = sp.x1 - t.WX0, y0 = sp.y0 - t.WY0, y1 = sp.y1 - t.WY0;
+  const int x0 = sp.x0 - ox, x1 = sp.x1 - ox, y0 = sp.y0 - oy, y1 = sp.y1 - oy;
   uint64_t mc = 0ull, mr = 0ull;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
@@ -207,7 +213,14 @@ __device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, i
     mc = (qx == i) ? bc : mc;
     mr = (qy == i) ? br : mr;
   }
-  uint64_t sel = (unc && kid < K) ? (mc & mr) : 0ull;
+  return mc & mr;
+}
+
+__device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, int c, bool unc,
+                                                 int K, const TileGeom &t, int kid) {
+  const int w = threadIdx.x >> 6;
+  uint64_t sel = chunk_hits(L, w, nsub, c, t.WX0, t.WY0);
+  sel = (unc && kid < K) ? sel : 0ull;
   if (__popcll(sel) > K - kid) sel = lowest_bits(sel, K - kid);
   return sel;
 }
@@ -216,14 +229,16 @@ __device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, i
 // Records are placed face-major (face j's pixels contiguous, pixels ascending): the transposed
 // selections give each face its record count and offset; each pixel lane then writes its own
 // records (slot = its running close-face count) at offset[j] + rank of the pixel in face j.
-__device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
-                                                   int K, const TileGeom &t, int64_t lo,
-                                                   int &my_kid, uint64_t *s_pm,
-                                                   unsigned short *s_off, int *s_nrec,
-                                                   SoftPairRec *rec,
-                                                   unsigned short (*s_ridx)[kBlock] = nullptr) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
+// The record writes of one chunk for a selection `sel` (pixel lane: its faces of the chunk),
+// slots from my_kid on (advanced).  tile_q: the pixel's thread index in the 16x16 tile frame (the
+// record's q); ridx_q: its column of the (slot, pixel) record table.
+__device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uint64_t sel, int c,
+                                                 int64_t lo, int &my_kid, uint64_t *s_pm,
+                                                 unsigned short *s_off, int *s_nrec,
+                                                 SoftPairRec *rec,
+                                                 unsigned short (*s_ridx)[kBlock], int tile_q,
+                                                 int ridx_q) {
+  const int lane = threadIdx.x & 63;
   // face lanes: pixel masks, record counts and offsets
   const uint64_t pm = wave_transpose64(sel);
   const int cnt = __popcll(pm);
@@ -238,11 +253,10 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
   wave_lds_sync();
   // pixel lanes: write own records, slots ascending with the face index
   const uint64_t below = (1ull << lane) - 1ull;
-  const int tile_q = w * kWave + lane;
   int slot = my_kid;
   for (uint64_t m = sel; m; m &= m - 1ull) {
     const int jj = __builtin_ctzll(m);
-    const int kk = L.sub[w][c * kWave + jj];
+    const int kk = L.sub[ls][c * kWave + jj];
     SoftPairRec r;
     r.row = (int32_t)(lo + L.f[kk]);
     r.slot = (uint16_t)slot++;
@@ -250,10 +264,106 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
     r.type = 0;
     const int ri = base + s_off[jj] + __popcll(s_pm[jj] & below);
     rec[ri] = r;
-    if (s_ridx) s_ridx[r.slot][tile_q] = (unsigned short)ri;  // (slot, pixel) -> record
+    if (s_ridx) s_ridx[r.slot][ridx_q] = (unsigned short)ri;  // (slot, pixel) -> record
   }
   my_kid = slot;
   wave_lds_sync();
+}
+
+__device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
+                                                   int K, const TileGeom &t, int64_t lo,
+                                                   int &my_kid, uint64_t *s_pm,
+                                                   unsigned short *s_off, int *s_nrec,
+                                                   SoftPairRec *rec,
+                                                   unsigned short (*s_ridx)[kBlock] = nullptr) {
+  const int tile_q = threadIdx.x;
+  const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
+  soft_chunk_write(L, threadIdx.x >> 6, sel, c, lo, my_kid, s_pm, s_off, s_nrec, rec, s_ridx,
+                   tile_q, tile_q);
+}
+
+// Balanced pass A (BAL, and the small-batch mode ST): one batch of the walk, its (sub-list s,
+// 64-face chunk c) items dealt to the waves in turn (item i = w, w + 4, ...), so a long sub-list
+// is worked on by every wave.  Slots follow the face order across the chunks: each item counts its
+// chunk's hits per pixel (capped at the pixel's remaining room), the counts of the sub-list's lower
+// chunks give each chunk's first slot, and the pixel's close-face count kid advances by the batch's
+// total (at most K).  NS = 4: sub-list s is sub-tile s's (pixel thread s * 64 + lane of the tile);
+// NS = 1 (ST): one sub-list (every wave built the same) for quadrant `quad`.  Called by every
+// thread of the workgroup (barriers inside).
+struct SoftItemsLDS {
+  uint64_t umask[4];                   // uncovered pixels of each sub-tile
+  unsigned char kid[4][kWave];         // close faces so far per pixel (knum <= kFuseSlots)
+  unsigned char hits[4][4][kWave];     // per (sub-tile, chunk) selected hits of the batch
+};
+
+template <int NS>
+__device__ __forceinline__ void soft_round_items(const TileLists &L, int K, const TileGeom &t,
+                                                 int64_t lo, int quad, SoftItemsLDS &B,
+                                                 uint64_t *s_pm, unsigned short *s_off,
+                                                 int *s_nrec, SoftPairRec *rec,
+                                                 unsigned short (*s_ridx)[kBlock]) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int nci[4] = {0, 0, 0, 0}, nitems = 0;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    nci[s] = B.umask[s] ? (L.nsub[s] + kWave - 1) / kWave : 0;
+    nitems += nci[s];
+  }
+  auto origin = [&](int s, int &ox, int &oy) {
+    ox = NS == 1 ? t.WX0 : t.X0 + (s & 1) * 8;
+    oy = NS == 1 ? t.WY0 : t.Y0 + (s >> 1) * 8;
+  };
+  // item it -> (sub-list s, chunk c) (unrolled: nci stays in registers)
+  auto item = [&](int it, int &s, int &c) {
+    s = 0;
+    c = it;
+#pragma unroll
+    for (int q = 0; q < NS - 1; ++q)
+      if (s == q && c >= nci[q]) {
+        c -= nci[q];
+        s = q + 1;
+      }
+  };
+  // the item's hits of this pixel lane (chunk_hits' ballots run on the whole wave: lane j is
+  // also face j of the chunk)
+  auto hits = [&](int s, int c) {
+    int ox, oy;
+    origin(s, ox, oy);
+    const uint64_t h = chunk_hits(L, s, L.nsub[s], c, ox, oy);
+    const bool unc = (B.umask[s] >> lane) & 1ull;
+    return (unc && B.kid[s][lane] < K) ? h : 0ull;
+  };
+  // phase 1: counts (at most 16 items: 4 sub-lists x 256 faces)
+  for (int it = w; it < nitems; it += 4) {
+    int s, c;
+    item(it, s, c);
+    const int n = __popcll(hits(s, c));
+    B.hits[s][c][lane] = (unsigned char)min(n, K - (int)B.kid[s][lane]);
+  }
+  __syncthreads();
+  // phase 2: each chunk's first slot from its sub-list's lower chunks; the masks are recomputed
+  // (cheaper than holding them across the barrier at this register budget)
+  for (int it = w; it < nitems; it += 4) {
+    int s, c;
+    item(it, s, c);
+    int slot = B.kid[s][lane];
+    for (int v = 0; v < c; ++v) slot += B.hits[s][v][lane];
+    const int need = K - slot;
+    uint64_t h = hits(s, c);  // (whole wave: chunk_hits' ballots)
+    if (need <= 0)
+      h = 0ull;
+    else if (__popcll(h) > need)
+      h = lowest_bits(h, need);
+    if (__ballot(h != 0ull))
+      soft_chunk_write(L, s, h, c, lo, slot, s_pm, s_off, s_nrec, rec, s_ridx,
+                       (NS == 1 ? quad : s) * kWave + lane, (NS == 1 ? 0 : s) * kWave + lane);
+  }
+  __syncthreads();  // every wave has read kid / hits
+  if (w < NS) {
+    int tot = B.kid[w][lane];
+    for (int v = 0; v < nci[w]; ++v) tot += B.hits[w][v][lane];
+    B.kid[w][lane] = (unsigned char)min(K, tot);
+  }
 }
 
 // The streaming form of one chunk (a tile without records): the pixel lane visits the same
@@ -281,14 +391,17 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
   const int novf = pb.counters[2];
+  const bool st = pb.counters[3] == 1;  // entries are 4 tile + quadrant (kd_dibr_fwd_st)
   for (int i = blockIdx.x; i < novf; i += gridDim.x) {
-    const int64_t tile = pb.ovf[i];
+    const int64_t ent = pb.ovf[i];
+    const int64_t tile = st ? ent >> 2 : ent;
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
     int64_t lo, hi;
     view_range(fs, b, lo, hi);
-    const TileGeom t = tile_geom(H, W, tl);
+    const TileGeom t = st ? tile_geom_st(H, W, tl, (int)(ent & 3)) : tile_geom(H, W, tl);
     const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-    const bool unc = t.inimg && a.face_idx[p] < 0;
+    // (ST: wave 0 owns the quadrant's pixels; the other waves only walk)
+    const bool unc = t.inimg && (!st || threadIdx.x < kWave) && a.face_idx[p] < 0;
     const bool wave_unc = __ballot(unc) != 0ull;
     const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
     int my_kid = 0;
@@ -318,6 +431,12 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
     if (__syncthreads_or(unc))
       tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg, done);
     if (unc && my_kid > 0 && a.soft) a.soft[p] = (T)(1.0 - (double)prod);
+    if (!FUSED && a.prob && t.inimg && (!st || threadIdx.x < kWave))
+      for (int s = my_kid; s < K; ++s) {  // the -1 / 0 / 0 padding (kd_soft_lists skips the tile)
+        a.prob[p * K + s] = (T)0;
+        a.cidx[p * K + s] = -1;
+        a.ctype[p * K + s] = 0;
+      }
     __syncthreads();
   }
 }
@@ -360,6 +479,21 @@ __device__ __forceinline__ void iou_tile_terms(const SoftArgs<T> &a, int b, int 
   }
 }
 
+// Side job of the fused forward launches: the backward's gradient buffers, zeroed grid-stride
+// (coalesced) by every workgroup of the grid -- also by those without a tile.
+template <typename T>
+__device__ __forceinline__ void zero_side_job(const SoftArgs<T> &a) {
+  const int64_t nz = a.nzero0 + a.nzero1;
+  const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
+  for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x; i < nz;
+       i += nblk * kBlock) {
+    if (i < a.nzero0)
+      a.zero0[i] = (T)0;
+    else
+      a.zero1[i - a.nzero0] = (T)0;
+  }
+}
+
 template <bool FUSED>
 struct SoftPairsLDS {
   unsigned short ridx[FUSED ? kFuseSlots : 1][kBlock];
@@ -369,29 +503,55 @@ struct SoftPairsLDS {
   int64_t base;
   int nrec, ibase, box[4];
   double iou[8];  // iou_tile_terms
+  SoftItemsLDS it;  // BAL / ST pass A (soft_round_items)
+  int wbox[4][4];   // per wave: the box of its pixels that can still take a face (walk filter)
 };
 
 // Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
 // (t.px, t.py) of tile_geom(H, W, tl); a.face_idx of that pixel is read by the same thread (the
 // fused forward wrote it in the same workgroup, same thread).
-template <typename T, bool FUSED>
+// BAL (FUSED only): pass A deals the batch's (sub-tile, chunk) items to the waves in turn
+// (soft_round_items), so a silhouette sub-tile with a long list is worked on by every wave.
+// ST (small-batch mode, FUSED only): quadrant `quad` of the tile (tile_geom_st); the four waves
+// share its 64 pixels (wave 0 owns them: soft values, product, IoU terms), pass A deals its
+// chunks to the four waves (soft_round_items), the pair math runs on all 256 threads; the
+// quadrant's records sit in its quarter of the tile's room, with the tile frame's pixel index.
+template <typename T, bool FUSED, bool ST = false, bool BAL = false>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
-                                                int b, int tl, int nbin, SoftPairsLDS<FUSED> &S) {
+                                                int b, int tl, int nbin, SoftPairsLDS<FUSED> &S,
+                                                int quad = 0) {
+  static_assert(!(ST || BAL) || FUSED, "the balanced / small-batch modes are the fused soft mask");
+  constexpr bool kItems = ST || BAL;
   TileLists &L = S.L;
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const bool own = !ST || w == 0;  // this thread writes its pixel's results
   const float M = fs.M;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   const int nview = (int)(hi - lo);
-  TileGeom t = tile_geom(H, W, tl);
+  TileGeom t = ST ? tile_geom_st(H, W, tl, quad) : tile_geom(H, W, tl);
   t.nbin = nbin;
   if (KD_DIAG && fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, bin) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-  const bool unc = t.inimg && a.face_idx[p] < 0;
+  bool unc;
+  if constexpr (ST) {  // wave 0 wrote the quadrant's face_idx: it hands the mask to the others
+    if (w == 0) {
+      const uint64_t m = __ballot(t.inimg && a.face_idx[p] < 0);
+      if (lane == 0) S.it.umask[0] = m;
+    }
+    __syncthreads();
+    unc = (S.it.umask[0] >> lane) & 1ull;
+  } else {
+    unc = t.inimg && a.face_idx[p] < 0;
+    if (BAL) {  // (the walk's first barrier orders these before pass A)
+      const uint64_t m = __ballot(unc);
+      if (lane == 0) S.it.umask[w] = m;
+    }
+  }
   const bool wave_unc = __ballot(unc) != 0ull;
   const int64_t tile = (int64_t)b * pb.ntiles + tl;
   int my_kid = 0;
@@ -406,6 +566,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     S.nrec = 0;
     S.base = -1;
   }
+  if (kItems && (BAL || w == 0)) S.it.kid[w][lane] = 0;
   {
     const uint64_t um = __ballot(unc);
     t.wave_live = t.wave_live && um != 0ull;
@@ -426,7 +587,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     atomicMin(&s_box[2], t.SY0);
     atomicMax(&s_box[3], t.SY1);
   }
-  const int U = __syncthreads_count(unc);
+  const int U = __syncthreads_count(unc && own);
   bool ovf = false;
   if (U > 0) {
     // the tile's room in the pool: its own 256 K records (`fixed`), or, reserved with one device
@@ -434,7 +595,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     // latency overlaps the walk's first loads (records are written after a barrier of
     // tile_rounds)
     if (pb.fixed) {
-      if (tid == 0) S.base = tile * kBlock * K;
+      if (tid == 0) S.base = tile * kBlock * K + (ST ? (int64_t)quad * kWave * K : 0);
     } else if (tid == 0) {
       const BinGeom &g = a.bb.g;
       const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
@@ -452,15 +613,61 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     t.FY1 = s_box[3];
     auto stage = [&](int, int64_t) {};  // pass A needs the spans only
     auto round = [&](int nsub, int) {
-      if (wave_unc && !ablate(fs.dbg, 1024))
+      if constexpr (kItems) {
+        soft_round_items<ST ? 1 : 4>(L, K, t, lo, quad, S.it, S.pm[w], S.off[w], &S.nrec,
+                                     pb.rec + S.base, S.ridx);
+      } else if (wave_unc && !ablate(fs.dbg, 1024)) {
         for (int c = 0; c * kWave < nsub; ++c)
           soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], &S.nrec,
                              pb.rec + S.base, FUSED ? S.ridx : nullptr);
+      }
     };
     // once every uncovered pixel holds K close faces, later faces cannot enter; a tile without
-    // room in the pool stops at the first barrier
+    // room in the pool stops at the first barrier.  Otherwise the walk's filter boxes shrink to
+    // the pixels that can still take a face (uncovered, fewer than K so far): a later face whose
+    // enlarged span reaches none of them cannot enter any list, so the next batches' tile list
+    // and sub-lists hold only faces that can (exact, like the first filter)
     auto done = [&]() {
-      return __syncthreads_and(!unc || my_kid >= K) != 0 || S.base == -2;
+      const int kk = kItems ? (int)S.it.kid[ST ? 0 : w][lane] : my_kid;
+      const bool open = unc && kk < K;
+      const uint64_t om = __ballot(open);
+      int bx0 = 1 << 30, bx1 = -1, by0 = 1 << 30, by1 = -1;
+      if (om) {
+        uint32_t cols = 0u;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cols |= (uint32_t)(om >> (8 * r)) & 0xffu;
+        bx0 = t.WX0 + __builtin_ctz(cols);
+        bx1 = t.WX0 + 31 - __builtin_clz(cols);
+        by0 = t.WY0 + __builtin_ctzll(om) / 8;
+        by1 = t.WY0 + (63 - __builtin_clzll(om)) / 8;
+      }
+      if (lane == 0) {
+        S.wbox[w][0] = bx0;
+        S.wbox[w][1] = bx1;
+        S.wbox[w][2] = by0;
+        S.wbox[w][3] = by1;
+      }
+      const bool all = __syncthreads_and(!open) != 0 || S.base == -2;
+      if (!all) {
+        t.wave_live = om != 0ull;
+        t.SX0 = bx0;
+        t.SX1 = bx1;
+        t.SY0 = by0;
+        t.SY1 = by1;
+        int fx0 = S.wbox[0][0], fx1 = S.wbox[0][1], fy0 = S.wbox[0][2], fy1 = S.wbox[0][3];
+#pragma unroll
+        for (int v = 1; v < 4; ++v) {
+          fx0 = min(fx0, S.wbox[v][0]);
+          fx1 = max(fx1, S.wbox[v][1]);
+          fy0 = min(fy0, S.wbox[v][2]);
+          fy1 = max(fy1, S.wbox[v][3]);
+        }
+        t.FX0 = fx0;
+        t.FX1 = fx1;
+        t.FY0 = fy0;
+        t.FY1 = fy1;
+      }
+      return all;
     };
     // (S.base == -2 is visible from tile_rounds' first barrier on, before any record is written)
     auto round_checked = [&](int nsub, int cnt) {
@@ -469,33 +676,33 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     tile_rounds(L, a.bb, nview, b, lo, t, stage, round_checked, fs.dbg, done);
     __syncthreads();
     ovf = S.base == -2;
+    if (KD_DIAG && fs.tbuf && tid == 0 && FUSED)  // diagnostics: end of pass A
+      fs.tbuf[5ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
+          wall_clock64();
+    if (kItems) my_kid = S.it.kid[ST ? 0 : w][lane];
   }
   if (ovf) {  // no records: kd_soft_ovf_fwd computes the tile's soft mask, kd_soft_ovf_bwd its
-              // backward
+              // backward (ST: the quadrant's, entry 4 tile + quadrant)
     my_kid = 0;
     if (tid == 0) {
-      pb.ovf[atomicAdd(&pb.counters[2], 1)] = (int32_t)tile;
+      pb.ovf[atomicAdd(&pb.counters[2], 1)] = ST ? (int32_t)(4 * tile + quad) : (int32_t)tile;
       S.nrec = 0;
     }
   }
   T sval = unc ? (T)0.0 : (T)1.0;  // this pixel's soft value (FUSED: the product below)
-  if (t.inimg) {
+  if (t.inimg && own) {
     if (!FUSED) pb.npix[p] = my_kid;  // the split pipeline's reduce
     if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
     else if (a.soft && my_kid == 0) a.soft[p] = (T)0.0;
     if (a.last && my_kid < K) a.last[p] = -1;
-    if (a.prob)  // -1 / 0 / 0 padding (dibr_soft_mask.cpp:86-97 pre-fill)
-      for (int s = my_kid; s < K; ++s) {
-        a.prob[p * K + s] = (T)0;
-        a.cidx[p * K + s] = -1;
-        a.ctype[p * K + s] = 0;
-      }
+    // (the close lists, values and -1 / 0 / 0 padding alike, are written row-coalesced by
+    // kd_soft_lists)
   }
   __syncthreads();
   const int n = S.nrec;
   const int64_t base = S.base;
-  if (tid == 0) {
-    pb.ntile[tile] = n;
+  if (tid == 0 && !ST) {  // (ST: four workgroups share the tile; the fused path never reads these)
+    pb.ntile[tile] = ovf ? -1 : n;  // -1: kd_soft_ovf_fwd streams the tile (lists included)
     pb.tbase[tile] = n > 0 ? base : 0;
   }
   if (n > 0) {  // work items of the math and backward passes
@@ -510,25 +717,16 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
           PairItem{base + (int64_t)c * kBlock, (int32_t)tile, min(kBlock, n - c * kBlock)};
   }
   if constexpr (FUSED) {
-    // side job of the launch: the backward's gradient buffers (grid-stride, coalesced)
-    const int64_t nz = a.nzero0 + a.nzero1;
-    const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
-    for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + tid; i < nz;
-         i += nblk * kBlock) {
-      if (i < a.nzero0)
-        a.zero0[i] = (T)0;
-      else
-        a.zero1[i - a.nzero0] = (T)0;
-    }
+    zero_side_job(a);
     if (n == 0) {
-      iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
+      iou_tile_terms<T>(a, b, tl, p, t.inimg && own, sval, S.iou);
       return;
     }
     // pair math over this tile's records (record order: coalesced reads)
     const int tx = tl % pb.ntx, ty = tl / pb.ntx;
     const SoftPairRec *rec = pb.rec + base;
     T *sp = pb.sprob + base;
-    for (int i = tid; i < n; i += kBlock) {
+    for (int i = tid; i < n && !ablate(fs.dbg, 32); i += kBlock) {  // (diag 32: no pair math)
       const SoftPairRec r = rec[i];
       T v[6];
       load_corners(fs, (int64_t)r.row, v);
@@ -543,14 +741,18 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
     }
     __syncthreads();  // the workgroup's probabilities are visible to it
+    if (KD_DIAG && fs.tbuf && tid == 0)  // diagnostics: end of the pair math
+      fs.tbuf[6ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
+          wall_clock64();
     // soft = 1 - prod(1 - p) in slot order (dibr_soft_mask_cuda.cu:174-181, double-promoted)
-    if (unc && my_kid > 0) {
+    if (unc && my_kid > 0 && own) {
       constexpr int U8 = 8;
+      const int rq = ST ? lane : tid;  // the pixel's column of the record table
       T prod = (T)1.0;
       for (int s0 = 0; s0 < my_kid; s0 += U8) {
         T pv[U8];
 #pragma unroll
-        for (int u = 0; u < U8; ++u) pv[u] = s0 + u < my_kid ? sp[S.ridx[s0 + u][tid]] : (T)0;
+        for (int u = 0; u < U8; ++u) pv[u] = s0 + u < my_kid ? sp[S.ridx[s0 + u][rq]] : (T)0;
 #pragma unroll
         for (int u = 0; u < U8; ++u)
           if (s0 + u < my_kid) prod = (T)((double)prod * (1.0 - (double)pv[u]));
@@ -558,7 +760,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       sval = (T)(1.0 - (double)prod);
       a.soft[p] = sval;
     }
-    iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
+    iou_tile_terms<T>(a, b, tl, p, t.inimg && own, sval, S.iou);
   }
 }
 
@@ -586,7 +788,11 @@ union DibrTileLDS {
 // DIAG (debug flag 64 with a debug buffer): per dispatch slot the tile, its bin counts, start,
 // duration and raster-phase end (tools/soft_timeline.py).  A separate instantiation: the clock's
 // live registers alone make the kernel spill.
-template <bool DIAG>
+// BAL: both phases deal their (sub-tile, chunk) items to the four waves in turn (balanced;
+// debug flag 1 << 28).  Measured at C3, 1 / 2 / 8 views: 73 / 81 / 176 us against 67 / 74 / 160
+// for the per-wave form (its extra barriers and per-item bookkeeping cost more than the balance
+// gains), so the production launch is the per-wave form.
+template <bool DIAG, bool BAL>
 __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
                                                               SoftArgs<float> a,
                                                               SoftPairBuf<float> pb) {
@@ -603,12 +809,49 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
     const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
     a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
   }
-  raster_pairs_tile(ra, b, tl, nbin, U.r);
+  raster_pairs_tile<false, BAL>(ra, b, tl, nbin, U.r);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
-  soft_pairs_tile<float, true>(a, pb, b, tl, -1, U.s);
+  soft_pairs_tile<float, true, false, BAL>(a, pb, b, tl, -1, U.s);
+}
+
+// The small-batch form of kd_dibr_fwd_tiles (few views: the grid of 16x16 tiles is about one
+// round of workgroup slots, so the kernel's length is its heaviest tile, not the chip's work):
+// one workgroup per 8x8 quadrant of a tile, over 16-pixel coarse bins, its four waves splitting
+// the quadrant's face chunks in both phases and its pair math (ST bodies above).  A tile's
+// serial work -- the silhouette and pole tiles' walk, pairs and pair math -- spreads over four
+// workgroups and four times the waves.  Same records, outputs and backward as the tile kernel.
+// DIAG: the per-slot timeline of kd_dibr_fwd_tiles<true> (tools/soft_timeline.py), slot = workgroup.
+template <bool DIAG>
+__global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_st(RasterFwdArgs<float> ra,
+                                                            SoftArgs<float> a,
+                                                            SoftPairBuf<float> pb) {
+  __shared__ DibrTileLDS U;
+  TileClock clk(DIAG ? a.fs.tbuf : nullptr, 1);
+  if (DIAG) clk.start_to(2);
+  int b, tl, nbin, quad;
+  // the overflow kernels' mode flag (counters[3], zeroed by kd_bin_count): overflow entries are
+  // (tile, quadrant) pairs
+  if (blockIdx.x == 0 && threadIdx.x == 0) pb.counters[3] = 1;
+  if (!st_of_block(ra.bb, ra.fs.B, ra.fs.H, ra.fs.W, b, tl, nbin, quad)) {
+    zero_side_job(a);  // (the grid is padded to whole groups of 32)
+    return;
+  }
+  if (DIAG && a.fs.tbuf && threadIdx.x == 0) {
+    const int64_t nb = gridDim.x, slot = blockIdx.x;
+    a.fs.tbuf[slot] = ((long long)nbin << 32) | (long long)(4 * (b * pb.ntiles + tl) + quad);
+    const BinGeom &g = a.bb.g;
+    const int tx = tl % pb.ntx, ty = tl / pb.ntx;
+    const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
+    a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
+  }
+  raster_pairs_tile<true>(ra, b, tl, nbin, U.r, quad);
+  __syncthreads();  // the raster phase is done with the LDS
+  if (DIAG && a.fs.tbuf && threadIdx.x == 0)
+    a.fs.tbuf[3ll * gridDim.x + blockIdx.x] = wall_clock64();
+  soft_pairs_tile<float, true, true>(a, pb, b, tl, -1, U.s, quad);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -666,6 +909,81 @@ __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPair
   for (int ti = blockIdx.x; ti < ntl; ti += gridDim.x) soft_reduce_tile<T>(a, pb, pb.tiles[ti], s_p);
 }
 
+// The split pipeline's soft mask and close-face lists, one workgroup per tile (grid-stride over
+// every tile: the lists of a tile without records are all padding): the tile's records are
+// placed in an LDS (slot, pixel) table kReduceSlots slots at a time; each pixel multiplies its
+// slots in order (dibr_soft_mask_cuda.cu:174-181, double-promoted), and the lists -- values
+// (:165-171) and the -1 / 0 / 0 padding of the unused slots (dibr_soft_mask.cpp:86-97) -- are
+// written in memory order: consecutive threads take consecutive elements of each tile row's
+// contiguous (16 pixels x K) block, so the 13 K bytes per pixel go out as whole lines (the
+// per-pixel rows of K elements written by one lane each were a 17x slower store shape).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_soft_lists(SoftArgs<T> a, SoftPairBuf<T> pb) {
+  __shared__ unsigned short s_ri[kReduceSlots][kBlock];  // (slot, pixel) -> record in the tile
+  __shared__ int s_np[kBlock];
+  const int K = a.K, H = a.fs.H, W = a.fs.W;
+  const int tid = threadIdx.x;
+  const int64_t nz = a.nzero0 + a.nzero1;  // side job: zero fills (grid-stride, coalesced)
+  for (int64_t i = (int64_t)blockIdx.x * kBlock + tid; i < nz; i += (int64_t)gridDim.x * kBlock) {
+    if (i < a.nzero0)
+      a.zero0[i] = (T)0;
+    else
+      a.zero1[i - a.nzero0] = (T)0;
+  }
+  const int64_t ntl = (int64_t)a.fs.B * pb.ntiles;
+  for (int64_t tile = blockIdx.x; tile < ntl; tile += gridDim.x) {
+    const int n = pb.ntile[tile];
+    if (n < 0) continue;  // overflowed: kd_soft_ovf_fwd wrote its soft mask and lists
+    const int64_t base = pb.tbase[tile];
+    const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
+    const int X0 = (tl % pb.ntx) * kTile, Y0 = (tl / pb.ntx) * kTile;
+    const int nx = min(kTile, W - X0), ny = min(kTile, H - Y0);
+    int64_t lo, hi;
+    view_range(a.fs, b, lo, hi);
+    int px, py;
+    tile_pixel(tl % pb.ntx, tl / pb.ntx, tid, px, py);
+    const bool in = px < W && py < H;
+    const int64_t p = ((int64_t)b * H + py) * W + px;
+    const int np = in ? pb.npix[p] : 0;
+    __syncthreads();  // the previous tile is done with s_np / s_ri
+    s_np[tid] = np;
+    T prod = (T)1.0;
+    for (int s0 = 0; s0 < K; s0 += kReduceSlots) {
+      const int S = min(kReduceSlots, K - s0);
+      __syncthreads();  // the previous pass is done with s_ri (and s_np is written)
+      for (int i = tid; i < n; i += kBlock) {
+        const uint32_t sq = ((const uint32_t *)(pb.rec + base + i))[1];  // slot | q << 16
+        const int s = (int)(sq & 0xffffu) - s0;
+        if (s >= 0 && s < S) s_ri[s][(sq >> 16) & 0xffu] = (unsigned short)i;
+      }
+      __syncthreads();
+      const int e_hi = min(np - s0, S);
+      for (int s = 0; s < e_hi; ++s)
+        prod = (T)((double)prod * (1.0 - (double)pb.sprob[base + s_ri[s][tid]]));
+      // the pass's slots of the tile's rows, in memory order
+      const int per_row = nx * S;
+      for (int e = tid; e < ny * per_row; e += kBlock) {
+        const int r = e / per_row, rem = e - r * per_row;
+        const int i = rem / S, s = rem - i * S;
+        const int q = ((r >> 3) * 2 + (i >> 3)) * kWave + (r & 7) * 8 + (i & 7);
+        const int64_t o = (((int64_t)b * H + Y0 + r) * W + X0 + i) * K + s0 + s;
+        if (s0 + s < s_np[q]) {
+          const int64_t ri = base + s_ri[s][q];
+          const SoftPairRec rr = pb.rec[ri];
+          a.prob[o] = pb.sprob[ri];
+          a.cidx[o] = (int64_t)rr.row - lo;
+          a.ctype[o] = (uint8_t)(rr.type + 1);
+        } else {
+          a.prob[o] = (T)0;
+          a.cidx[o] = -1;
+          a.ctype[o] = 0;
+        }
+      }
+    }
+    if (np > 0) a.soft[p] = (T)(1.0 - (double)prod);
+  }
+}
+
 // Flat over the (tile, 256-record) items: each record's distance type and probability
 // (bit-identical to the reference) and optionally the close lists.
 template <typename T, bool LISTS>
@@ -691,17 +1009,12 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
     soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
     pb.sprob[i] = prob;
     pb.rec[i].type = (uint8_t)et;
-    if (LISTS || a.last) {
+    // (LISTS: kd_soft_lists writes the close lists from the records, row-coalesced)
+    if (a.last && r.slot == K - 1) {
       const int64_t gp = ((int64_t)b * H + py) * W + px;
       int64_t lo, hi;
       view_range(fs, b, lo, hi);
-      if (LISTS) {
-        const int64_t o = gp * K + r.slot;
-        a.prob[o] = prob;
-        a.cidx[o] = (int64_t)r.row - lo;
-        a.ctype[o] = (uint8_t)(et + 1);
-      }
-      if (a.last && r.slot == K - 1) a.last[gp] = (int32_t)((int64_t)r.row - lo);
+      a.last[gp] = (int32_t)((int64_t)r.row - lo);
     }
   }
 }
@@ -869,14 +1182,16 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_bwd(SoftArgs<T> a, SoftPai
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
   const int novf = pb.counters[2];
+  const bool st = pb.counters[3] == 1;  // entries are 4 tile + quadrant (kd_dibr_fwd_st)
   for (int i = blk; i < novf; i += nblk) {
-    const int64_t tile = pb.ovf[i];
+    const int64_t ent = pb.ovf[i];
+    const int64_t tile = st ? ent >> 2 : ent;
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
     int64_t lo, hi;
     view_range(fs, b, lo, hi);
-    const TileGeom t = tile_geom(H, W, tl);
+    const TileGeom t = st ? tile_geom_st(H, W, tl, (int)(ent & 3)) : tile_geom(H, W, tl);
     const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-    const bool unc = t.inimg && a.face_idx[p] < 0;
+    const bool unc = t.inimg && (!st || threadIdx.x < kWave) && a.face_idx[p] < 0;
     const bool wave_unc = __ballot(unc) != 0ull;
     const double sp =
         unc ? -(double)a.sigmainv * (double)soft_grad_at<T>(a, b, p) * (1.0 - (double)a.soft_in[p])
@@ -1000,7 +1315,12 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
-    hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(8192), dim3(kBlock), 0, stream, a, pb);
+    if (a.prob)  // soft mask + the close lists, row-coalesced
+      hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), 0, stream, a, pb);
+    else
+      hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(8192), dim3(kBlock), 0, stream, a, pb);
+  } else if (a.prob) {
+    return set_error(KD_ERR_INVALID_ARGUMENT, "close lists need the soft mask");
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
@@ -1017,17 +1337,37 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   ra.fs.dbg = a.fs.dbg = debug_flags();
   ra.fs.tbuf = nullptr;
   a.fs.tbuf = debug_tile_buffer();
-  {
+  if (ra.bb.g.ct == kTile && ra.bb.nchunk > 0) {  // small batch: dibr_small_batch() binned at 16 px
     ProfScope prof(K_DIBR_FWD, stream);
+    const int64_t n = (int64_t)pb.ntiles * ra.fs.B;
+    const int64_t nwg = 4 * ((n + 7) / 8 * 8);
+    if (KD_DIAG && a.fs.tbuf)
+      hipLaunchKernelGGL(kd_dibr_fwd_st<KD_DIAG != 0>, dim3((unsigned)nwg), dim3(kBlock), 0,
+                         stream, ra, a, pb);
+    else
+      hipLaunchKernelGGL(kd_dibr_fwd_st<false>, dim3((unsigned)nwg), dim3(kBlock), 0, stream, ra,
+                         a, pb);
+  } else {
+    ProfScope prof(K_DIBR_FWD, stream);
+    const dim3 grid((unsigned)pb.ntiles, ra.fs.B);
+    const bool bal = (a.fs.dbg & (1 << 28)) != 0;  // measured slower: diagnostics only
     if constexpr (KD_DIAG) {
       if (a.fs.tbuf) {
-        hipLaunchKernelGGL(kd_dibr_fwd_tiles<true>, dim3((unsigned)pb.ntiles, ra.fs.B),
-                           dim3(kBlock), 0, stream, ra, a, pb);
+        if (bal)
+          hipLaunchKernelGGL((kd_dibr_fwd_tiles<true, true>), grid, dim3(kBlock), 0, stream, ra,
+                             a, pb);
+        else
+          hipLaunchKernelGGL((kd_dibr_fwd_tiles<true, false>), grid, dim3(kBlock), 0, stream, ra,
+                             a, pb);
         goto launched;
       }
     }
-    hipLaunchKernelGGL(kd_dibr_fwd_tiles<false>, dim3((unsigned)pb.ntiles, ra.fs.B),
-                       dim3(kBlock), 0, stream, ra, a, pb);
+    if (bal)
+      hipLaunchKernelGGL((kd_dibr_fwd_tiles<false, true>), grid, dim3(kBlock), 0, stream, ra, a,
+                         pb);
+    else
+      hipLaunchKernelGGL((kd_dibr_fwd_tiles<false, false>), grid, dim3(kBlock), 0, stream, ra, a,
+                         pb);
   launched:;
   }
   if (pool_may_overflow(a.K)) ovf_fwd_launch<float, true>(a, pb, stream);

@@ -1,0 +1,92 @@
+"""GPU: the reference-structured close-face lists (the (B, H, W, K) prob / idx / type tensors of
+dibr_soft_mask_forward_cuda, dibr_soft_mask.cpp:86-107, and DibrSoftMaskCuda's saved tensors,
+dibr.py:40-54) as written row-coalesced by kd_soft_lists, and the op-form backward over given lists
+(kd_soft_bwd_lists, dibr_soft_mask_cuda.cu:230-353) -- against the oracle.
+
+Bars: close_face_idx and close_face_dist_type bit-exact (including the -1 / 0 / 0 padding),
+probabilities and soft mask rtol 1e-6, gradients rtol 1e-4 (fp32, atomic summation order) with an
+absolute floor of 1e-5 x the largest magnitude; 1e-9 in fp64.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import TORCH_DTYPES
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _native():
+    from kaolin_amd import _lib
+    _lib.load()
+    assert torch.cuda.is_available()
+    yield
+    _lib.load().kd_debug_set(0)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def _view(n_lon, n_lat, h, B, dt, elevation=0.3):
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import rasterize
+    v = workloads.sphere_views(n_lon, n_lat, h, h, B, DEV, dtype=dt, elevation=elevation)
+    _, face_idx = rasterize(h, h, v['fvz'], v['fvi'], v['feats'], v['normals_z'] >= 0)
+    return v['fvi'].contiguous(), face_idx
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('knum', [30, 40, 70])
+def test_lists_vs_oracle(dname, knum):
+    """Whole views (C2 mesh, 256x256, 2 views, the pole in view): every list element, padding
+    included; knum 40 and 70 take several 32-slot passes."""
+    from kaolin_amd import _C
+    dt = TORCH_DTYPES[dname]
+    fvi, face_idx = _view(100, 51, 256, 2, dt, elevation=0.7)
+    sig, box = 7000., 0.03
+    soft, _, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
+        fvi, face_idx, sig, box, knum, 1000., with_lists=True, want_grad=False)
+    osoft, oprob, ocidx, octype, _ = oracle.soft_mask_forward(N(fvi), N(face_idx), sig, box, knum)
+    np.testing.assert_array_equal(N(cidx), ocidx)
+    np.testing.assert_array_equal(N(ctype), octype)
+    np.testing.assert_allclose(N(prob), oprob, rtol=1e-6, atol=1e-37)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+    assert (ocidx[..., knum - 1] >= 0).any()  # some rows are full
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('knum', [30, 40])
+def test_op_backward_on_lists_with_holes(dname, knum):
+    """The op backward reads given lists and stops at a row's first -1, whatever follows it
+    (dibr_soft_mask_cuda.cu:273-276): rows with a -1 punched into slot 3 must drop their later
+    entries -- in the coalesced form and in the lane-per-pixel form (debug flag 1 << 29)."""
+    from kaolin_amd import _C, _lib
+    dt = TORCH_DTYPES[dname]
+    fvi, face_idx = _view(100, 51, 256, 2, dt, elevation=0.7)
+    sig, box, M = 7000., 0.03, 1000.
+    soft, _, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
+        fvi, face_idx, sig, box, knum, M, with_lists=True, want_grad=False)
+    holes = cidx.clone()
+    rows = holes[..., 5] >= 0
+    holes[..., 3][rows & (torch.arange(rows.numel(), device=DEV).reshape(rows.shape) % 3 == 0)] = -1
+    g = torch.Generator().manual_seed(5)
+    gs = torch.rand(soft.shape, generator=g, dtype=torch.float64).to(DEV, dt)
+    sfvi = (fvi * M).contiguous()
+    osoft, oprob, _, octype, osfvi = oracle.soft_mask_forward(N(fvi), N(face_idx), sig, box, knum)
+    ref = oracle.soft_mask_backward(N(gs), N(soft), N(face_idx), N(prob), N(holes), N(ctype),
+                                    N(sfvi), sig, M)
+    tol = 1e-4 if dname == 'f32' else 1e-9
+    for flags in (0, 1 << 29):
+        _lib.load().kd_debug_set(flags)
+        try:
+            gop = _C.render.mesh.dibr_soft_mask_backward_cuda(gs, soft, face_idx, prob, holes,
+                                                              ctype, sfvi, sig, M)
+            torch.cuda.synchronize()
+        finally:
+            _lib.load().kd_debug_set(0)
+        np.testing.assert_allclose(N(gop), ref, rtol=tol, atol=tol * 0.1 * np.abs(ref).max())

@@ -22,19 +22,20 @@ v = workloads.sphere_views(n_lon, n_lat, H, W, B, dev, elevation=elev)
 fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['normals_z']
 ntx, nty = (W + 15) // 16, (H + 15) // 16
 n = B * ntx * nty
-buf = torch.zeros(5 * n, dtype=torch.int64, device=dev)
+buf = torch.zeros(7 * n, dtype=torch.int64, device=dev)
 extra = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
 lib = _lib.load()
 lib.kd_debug_buffer(buf.data_ptr())
+lib.kd_debug_set(1 << 27)  # the tile kernel (the mode fixes the workspace layout: set it first)
 for _ in range(3):
     dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
-lib.kd_debug_set(64 | extra)
+lib.kd_debug_set(64 | extra | (1 << 27))  # the tile kernel (not the small-batch form)
 dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
 lib.kd_debug_set(0)
 lib.kd_debug_buffer(None)
-t = buf.view(5, n).cpu().numpy()
+t = buf.view(7, n).cpu().numpy()
 dur = t[1] / 100.0          # us (100 MHz wall clock)
 start = (t[2] - t[2].min()) / 100.0
 end = start + dur
@@ -73,6 +74,15 @@ if t[3].any():  # per-slot table for offline study: slot, tile, raster / soft bi
             fh.write(f'{i},{tile[i]},{nbin[i]},{t[4][i]},{u_slot[i]},{start[i]:.2f},'
                      f'{rdur[i]:.2f},{dur[i] - rdur[i]:.2f}\n')
     print('wrote', out)
+if t[5].any():  # soft phase split: pass A (walk + records), pair math, product (+ IoU)
+    rend = t[3]
+    pa = np.where(t[5] > 0, (t[5] - rend) / 100.0, 0)
+    pm = np.where((t[6] > 0) & (t[5] > 0), (t[6] - t[5]) / 100.0, 0)
+    print('slowest tiles: slot | raster us | soft: passA pairmath rest | soft_nbin unc')
+    for i in np.argsort(end)[::-1][:15]:
+        print(f'  {i:5d} | {rdur[i]:6.1f} | {pa[i]:6.1f} {pm[i]:6.1f} '
+              f'{dur[i] - rdur[i] - pa[i] - pm[i]:6.1f} | {t[4][i]:5d} {u_slot[i]:4d}')
+    print(f'sums (ms): passA {pa.sum() / 1e3:.2f} pairmath {pm.sum() / 1e3:.2f}')
 late = np.argsort(end)[::-1][:10]
 print('latest ending (slot, start, dur):', [(int(i), round(float(start[i]), 1),
                                             round(float(dur[i]), 1)) for i in late])

@@ -1,0 +1,38 @@
+"""Kernel timeline of the bench's timed steps from a rocprofv3 --kernel-trace CSV: per kernel of
+one step its duration and the gap since the previous kernel ended (graph replays back to back).
+python tools/trace_steps.py DIR [kernels_per_step]"""
+import csv
+import glob
+import sys
+from collections import defaultdict
+
+d = sys.argv[1]
+f = glob.glob(d + '/**/*kernel_trace.csv', recursive=True)[0]
+rows = list(csv.DictReader(open(f)))
+ev = sorted(((int(r['Start_Timestamp']), int(r['End_Timestamp']),
+              r['Kernel_Name'].split('(')[0].replace('void ', '')) for r in rows))
+kd = [e for e in ev if 'kd::' in e[2]]
+# the step starts at kd_prepare_fwd
+starts = [i for i, e in enumerate(kd) if 'prepare_fwd' in e[2]]
+steps = [kd[a:b] for a, b in zip(starts, starts[1:])]
+# the graph replays (back-to-back launches) are the steps with the shortest span; the eager
+# profiling pass that follows them in bench.py has host-side gaps
+steps = sorted(steps, key=lambda st: st[-1][1] - st[0][0])[:10]
+agg = defaultdict(list)
+tot = []
+for st in steps:
+    tot.append((st[-1][1] - st[0][0]) / 1e3)
+    prev = None
+    for k, (s, e, n) in enumerate(st):
+        agg[(k, n)].append(((e - s) / 1e3, (s - prev) / 1e3 if prev else 0.0))
+        prev = e
+print(f'steps {len(steps)}: first kernel start -> last kernel end {min(tot):.1f} / '
+      f'{sorted(tot)[len(tot) // 2]:.1f} us (min / median)')
+for (k, n), v in sorted(agg.items()):
+    durs = sorted(x[0] for x in v)
+    gaps = sorted(x[1] for x in v)
+    print(f'  {k:2d} {n[:60]:60s} dur {durs[len(durs) // 2]:7.2f}  gap {gaps[len(gaps) // 2]:6.2f}')
+# steps' starts: period
+if len(steps) > 2:
+    per = [(steps[i + 1][0][0] - steps[i][0][0]) / 1e3 for i in range(len(steps) - 1)]
+    print(f'step period (start to start) median {sorted(per)[len(per) // 2]:.1f} us')
