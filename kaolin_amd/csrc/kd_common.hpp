@@ -30,7 +30,7 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       raster / soft mask, 64 record per-tile durations into the kd_debug_buffer array,
 //       8192 skip the fp32 raster's per-pixel epilogue (winner reload, output writes),
 //       32 also skips the fused soft mask's pair math (kd_softpair.hip soft_pairs_tile),
-//       1 << 27 (production too) disables the small-batch forward (kd_soft.hpp dibr_small_batch),
+//       1 << 27 (production too) enables the small-batch forward (kd_soft.hpp dibr_small_batch),
 //       1 << 28 (production too) the balanced (item-dealing) fused forward tiles,
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
 int debug_flags();

@@ -250,15 +250,20 @@ template <typename T>
 int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream);
 // Small-batch mode of dibr_rasterization (fp32): few enough 16x16 tiles that the tile grid is
 // about one round of workgroup slots -- the forward then runs one workgroup per 8x8 quadrant over
-// 16-pixel coarse bins (kd_dibr_fwd_st).  A function of the call's sizes only, so the forward and
-// the backward carve the same workspace.
+// 16-pixel coarse bins (kd_dibr_fwd_st).  A function of the call's sizes and the debug flags
+// only, so the forward and the backward carve the same workspace.  Measured at C3 (1 / 2 views,
+// rocprof + bench, same box): forward 60 / 96 us against 67 / 73 for the tile kernel, but the
+// 16-px bins cost 12 us more binning -- the step is no faster (0.126 vs 0.119 ms at 1 view; with
+// 32-px bins, debug flag 1 << 30, 0.118), so it runs only on request (debug flag 1 << 27).
 constexpr int64_t kSmallBatchTiles = 2048;  // B x 16x16 tiles
 inline bool dibr_small_batch(int B, int H, int W, int esize) {
   const int64_t tiles = (int64_t)B * ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-  return esize == 4 && tiles > 0 && tiles <= kSmallBatchTiles && !(debug_flags() & (1 << 27));
+  return esize == 4 && tiles > 0 && tiles <= kSmallBatchTiles && (debug_flags() & (1 << 27));
 }
+// its coarse bins: 16 px (each quadrant walks a quarter of a 32-px bin's area); debug flag
+// 1 << 30 keeps 32 px (A/B)
 inline int dibr_ct0(int B, int H, int W, int esize) {
-  return dibr_small_batch(B, H, W, esize) ? kTile : kCoarseTile0;
+  return dibr_small_batch(B, H, W, esize) && !(debug_flags() & (1 << 30)) ? kTile : kCoarseTile0;
 }
 // The raster forward (fp32 pair pipeline) and the fused soft mask in one launch, when both apply.
 template <typename T>

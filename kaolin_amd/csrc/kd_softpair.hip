@@ -835,7 +835,9 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_st(RasterFwdArgs<float>
   // the overflow kernels' mode flag (counters[3], zeroed by kd_bin_count): overflow entries are
   // (tile, quadrant) pairs
   if (blockIdx.x == 0 && threadIdx.x == 0) pb.counters[3] = 1;
-  if (!st_of_block(ra.bb, ra.fs.B, ra.fs.H, ra.fs.W, b, tl, nbin, quad)) {
+  // dispatch order: the raster bins' heaviest first, or (debug flag 1 << 25, A/B) the soft bins'
+  const bool soft_order = (ra.fs.dbg & (1 << 25)) != 0;
+  if (!st_of_block(soft_order ? a.bb : ra.bb, ra.fs.B, ra.fs.H, ra.fs.W, b, tl, nbin, quad)) {
     zero_side_job(a);  // (the grid is padded to whole groups of 32)
     return;
   }
@@ -847,7 +849,7 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_st(RasterFwdArgs<float>
     const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
     a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
   }
-  raster_pairs_tile<true>(ra, b, tl, nbin, U.r, quad);
+  raster_pairs_tile<true>(ra, b, tl, soft_order ? -1 : nbin, U.r, quad);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x + blockIdx.x] = wall_clock64();
@@ -1337,7 +1339,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   ra.fs.dbg = a.fs.dbg = debug_flags();
   ra.fs.tbuf = nullptr;
   a.fs.tbuf = debug_tile_buffer();
-  if (ra.bb.g.ct == kTile && ra.bb.nchunk > 0) {  // small batch: dibr_small_batch() binned at 16 px
+  if (dibr_small_batch(ra.fs.B, ra.fs.H, ra.fs.W, 4) && ra.bb.nchunk > 0) {  // small batch
     ProfScope prof(K_DIBR_FWD, stream);
     const int64_t n = (int64_t)pb.ntiles * ra.fs.B;
     const int64_t nwg = 4 * ((n + 7) / 8 * 8);

@@ -26,11 +26,10 @@ buf = torch.zeros(7 * n, dtype=torch.int64, device=dev)
 extra = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
 lib = _lib.load()
 lib.kd_debug_buffer(buf.data_ptr())
-lib.kd_debug_set(1 << 27)  # the tile kernel (the mode fixes the workspace layout: set it first)
 for _ in range(3):
     dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
-lib.kd_debug_set(64 | extra | (1 << 27))  # the tile kernel (not the small-batch form)
+lib.kd_debug_set(64 | extra)
 dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
 lib.kd_debug_set(0)

@@ -26,10 +26,11 @@ nwg = 4 * ((n + 7) // 8 * 8)
 buf = torch.zeros(5 * nwg, dtype=torch.int64, device=dev)
 lib = _lib.load()
 lib.kd_debug_buffer(buf.data_ptr())
+lib.kd_debug_set(1 << 27)  # the small-batch form (the mode fixes the workspace layout: set first)
 for _ in range(3):
     dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
-lib.kd_debug_set(64)
+lib.kd_debug_set(64 | (1 << 27))
 _, _, fidx = dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
 lib.kd_debug_set(0)
