@@ -61,9 +61,10 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
 
 // Edge-culling coefficients of one face for the fp32 pair raster: kd_cull.hpp (the rule and its
 // proof; host-compilable for tools/cull_check.cpp).
-__device__ void raster_cull_coefs(const float v[6], float M, int H, int W, Span sp, float eps,
+template <typename T>
+__device__ void raster_cull_coefs(const T v[6], float M, int H, int W, Span sp, float eps,
                                   float out[8]) {
-  raster_cull_coefs_at(v, M, H, W, sp.x0, sp.y0, sp.y1, eps, out);
+  raster_cull_coefs_at<T>(v, M, H, W, sp.x0, sp.y0, sp.y1, eps, out);
 }
 
 template <typename T>
@@ -99,13 +100,11 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
         load_corners(fs, i, v);
         face_box(fs, i, v, box);
         s = make_span_k<T>(box[0], box[1], box[2], box[3], jobs.k[blockIdx.z]);
-        if constexpr (std::is_same<T, float>::value) {
-          if (bb.cull && !span_empty(s)) {
-            float cc[8];
-            raster_cull_coefs(v, fs.M, fs.H, fs.W, s, bb.cull_eps, cc);
-            bb.cull[2 * i] = make_float4(cc[0], cc[1], cc[2], cc[3]);
-            bb.cull[2 * i + 1] = make_float4(cc[4], cc[5], cc[6], cc[7]);
-          }
+        if (bb.cull && !span_empty(s)) {  // fp32 and fp64 (kd_cull.hpp)
+          float cc[8];
+          raster_cull_coefs<T>(v, fs.M, fs.H, fs.W, s, bb.cull_eps, cc);
+          bb.cull[2 * i] = make_float4(cc[0], cc[1], cc[2], cc[3]);
+          bb.cull[2 * i + 1] = make_float4(cc[4], cc[5], cc[6], cc[7]);
         }
       } else {
         s.x0 = 1;

@@ -59,8 +59,9 @@ struct BinBuffers {
 };
 
 // Edge-culling coefficients of one face in its own frame (column span.x0, row span.y0); see
-// kd_binning.hip.  out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}.
-__device__ void raster_cull_coefs(const float v[6], float M, int H, int W, Span sp, float eps,
+// kd_cull.hpp.  out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}.
+template <typename T>
+__device__ void raster_cull_coefs(const T v[6], float M, int H, int W, Span sp, float eps,
                                   float out[8]);
 
 // Bin (b, c) of view b (rows [lo, lo + nview)): its ascending local face indices and count, or

@@ -17,7 +17,8 @@
 // fl(fl(w0 + w1) + w2) is within 3 tau + 1.25 tau of N, so when |N| > 6 tau it has the sign s of
 // N, and adding copysign(eps, .) keeps that sign: a pixel with s W_i < -2 tau has s w_i < -tau,
 // so w_i / norm < 0 and the reference rejects it (rasterization_cuda.cu:145; |eps| <= 2^20 tau
-// keeps |norm| below 2^126 tau, so the quotient is a normal number, never -0) -- culling it
+// (fp64: 2^500 tau) keeps |norm| finite and below 2^126 tau, so the quotient is a normal number,
+// never -0) -- culling it
 // cannot change the result.  Keep iff s W_i >= -2 tau is, for s B_i > 0 (< 0), x0 >= (<=) X*(y0);
 // in pixel units relative to the face's own span (column span.x0, row span.y0),
 //   p*(y0) = P0 + P1 (y0 - y0ref),  y0ref = centre of row span.y0,
@@ -28,6 +29,10 @@
 // double N carries its own rounding margin (2^-48 E^2) in the |N| test.  Edges outside these
 // bounds, degenerate or non-finite faces and non-positive pixel steps cull nothing (slots stay
 // -inf / +inf).
+// fp64 data (T = double): the reference evaluates the same expressions in double from the fp32
+// centres, so the same derivation holds with u = 2^-53: tau = 2^-49 Wb Hb (> 8.04 u Wb Hb), and
+// the corners' products are no longer exact in double -- their rounding (2^-52 E^2 at most) is
+// inside the 2^-48 E^2 margin of the |N| test and, through the 2^40 px bound, the 1/64 px slack.
 // out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}
 #pragma once
 
@@ -44,9 +49,11 @@
 
 namespace kd {
 
-__host__ __device__ inline void raster_cull_coefs_at(const float v[6], float M, int H, int W,
+template <typename T>
+__host__ __device__ inline void raster_cull_coefs_at(const T v[6], float M, int H, int W,
                                                      int span_x0, int span_y0, int span_y1,
                                                      float eps, float out[8]) {
+  constexpr double kTauScale = sizeof(T) == 8 ? 0x1p-49 : 0x1p-20;  // > 8.04 u
   out[0] = out[2] = -INFINITY;
   out[4] = out[6] = INFINITY;
   out[1] = out[3] = out[5] = out[7] = 0.f;
@@ -61,12 +68,15 @@ __host__ __device__ inline void raster_cull_coefs_at(const float v[6], float M, 
   const double Hb = (fmax(fmax(ay, by), cy) - fmin(fmin(ay, by), cy)) * (1.0 + 0x1p-50);
   // both bounds hold (|bex| <= E as well); the smaller one culls more (+ a floor below fp32
   // subnormal products)
-  const double tau = 0x1p-20 * fmin(Wb * Hb, E * E) + 0x1p-140;
+  const double tau = kTauScale * fmin(Wb * Hb, E * E) + 0x1p-140;
   const double A[3] = {bx * cy - by * cx, cx * ay - cy * ax, ax * by - ay * bx};
   const double Bc[3] = {by - cy, cy - ay, ay - by};
   const double Cc[3] = {cx - bx, ax - cx, bx - ax};
   const double N = A[0] + A[1] + A[2];
-  if (!(fabs(N) > 6.0 * tau + 0x1p-48 * E * E) || !(fabs((double)eps) <= 0x1p20 * tau)) return;
+  // |eps| keeps |norm| finite and the quotient a normal number (|w_i| > tau): fp32 |norm| <=
+  // 2^126 tau, fp64 far wider
+  constexpr double kEpsScale = sizeof(T) == 8 ? 0x1p500 : 0x1p20;
+  if (!(fabs(N) > 6.0 * tau + 0x1p-48 * E * E) || !(fabs((double)eps) <= kEpsScale * tau)) return;
   const double s = N > 0.0 ? 1.0 : -1.0;
   const double sx = sxf, sy = syf;
   const double y0ref = (double)(M / (float)H * (float)(H - 2 * span_y0 - 1));  // px_cy

@@ -143,11 +143,9 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   sa.iou_B = B;
   int rc = KD_OK;
   bool done = false;
-  if constexpr (std::is_same<T, float>::value) {
-    if (dibr_fwd_fusable(ra, sa)) {
-      rc = dibr_fwd_fused_launch(ra, sa, d.pb, stream);
-      done = true;
-    }
+  if (dibr_fwd_fusable(ra, sa)) {  // (fp32 and fp64)
+    rc = dibr_fwd_fused_launch(ra, sa, d.pb, stream);
+    done = true;
   }
   if (!done) {
     rc = raster_launch<T>(ra, stream);

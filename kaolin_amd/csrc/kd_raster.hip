@@ -108,13 +108,15 @@ __global__ __launch_bounds__(kBlock) void kd_raster_fwd(RasterFwdArgs<T> a) {
 }
 
 
-__global__ __launch_bounds__(kBlock, 6) void kd_raster_fwd_pairs(RasterFwdArgs<float> a) {
+template <typename T>
+__global__ __launch_bounds__(kBlock, sizeof(T) == 8 ? 4 : 6) void kd_raster_fwd_pairs(
+    RasterFwdArgs<T> a) {
   TileClock clk(a.fs.tbuf, 0);
-  __shared__ RasterPairsLDS S;
+  __shared__ RasterPairsLDS<T> S;
   if (ablate(a.fs.dbg, 16384)) return;  // diagnostics: dispatch cost only
   int b, tl, nbin;
   tile_of_block(a.bb, a.fs.H, a.fs.W, b, tl, nbin, a.fs.dbg);
-  raster_pairs_tile(a, b, tl, nbin, S);
+  raster_pairs_tile<T>(a, b, tl, nbin, S);
 }
 
 // General per-pixel form for wide features (D > 8): one thread per pixel, float atomics.
@@ -178,9 +180,10 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(RasterBwdArgs<T> ra
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
+// the pair pipeline with edge culling (fp32 and fp64; debug flag 8: the lane-per-pixel kernel)
 template <typename T>
 bool raster_uses_cull() {
-  return std::is_same<T, float>::value && !(debug_flags() & 8);
+  return !(debug_flags() & 8);
 }
 
 template <typename T>
@@ -191,14 +194,10 @@ int raster_launch(RasterFwdArgs<T> &a, hipStream_t stream) {
   const int ntiles = ((fs.W + kTile - 1) / kTile) * ((fs.H + kTile - 1) / kTile);
   {
     ProfScope prof(K_RASTER_FWD, stream);
-    if constexpr (std::is_same<T, float>::value) {
-      if (a.bb.cull)
-        hipLaunchKernelGGL(kd_raster_fwd_pairs, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-      else
-        hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-    } else {
+    if (a.bb.cull)
+      hipLaunchKernelGGL(kd_raster_fwd_pairs<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
+    else
       hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-    }
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "raster fwd: %s", hipGetErrorString(e));

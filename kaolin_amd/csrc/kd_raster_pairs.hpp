@@ -79,14 +79,24 @@ __device__ __forceinline__ uint32_t ordered_f32(float z) {
   const uint32_t u = __float_as_uint(z + 0.0f);  // -0 -> +0
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
+__device__ __forceinline__ unsigned long long ordered_f64(double z) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(z + 0.0);  // -0 -> +0
+  return (u & 0x8000000000000000ull) ? ~u : (u | 0x8000000000000000ull);
+}
 
-// LDS of one tile of the pair pipeline
+// LDS of one tile of the pair pipeline.  fp64: the 64-bit winner key holds the depth rounded
+// down to fp32 (monotone: the deepest face keeps the largest key) and the exact maximum depth is
+// kept beside it (zx): the key's face is the reference's winner when its own depth is that
+// maximum -- else (two faces within one fp32 step of depth, the lower index the shallower) the
+// pixel replays the reference's loop.
+template <typename T>
 struct RasterPairsLDS {
   TileLists L;
-  float geo[9][kCap];   // ax ay bx by cx cy (scaled), az bz cz
+  T geo[9][kCap];        // ax ay bx by cx cy (scaled), az bz cz
   float4 cull[2][kCap];  // raster_cull_coefs (kd_binning), face frame
   unsigned short pair[4][kRasterPairCap];  // (q << 8) | sub-list entry
   unsigned long long key[4][64];
+  unsigned long long zx[sizeof(T) == 8 ? 4 : 1][64];  // fp64: ordered exact maximum depth
   unsigned long long nan[4];
 };
 
@@ -99,9 +109,10 @@ struct RasterPairsLDS {
 // ST (small-batch mode, kd_dibr_fwd_st): the workgroup covers quadrant `quad` of the tile only
 // (tile_geom_st); its four waves share the quadrant's 64 pixels and its one list (every wave built
 // the same sub-list), the chunks dealt as with BAL, and wave 0 writes the outputs.
-template <bool ST = false, bool BAL = false>
-__device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a, int b, int tl,
-                                                  int nbin, RasterPairsLDS &S, int quad = 0) {
+template <typename T, bool ST = false, bool BAL = false>
+__device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int b, int tl,
+                                                  int nbin, RasterPairsLDS<T> &S, int quad = 0) {
+  constexpr bool kF64 = sizeof(T) == 8;
   constexpr bool kItems = ST || BAL;  // chunks dealt to the waves as (sub-tile, chunk) items
   constexpr int NS = ST ? 1 : 4;       // sub-lists of the workgroup
   TileLists &L = S.L;
@@ -110,7 +121,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   auto &s_pair = S.pair;
   auto &s_key = S.key;
   auto &s_nan = S.nan;
-  const FaceSet<float> &fs = a.fs;
+  const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const float M = fs.M;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -122,6 +133,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
   if (!ST || w == 0) {  // (the walk's first barrier orders these before any pass B)
     s_key[kw][lane] = 0ull;
+    if (kF64) S.zx[kF64 ? kw : 0][lane] = 0ull;
     if (lane == 0) s_nan[kw] = 0ull;
   }
   // this wave's row centres relative to its first row
@@ -132,11 +144,11 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
   constexpr float kSlack = 1.f / 64.f;
 
   auto stage = [&](int k, int64_t fi) {
-    float v[6];
+    T v[6];
     load_corners(fs, fi, v);
 #pragma unroll
     for (int q = 0; q < 6; ++q) s_geo[q][k] = v[q];
-    const float *zz = a.fvz + fi * a.fvz_fs;
+    const T *zz = a.fvz + fi * a.fvz_fs;
     s_geo[6][k] = zz[0];
     s_geo[7][k] = zz[a.fvz_cs];
     s_geo[8][k] = zz[2 * a.fvz_cs];
@@ -161,17 +173,24 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
         const int krow = kItems ? ps : kw;
         const float x0 = sx * (float)(2 * (ox + (q & 7)) + 1 - W);
         const float y0 = sy * (float)(H - 2 * (oy + (q >> 3)) - 1);
-        float w0, w1, w2, z0;
-        if (raster_face_test<float, false>(x0, y0, s_geo[0][k], s_geo[1][k], s_geo[2][k],
-                                           s_geo[3][k], s_geo[4][k], s_geo[5][k], s_geo[6][k],
-                                           s_geo[7][k], s_geo[8][k], a.eps, w0, w1, w2, z0)) {
+        T w0, w1, w2, z0;
+        if (raster_face_test<T, false>((T)x0, (T)y0, s_geo[0][k], s_geo[1][k], s_geo[2][k],
+                                       s_geo[3][k], s_geo[4][k], s_geo[5][k], s_geo[6][k],
+                                       s_geo[7][k], s_geo[8][k], a.eps, w0, w1, w2, z0)) {
           if (isnan(z0)) {
             atomicOr(&s_nan[krow], 1ull << q);
-          } else if (z0 != -INFINITY) {
+          } else if (z0 != (T)-INFINITY) {
+            // fp64: the depth rounded down to fp32 in the key, the exact one in zx
+            float zk;
+            if constexpr (kF64)
+              zk = __double2float_rd((double)z0);
+            else
+              zk = (float)z0;
             const unsigned long long key =
-                ((unsigned long long)ordered_f32(z0) << 32) |
+                ((unsigned long long)ordered_f32(zk) << 32) |
                 (unsigned long long)(0xffffffffu - (uint32_t)L.f[k]);
             atomicMax(&s_key[krow][q], key);
+            if constexpr (kF64) atomicMax(&S.zx[krow][q], ordered_f64((double)z0));
           }
         }
       }
@@ -260,25 +279,39 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
 
   if (!t.inimg || (ST && w != 0) || ablate(fs.dbg, 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-  const float x0 = px_cx(M, W, t.px), y0 = px_cy(M, H, t.py);
+  const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
   int best = -1;
-  float bw0 = 0.f, bw1 = 0.f, bw2 = 0.f;
-  if ((s_nan[kw] >> lane) & 1ull) {
+  T bw0 = (T)0, bw1 = (T)0, bw2 = (T)0;
+  bool replay = (s_nan[kw] >> lane) & 1ull;
+  if (!replay && s_key[kw][lane] != 0ull) {
+    best = (int)(0xffffffffu - (uint32_t)(s_key[kw][lane] & 0xffffffffull));
+    T v[6];
+    load_corners(fs, lo + best, v);
+    const T *zz = a.fvz + (lo + best) * a.fvz_fs;
+    T z0;
+    raster_face_test<T>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[a.fvz_cs],
+                        zz[2 * a.fvz_cs], a.eps, bw0, bw1, bw2, z0);
+    // fp64: the key's face is the winner only if its depth is the exact maximum
+    if constexpr (kF64) replay = ordered_f64((double)z0) != S.zx[kw][lane];
+  }
+  if (replay) {
     // the reference's sequential loop over this pixel's coarse bin (ascending faces)
+    best = -1;
+    bw0 = bw1 = bw2 = (T)0;
     const BinGeom &g = a.bb.g;
     const int ct = (t.py >> g.sh) * g.nctx + (t.px >> g.sh);
     int n;
     const int *bin = bin_list(a.bb, b, ct, lo, (int)(hi - lo), -1, n);
-    float max_z0 = -INFINITY;
+    T max_z0 = (T)-INFINITY;
     for (int e = 0; e < n; ++e) {
       const int f = bin ? bin[e] : e;
       if (!pspan_has(pack_span(a.bb.spans[lo + f]), t.px, t.py)) continue;
-      float v[6];
+      T v[6];
       load_corners(fs, lo + f, v);
-      const float *zz = a.fvz + (lo + f) * a.fvz_fs;
-      float w0, w1, w2, z0;
-      if (!raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0],
-                                   zz[a.fvz_cs], zz[2 * a.fvz_cs], a.eps, w0, w1, w2, z0))
+      const T *zz = a.fvz + (lo + f) * a.fvz_fs;
+      T w0, w1, w2, z0;
+      if (!raster_face_test<T>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0],
+                               zz[a.fvz_cs], zz[2 * a.fvz_cs], a.eps, w0, w1, w2, z0))
         continue;
       if (z0 <= max_z0) continue;
       max_z0 = z0;
@@ -287,30 +320,22 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<float> &a,
       bw1 = w1;
       bw2 = w2;
     }
-  } else if (s_key[kw][lane] != 0ull) {
-    best = (int)(0xffffffffu - (uint32_t)(s_key[kw][lane] & 0xffffffffull));
-    float v[6];
-    load_corners(fs, lo + best, v);
-    const float *zz = a.fvz + (lo + best) * a.fvz_fs;
-    float z0;
-    raster_face_test<float>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[a.fvz_cs],
-                            zz[2 * a.fvz_cs], a.eps, bw0, bw1, bw2, z0);
   }
   a.face_idx[p] = best;
-  float *wo = a.weights + p * 3;
-  float *io = a.interp + p * a.D;
+  T *wo = a.weights + p * 3;
+  T *io = a.interp + p * a.D;
   if (best >= 0) {
     wo[0] = bw0;
     wo[1] = bw1;
     wo[2] = bw2;
-    const float *r = a.feat + (lo + best) * 3 * a.D;
+    const T *r = a.feat + (lo + best) * 3 * a.D;
     for (int d = 0; d < a.D; ++d)
       io[d] = bw0 * r[d] + bw1 * r[a.D + d] + bw2 * r[2 * a.D + d];
   } else {
-    wo[0] = 0.f;
-    wo[1] = 0.f;
-    wo[2] = 0.f;
-    for (int d = 0; d < a.D; ++d) io[d] = 0.f;
+    wo[0] = (T)0;
+    wo[1] = (T)0;
+    wo[2] = (T)0;
+    for (int d = 0; d < a.D; ++d) io[d] = (T)0;
   }
 }
 

@@ -268,6 +268,9 @@ inline int dibr_ct0(int B, int H, int W, int esize) {
 // The raster forward (fp32 pair pipeline) and the fused soft mask in one launch, when both apply.
 template <typename T>
 struct RasterFwdArgs;
+bool dibr_fwd_fusable(const RasterFwdArgs<double> &ra, const SoftArgs<double> &a);
+int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a, SoftPairBuf<double> &pb,
+                          hipStream_t stream);
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a);
 int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
                           hipStream_t stream);

@@ -780,8 +780,9 @@ __global__ __launch_bounds__(kBlock, OCC) void kd_soft_pairs(SoftArgs<T> a, Soft
 // owns the same pixel in both, so the soft phase reads the face_idx its own thread just wrote.
 // No launch boundary between the two, and a tile's raster and soft work (heavy in different
 // tiles: interior vs silhouette) share one workgroup slot.  The two phases' LDS is a union.
+template <typename T>
 union DibrTileLDS {
-  RasterPairsLDS r;
+  RasterPairsLDS<T> r;
   SoftPairsLDS<true> s;
 };
 
@@ -796,7 +797,7 @@ template <bool DIAG, bool BAL>
 __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
                                                               SoftArgs<float> a,
                                                               SoftPairBuf<float> pb) {
-  __shared__ DibrTileLDS U;
+  __shared__ DibrTileLDS<float> U;
   TileClock clk(DIAG ? a.fs.tbuf : nullptr, 1);
   if (DIAG) clk.start_to(2);
   int b, tl, nbin;
@@ -809,7 +810,7 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
     const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
     a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
   }
-  raster_pairs_tile<false, BAL>(ra, b, tl, nbin, U.r);
+  raster_pairs_tile<float, false, BAL>(ra, b, tl, nbin, U.r);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
@@ -828,7 +829,7 @@ template <bool DIAG>
 __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_st(RasterFwdArgs<float> ra,
                                                             SoftArgs<float> a,
                                                             SoftPairBuf<float> pb) {
-  __shared__ DibrTileLDS U;
+  __shared__ DibrTileLDS<float> U;
   TileClock clk(DIAG ? a.fs.tbuf : nullptr, 1);
   if (DIAG) clk.start_to(2);
   int b, tl, nbin, quad;
@@ -849,11 +850,25 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_st(RasterFwdArgs<float>
     const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
     a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
   }
-  raster_pairs_tile<true>(ra, b, tl, soft_order ? -1 : nbin, U.r, quad);
+  raster_pairs_tile<float, true>(ra, b, tl, soft_order ? -1 : nbin, U.r, quad);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x + blockIdx.x] = wall_clock64();
   soft_pairs_tile<float, true, true>(a, pb, b, tl, -1, U.s, quad);
+}
+
+// The fp64 DIB-R forward in one launch: the pair raster (fp64 test, fp64-culled candidates, the
+// exact-depth winner of RasterPairsLDS<double>) and the fused soft mask per tile, as
+// kd_dibr_fwd_tiles does for fp32 (36 KB of LDS: four workgroups per CU).
+__global__ __launch_bounds__(kBlock, 4) void kd_dibr_fwd_tiles_f64(RasterFwdArgs<double> ra,
+                                                                 SoftArgs<double> a,
+                                                                 SoftPairBuf<double> pb) {
+  __shared__ DibrTileLDS<double> U;
+  int b, tl, nbin;
+  tile_of_block(ra.bb, ra.fs.H, ra.fs.W, b, tl, nbin, ra.fs.dbg);
+  raster_pairs_tile<double>(ra, b, tl, nbin, U.r);
+  __syncthreads();  // the raster phase is done with the LDS
+  soft_pairs_tile<double, true>(a, pb, b, tl, -1, U.s);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1326,6 +1341,27 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
+  return KD_OK;
+}
+
+bool dibr_fwd_fusable(const RasterFwdArgs<double> &ra, const SoftArgs<double> &a) {
+  return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
+         !(debug_flags() & ((1 << 26) | 4096));
+}
+
+int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
+                          SoftPairBuf<double> &pb, hipStream_t stream) {
+  ra.fs.dbg = a.fs.dbg = debug_flags();
+  ra.fs.tbuf = nullptr;
+  a.fs.tbuf = nullptr;
+  {
+    ProfScope prof(K_DIBR_FWD, stream);
+    hipLaunchKernelGGL(kd_dibr_fwd_tiles_f64, dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
+                       stream, ra, a, pb);
+  }
+  if (pool_may_overflow(a.K)) ovf_fwd_launch<double, true>(a, pb, stream);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr fwd: %s", hipGetErrorString(e));
   return KD_OK;
 }
 

@@ -17,24 +17,27 @@ static float px_cx(float M, int W, int w) { return M / (float)W * (float)(2 * w 
 static float px_cy(float M, int H, int h) { return M / (float)H * (float)(H - 2 * h - 1); }
 static float fmed3(float x, float lo, float hi) { return std::min(std::max(x, lo), hi); }
 
-// the reference test for one pixel whose centre passed the box test
-static bool ref_accepts(float x0, float y0, const float v[6], float eps) {
-  const float ax = v[0] - x0, ay = v[1] - y0, bx = v[2] - x0, by = v[3] - y0;
-  const float cx = v[4] - x0, cy = v[5] - y0;
-  float w0 = bx * cy - by * cx;
-  float w1 = cx * ay - cy * ax;
-  float w2 = ax * by - ay * bx;
-  float norm = w0 + w1 + w2;
-  norm = (float)((double)norm + std::copysign((double)eps, (double)norm));
+// the reference test for one pixel whose centre passed the box test (T = the data type; the
+// centres are fp32, widened)
+template <typename T>
+static bool ref_accepts(float x0f, float y0f, const T v[6], float eps) {
+  const T x0 = x0f, y0 = y0f;
+  const T ax = v[0] - x0, ay = v[1] - y0, bx = v[2] - x0, by = v[3] - y0;
+  const T cx = v[4] - x0, cy = v[5] - y0;
+  T w0 = bx * cy - by * cx;
+  T w1 = cx * ay - cy * ax;
+  T w2 = ax * by - ay * bx;
+  T norm = w0 + w1 + w2;
+  norm = (T)((double)norm + std::copysign((double)eps, (double)norm));
   w0 /= norm;
   w1 /= norm;
   w2 /= norm;
-  return !(w0 < 0.f || w1 < 0.f || w2 < 0.f);
+  return !(w0 < 0 || w1 < 0 || w2 < 0);
 }
 
-int main(int argc, char **argv) {
-  const long nf = argc > 1 ? atol(argv[1]) : 200000;
-  std::mt19937_64 g(argc > 2 ? atol(argv[2]) : 7);
+template <typename T>
+static int run(long nf, long seed) {
+  std::mt19937_64 g(seed);
   std::uniform_real_distribution<double> u(0.0, 1.0);
   long cand = 0, culled = 0, bad = 0, acc = 0;
   long kc[6] = {0}, kcul[6] = {0}, kacc[6] = {0};
@@ -88,23 +91,23 @@ int main(int argc, char **argv) {
         p[2 * k + 1] = px_cy(1.f, H, iy);
       }
     }
-    float v[6];
-    for (int k = 0; k < 6; ++k) v[k] = (float)p[k] * M;  // fvi * M (fp32 product)
-    const float xmin = std::min({v[0], v[2], v[4]}), xmax = std::max({v[0], v[2], v[4]});
-    const float ymin = std::min({v[1], v[3], v[5]}), ymax = std::max({v[1], v[3], v[5]});
+    T v[6];
+    for (int k = 0; k < 6; ++k) v[k] = (T)p[k] * (T)M;  // fvi * M (in the data type)
+    const T xmin = std::min({v[0], v[2], v[4]}), xmax = std::max({v[0], v[2], v[4]});
+    const T ymin = std::min({v[1], v[3], v[5]}), ymax = std::max({v[1], v[3], v[5]});
     // exact span of the half-open box test
     int x0s = W, x1s = -1, y0s = H, y1s = -1;
     for (int x = 0; x < W; ++x) {
-      const float c = px_cx(M, W, x);
+      const T c = px_cx(M, W, x);
       if (!(c < xmin) && !(c >= xmax)) { x0s = std::min(x0s, x); x1s = std::max(x1s, x); }
     }
     for (int y = 0; y < H; ++y) {
-      const float c = px_cy(M, H, y);
+      const T c = px_cy(M, H, y);
       if (!(c < ymin) && !(c >= ymax)) { y0s = std::min(y0s, y); y1s = std::max(y1s, y); }
     }
     if (x0s > x1s || y0s > y1s) continue;
     float cc[8];
-    kd::raster_cull_coefs_at(v, M, H, W, x0s, y0s, y1s, eps, cc);
+    kd::raster_cull_coefs_at<T>(v, M, H, W, x0s, y0s, y1s, eps, cc);
     for (int y = y0s; y <= y1s; ++y) {
       const int WY0 = y & ~7, r = y - WY0;
       const float ysub = px_cy(M, H, WY0);
@@ -119,7 +122,7 @@ int main(int argc, char **argv) {
         const int xs = std::max((int)std::ceil(fmed3(plo, -1.f, 9.f)), rx0);
         const int xe = std::min((int)std::floor(fmed3(phi, -1.f, 9.f)), rx1);
         const bool keep = xs <= x - WX0 && x - WX0 <= xe;
-        const bool a = ref_accepts(px_cx(M, W, x), px_cy(M, H, y), v, eps);
+        const bool a = ref_accepts<T>(px_cx(M, W, x), px_cy(M, H, y), v, eps);
         ++cand;
         acc += a;
         culled += !keep;
@@ -139,7 +142,14 @@ int main(int argc, char **argv) {
     printf("  %-15s candidates %11ld accepted %5.1f%% culled %5.1f%% (of the rejects %5.1f%%)\n",
            kn[k], kc[k], 100.0 * kacc[k] / std::max(kc[k], 1L), 100.0 * kcul[k] / std::max(kc[k], 1L),
            100.0 * kcul[k] / std::max(kc[k] - kacc[k], 1L));
-  printf("faces %ld, box candidates %ld, accepted %ld, culled %ld (%.1f%%), violations %ld\n", nf,
+  printf("%s: faces %ld, box candidates %ld, accepted %ld, culled %ld (%.1f%%), violations %ld\n", sizeof(T) == 8 ? "f64" : "f32", nf,
          cand, acc, culled, 100.0 * culled / std::max(cand, 1L), bad);
   return bad != 0;
+}
+
+int main(int argc, char **argv) {
+  const long nf = argc > 1 ? atol(argv[1]) : 200000;
+  const long seed = argc > 2 ? atol(argv[2]) : 7;
+  const bool f64 = argc > 3 && argv[3][0] == 'd';
+  return f64 ? run<double>(nf, seed) : run<float>(nf, seed);
 }
