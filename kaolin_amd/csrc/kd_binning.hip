@@ -74,62 +74,87 @@ struct BinJobs {
   SpanConsts k[2];  // make_span constants of each set (host-computed)
 };
 
-template <typename T, int PER>  // PER = chunk / 256 faces per thread
+// One face of one set: its exact span (stored), the raster set's cull coefficients, and its
+// coarse tiles counted in LDS.  v: the face's scaled corners (loaded once for both sets).
+template <typename T>
+__device__ __forceinline__ void bin_count_face(const FaceSet<T> &fs, const BinBuffers &bb,
+                                               const SpanConsts &k, int64_t i, const T v[6],
+                                               int *s_cnt) {
+  Span s;
+  const bool ok = (!fs.valid || fs.valid[i]) && (!fs.nz || fs.nz[i * fs.nz_stride] >= (T)0);
+  if (ok) {
+    T box[4];
+    face_box(fs, i, v, box);
+    s = make_span_k<T>(box[0], box[1], box[2], box[3], k);
+    if (bb.cull && !span_empty(s) && !ablate(fs.dbg, 1 << 18)) {  // fp32 and fp64 (kd_cull.hpp)
+      float cc[8];
+      raster_cull_coefs<T>(v, fs.M, fs.H, fs.W, s, bb.cull_eps, cc);
+      bb.cull[2 * i] = make_float4(cc[0], cc[1], cc[2], cc[3]);
+      bb.cull[2 * i + 1] = make_float4(cc[4], cc[5], cc[6], cc[7]);
+    }
+  } else {
+    s.x0 = 1;
+    s.x1 = 0;
+    s.y0 = 1;
+    s.y1 = 0;
+  }
+  bb.spans[i] = s;
+  if (!span_empty(s) && !ablate(fs.dbg, 1 << 19)) {
+    const int cx0 = s.x0 >> bb.g.sh, cx1 = s.x1 >> bb.g.sh;
+    const int cy0 = s.y0 >> bb.g.sh, cy1 = s.y1 >> bb.g.sh;
+    for (int cy = cy0; cy <= cy1; ++cy)
+      for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&s_cnt[cy * bb.g.nctx + cx], 1);
+  }
+}
+
+// One workgroup per (chunk, view): the chunk's faces in the NS sets (NS = 2: the raster's and
+// the soft mask's boxes of the same corners, which are loaded once), their counts per coarse
+// tile written tile-major (counts[b][c][chunk]: the scan reads each tile's chunks contiguously).
+template <typename T, int PER, int NS>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
-  const FaceSet<T> &fs = jobs.fs[blockIdx.z];
-  const BinBuffers &bb = jobs.bb[blockIdx.z];
-  __shared__ int s_cnt[kMaxCtiles];
+  __shared__ int s_cnt[NS][kMaxCtiles];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
-  const int nct = bb.g.nct();
-  for (int c = tid; c < nct; c += kBlock) s_cnt[c] = 0;
+  const int z0 = NS == 2 ? 0 : blockIdx.z;  // NS = 1: blockIdx.z selects the set
+  const int nct = jobs.bb[z0].g.nct();
+#pragma unroll
+  for (int z = 0; z < NS; ++z)
+    for (int c = tid; c < nct; c += kBlock) s_cnt[z][c] = 0;
   if (b == 0 && chunk == 0) {
-    if (bb.clear && tid < bb.n_clear) bb.clear[tid] = 0;
-    for (int i = tid; i < bb.n_clear_b; i += kBlock) bb.clear_b[i] = 0;
+#pragma unroll
+    for (int z = 0; z < NS; ++z) {
+      const BinBuffers &bb = jobs.bb[z0 + z];
+      if (bb.clear && tid < bb.n_clear) bb.clear[tid] = 0;
+      for (int i = tid; i < bb.n_clear_b; i += kBlock) bb.clear_b[i] = 0;
+    }
   }
   int64_t lo, hi;
-  view_range(fs, b, lo, hi);
+  view_range(jobs.fs[z0], b, lo, hi);
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
     const int64_t i = lo + (int64_t)chunk * (PER * kBlock) + u * kBlock + tid;
     if (i < hi) {
-      Span s;
-      const bool ok = (!fs.valid || fs.valid[i]) && (!fs.nz || fs.nz[i * fs.nz_stride] >= (T)0);
-      if (ok) {
-        T v[6], box[4];
-        load_corners(fs, i, v);
-        face_box(fs, i, v, box);
-        s = make_span_k<T>(box[0], box[1], box[2], box[3], jobs.k[blockIdx.z]);
-        if (bb.cull && !span_empty(s)) {  // fp32 and fp64 (kd_cull.hpp)
-          float cc[8];
-          raster_cull_coefs<T>(v, fs.M, fs.H, fs.W, s, bb.cull_eps, cc);
-          bb.cull[2 * i] = make_float4(cc[0], cc[1], cc[2], cc[3]);
-          bb.cull[2 * i + 1] = make_float4(cc[4], cc[5], cc[6], cc[7]);
-        }
-      } else {
-        s.x0 = 1;
-        s.x1 = 0;
-        s.y0 = 1;
-        s.y1 = 0;
-      }
-      bb.spans[i] = s;
-      if (!span_empty(s)) {
-        const int cx0 = s.x0 >> bb.g.sh, cx1 = s.x1 >> bb.g.sh;
-        const int cy0 = s.y0 >> bb.g.sh, cy1 = s.y1 >> bb.g.sh;
-        for (int cy = cy0; cy <= cy1; ++cy)
-          for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&s_cnt[cy * bb.g.nctx + cx], 1);
-      }
+      T v[6];
+      load_corners(jobs.fs[z0], i, v);
+#pragma unroll
+      for (int z = 0; z < NS; ++z)
+        bin_count_face<T>(jobs.fs[z0 + z], jobs.bb[z0 + z], jobs.k[z0 + z], i, v, s_cnt[z]);
     }
   }
   __syncthreads();
-  int *out = bb.counts + ((int64_t)b * bb.nchunk + chunk) * nct;
-  for (int c = tid; c < nct; c += kBlock) out[c] = s_cnt[c];
+#pragma unroll
+  for (int z = 0; z < NS; ++z) {
+    const BinBuffers &bb = jobs.bb[z0 + z];
+    int *out = bb.counts + (int64_t)b * nct * bb.nchunk + chunk;
+    for (int c = tid; c < nct; c += kBlock) out[(int64_t)c * bb.nchunk] = s_cnt[z][c];
+  }
 }
 
-// One wave per (coarse tile, view, set), four per workgroup: exclusive scan of counts[b][*][c]
-// over the chunks.  Lane l owns the contiguous run of chunks [l*per, l*per + per), held in
-// registers; the run sums are scanned with DPP (wave_incl_scan).  No LDS, no barriers: every
-// wave's loads are in flight at once and the grid is one round on the chip.
+// One wave per (coarse tile, view, set), four per workgroup: exclusive scan of counts[b][c][*]
+// over the chunks (contiguous: tile-major).  Lane l owns the contiguous run of chunks
+// [l*per, l*per + per), held in registers; the run sums are scanned with DPP (wave_incl_scan).
+// No LDS, no barriers: every wave's loads are in flight at once and the grid is one round on the
+// chip.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
   const BinBuffers &bb = jobs.bb[blockIdx.z];
@@ -139,7 +164,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
   const int b = blockIdx.y, lane = threadIdx.x & (kWave - 1);
   const int n = bb.nchunk;
   const int per = (n + kWave - 1) / kWave;
-  int *base = bb.counts + (int64_t)b * n * nct + c;
+  int *base = bb.counts + ((int64_t)b * nct + c) * n;
   constexpr int kMaxPer = 16;  // register-held run (n <= 1024 chunks = 262k faces per view)
   int v[kMaxPer];
   int local = 0;
@@ -148,13 +173,13 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
 #pragma unroll
     for (int k = 0; k < kMaxPer; ++k) {
       const int j = lane * per + k;
-      v[k] = (k < per && j < n) ? base[(int64_t)j * nct] : 0;
+      v[k] = (k < per && j < n) ? base[j] : 0;
       local += v[k];
     }
   } else if (live) {
     for (int k = 0; k < per; ++k) {
       const int j = lane * per + k;
-      if (j < n) local += base[(int64_t)j * nct];
+      if (j < n) local += base[j];
     }
   }
   const int incl = wave_incl_scan(local);
@@ -165,7 +190,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
     for (int k = 0; k < kMaxPer; ++k) {
       const int j = lane * per + k;
       if (k < per && j < n) {
-        base[(int64_t)j * nct] = run;
+        base[j] = run;
         run += v[k];
       }
     }
@@ -173,8 +198,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
     for (int k = 0; k < per; ++k) {
       const int j = lane * per + k;
       if (j < n) {
-        const int x = base[(int64_t)j * nct];
-        base[(int64_t)j * nct] = run;
+        const int x = base[j];
+        base[j] = run;
         run += x;
       }
     }
@@ -195,10 +220,14 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   // it; each thread holds faces tid (and tid + 256).
   constexpr int kWords = PER * kBlock / 32, kPerT = PER;
   extern __shared__ uint32_t s_mask[];  // [nct][kWords]
-  __shared__ int s_bbase[kMaxCtiles], s_scan[kBlock / kWave];
+  __shared__ int s_bbase[kMaxCtiles], s_offs[kMaxCtiles], s_scan[kBlock / kWave];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
   for (int k = tid; k < nct * kWords; k += kBlock) s_mask[k] = 0u;
+  {  // this chunk's exclusive offsets in every tile's bin (strided reads, once)
+    const int *offs = bb.counts + (int64_t)b * nct * bb.nchunk + chunk;
+    for (int c = tid; c < nct; c += kBlock) s_offs[c] = offs[(int64_t)c * bb.nchunk];
+  }
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   Span sp[kPerT];
@@ -247,7 +276,7 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
         atomicOr(&s_mask[(cy * bb.g.nctx + cx) * kWords + word], bit);
   }
   __syncthreads();
-  const int *offs = bb.counts + ((int64_t)b * bb.nchunk + chunk) * nct;
+  const int *offs = s_offs;  // (staged above: counts are tile-major)
   const int *bbase = s_bbase;
   int *bins = bb.bins + (int64_t)bb.xper * lo;
 #pragma unroll
@@ -344,7 +373,9 @@ __device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty) {
 }
 
 template <typename T>
-static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream) {
+static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t stream) {
+  BinJobs<T> jobs = jobs_in;
+  jobs.fs[0].dbg = jobs.fs[1].dbg = debug_flags();  // (diagnostic ablations 1 << 18, 1 << 19)
   const FaceSet<T> &fs = jobs.fs[0];
   const BinBuffers &bb = jobs.bb[0];
   if (bb.nchunk <= 0 || fs.B <= 0) {
@@ -371,12 +402,24 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs, int njobs, hipStream_t stream
   const dim3 grid_c(bb.nchunk, fs.B, njobs);
   const dim3 grid_t((bb.g.nct() + kBlock / kWave - 1) / (kBlock / kWave), fs.B, njobs);
   const bool two = bb.chunk == 2 * kBlock;
+  // both sets in one workgroup when they share the corners (dibr_rasterization's raster and soft
+  // boxes), the corners loaded once: measured slower at C3 (24.6 vs 19.8 us at 8 views, 11.7 vs
+  // 7.2 at 1: twice the work per wave at 93 VGPRs), so only on request (debug flag 1 << 21)
+  const bool shared = (debug_flags() & (1 << 21)) && njobs == 2 &&
+                      jobs.fs[0].fvi == jobs.fs[1].fvi &&
+                      jobs.fs[0].scale == jobs.fs[1].scale && jobs.fs[0].F == jobs.fs[1].F &&
+                      jobs.fs[0].first_idx == jobs.fs[1].first_idx;
   {
     ProfScope prof(K_BIN_COUNT, stream);
-    if (two)
-      hipLaunchKernelGGL((kd_bin_count<T, 2>), grid_c, dim3(kBlock), 0, stream, jobs);
+    const dim3 grid_s(bb.nchunk, fs.B, 1);
+    if (shared && two)
+      hipLaunchKernelGGL((kd_bin_count<T, 2, 2>), grid_s, dim3(kBlock), 0, stream, jobs);
+    else if (shared)
+      hipLaunchKernelGGL((kd_bin_count<T, 1, 2>), grid_s, dim3(kBlock), 0, stream, jobs);
+    else if (two)
+      hipLaunchKernelGGL((kd_bin_count<T, 2, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
     else
-      hipLaunchKernelGGL((kd_bin_count<T, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
+      hipLaunchKernelGGL((kd_bin_count<T, 1, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
   }
   {
     ProfScope prof(K_BIN_SCAN, stream);

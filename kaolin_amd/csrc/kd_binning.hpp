@@ -15,7 +15,7 @@
 //                     bins in the view's region (CSR; the chunk-0 workgroup stores the bases).
 // Layout in the workspace (N = rows of the face arrays):
 //   spans  [N]           Span (8 B)
-//   counts [B][nchunk][nct] int32 (turned into exclusive offsets by the scan)
+//   counts [B][nct][nchunk] int32, tile-major (turned into exclusive offsets by the scan)
 //   totals [B][nct]      int32
 //   base   [B][nct]      int32 start of bin (b, c) inside view b's region, -1 = overflowed
 //   bins   [xper * N]    int32 local face index; view b owns the region [xper*lo, xper*hi) of

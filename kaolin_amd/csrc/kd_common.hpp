@@ -32,6 +32,7 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       32 also skips the fused soft mask's pair math (kd_softpair.hip soft_pairs_tile),
 //       1 << 27 (production too) enables the small-batch forward (kd_soft.hpp dibr_small_batch),
 //       1 << 28 (production too) the balanced (item-dealing) fused forward tiles,
+//       1 << 18 / 1 << 19 skip kd_bin_count's cull coefficients / its LDS tile counts,
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
 int debug_flags();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
@@ -62,8 +63,11 @@ constexpr int kBlock = 256;      // 4 waves
 constexpr int kTile = 16;        // fine tile: 16x16 pixels per workgroup, 8x8 per wave
 constexpr int kChunk = 512;      // faces per binning workgroup (two per thread) ...
 // ... or one per thread when the batch is small, so the binning grids still fill the chip
-__host__ __device__ inline int bin_chunk(int B, int64_t max_per_view) {
-  return (int64_t)B * ((max_per_view + kChunk - 1) / kChunk) < 256 ? kChunk / 2 : kChunk;
+int debug_flags();
+inline int bin_chunk(int B, int64_t max_per_view) {  // (debug flag 1 << 20: always 256)
+  return (int64_t)B * ((max_per_view + kChunk - 1) / kChunk) < 256 || (debug_flags() & (1 << 20))
+             ? kChunk / 2
+             : kChunk;
 }
 constexpr int kMaxCtiles = 1024; // coarse tiles per view (LDS bound of the binning kernels)
 

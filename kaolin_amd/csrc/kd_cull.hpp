@@ -54,14 +54,24 @@ __host__ __device__ inline void raster_cull_coefs_at(const T v[6], float M, int 
                                                      int span_x0, int span_y0, int span_y1,
                                                      float eps, float out[8]) {
   constexpr double kTauScale = sizeof(T) == 8 ? 0x1p-49 : 0x1p-20;  // > 8.04 u
-  out[0] = out[2] = -INFINITY;
-  out[4] = out[6] = INFINITY;
-  out[1] = out[3] = out[5] = out[7] = 0.f;
+  // (scalar slots, constant indices into out[]: a dynamically indexed out[] is a scratch array)
+  float lo0p0 = -INFINITY, lo0p1 = 0.f, lo1p0 = -INFINITY, lo1p1 = 0.f;
+  float hi0p0 = INFINITY, hi0p1 = 0.f, hi1p0 = INFINITY, hi1p1 = 0.f;
+  auto emit = [&]() {
+    out[0] = lo0p0;
+    out[1] = lo0p1;
+    out[2] = lo1p0;
+    out[3] = lo1p1;
+    out[4] = hi0p0;
+    out[5] = hi0p1;
+    out[6] = hi1p0;
+    out[7] = hi1p1;
+  };
   const double ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
   const double vm = fmax(fmax(fmax(fabs(ax), fabs(ay)), fmax(fabs(bx), fabs(by))),
                          fmax(fabs(cx), fabs(cy)));
   const float sxf = M / (float)W, syf = M / (float)H;
-  if (!(vm < 0x1p59) || !(sxf > 0.f) || !(syf > 0.f) || W > 32768 || H > 32768) return;
+  if (!(vm < 0x1p59) || !(sxf > 0.f) || !(syf > 0.f) || W > 32768 || H > 32768) return emit();
   const double E = vm + 1.001 * fabs((double)M);
   // the box extents (corner differences in double; rounded up)
   const double Wb = (fmax(fmax(ax, bx), cx) - fmin(fmin(ax, bx), cx)) * (1.0 + 0x1p-50);
@@ -76,7 +86,8 @@ __host__ __device__ inline void raster_cull_coefs_at(const T v[6], float M, int 
   // |eps| keeps |norm| finite and the quotient a normal number (|w_i| > tau): fp32 |norm| <=
   // 2^126 tau, fp64 far wider
   constexpr double kEpsScale = sizeof(T) == 8 ? 0x1p500 : 0x1p20;
-  if (!(fabs(N) > 6.0 * tau + 0x1p-48 * E * E) || !(fabs((double)eps) <= kEpsScale * tau)) return;
+  if (!(fabs(N) > 6.0 * tau + 0x1p-48 * E * E) || !(fabs((double)eps) <= kEpsScale * tau))
+    return emit();
   const double s = N > 0.0 ? 1.0 : -1.0;
   const double sx = sxf, sy = syf;
   const double y0ref = (double)(M / (float)H * (float)(H - 2 * span_y0 - 1));  // px_cy
@@ -96,15 +107,26 @@ __host__ __device__ inline void raster_cull_coefs_at(const T v[6], float M, int 
     P0 = fmin(fmax(P0, -0x1p14), 0x1p14);
     // the exact signs of the B_i cannot all agree (B0 + B1 + B2 = 0): at most two per side
     if (sB > 0.0) {
-      out[has_lo ? 2 : 0] = (float)P0;
-      out[has_lo ? 3 : 1] = (float)P1;
+      if (has_lo) {
+        lo1p0 = (float)P0;
+        lo1p1 = (float)P1;
+      } else {
+        lo0p0 = (float)P0;
+        lo0p1 = (float)P1;
+      }
       has_lo = true;
     } else {
-      out[has_hi ? 6 : 4] = (float)P0;
-      out[has_hi ? 7 : 5] = (float)P1;
+      if (has_hi) {
+        hi1p0 = (float)P0;
+        hi1p1 = (float)P1;
+      } else {
+        hi0p0 = (float)P0;
+        hi0p1 = (float)P1;
+      }
       has_hi = true;
     }
   }
+  emit();
 }
 
 }  // namespace kd

@@ -1086,6 +1086,23 @@ __device__ __forceinline__ void seg_scan_dpp(int seg, float g[6]) {
   }
 }
 
+// fp64 form: the two 32-bit halves of each sum move by DPP (no LDS permutes)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void seg_scan_dpp(int seg, double g[6]) {
+  int os = __builtin_amdgcn_update_dpp(-1, seg, CTRL, ROWS, 0xf, false);
+  asm volatile("" : "+v"(os));
+  const bool take = os == seg;
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const long long x = __double_as_longlong(g[q]);
+    int lo = __builtin_amdgcn_update_dpp(0, (int)(x & 0xffffffffll), CTRL, ROWS, 0xf, false);
+    int hi = __builtin_amdgcn_update_dpp(0, (int)(x >> 32), CTRL, ROWS, 0xf, false);
+    asm volatile("" : "+v"(lo), "+v"(hi));
+    const double o = __longlong_as_double(((long long)(unsigned)lo) | ((long long)hi << 32));
+    g[q] += take ? o : 0.0;
+  }
+}
+
 template <typename T>
 __device__ __forceinline__ void seg_scan_shfl(int seg, int lane, T g[6]) {
 #pragma unroll
@@ -1162,16 +1179,12 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
       const int prev_key = __shfl_up(key, 1);
       const uint64_t heads = __ballot(lane == 0 || prev_key != key);
       const int seg = __popcll(heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)));
-      if constexpr (std::is_same<T, float>::value) {
-        seg_scan_dpp<0x111, 0xf>(seg, g);  // row_shr:1
-        seg_scan_dpp<0x112, 0xf>(seg, g);  // row_shr:2
-        seg_scan_dpp<0x114, 0xf>(seg, g);  // row_shr:4
-        seg_scan_dpp<0x118, 0xf>(seg, g);  // row_shr:8
-        seg_scan_dpp<0x142, 0xa>(seg, g);  // row_bcast:15 -> rows 1, 3
-        seg_scan_dpp<0x143, 0xc>(seg, g);  // row_bcast:31 -> rows 2, 3
-      } else {
-        seg_scan_shfl<T>(seg, lane, g);
-      }
+      seg_scan_dpp<0x111, 0xf>(seg, g);  // row_shr:1
+      seg_scan_dpp<0x112, 0xf>(seg, g);  // row_shr:2
+      seg_scan_dpp<0x114, 0xf>(seg, g);  // row_shr:4
+      seg_scan_dpp<0x118, 0xf>(seg, g);  // row_shr:8
+      seg_scan_dpp<0x142, 0xa>(seg, g);  // row_bcast:15 -> rows 1, 3
+      seg_scan_dpp<0x143, 0xc>(seg, g);  // row_bcast:31 -> rows 2, 3
       const int next_key = __shfl_down(key, 1);
       const bool tail = key >= 0 && (lane == kWave - 1 || next_key != key);
       if (tail) {

@@ -5,9 +5,16 @@ import subprocess
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'kaolin_amd',
                     'csrc')
+import sys
+sys.path.insert(0, os.path.dirname(CSRC))
+import _build  # noqa: E402  (the library's own flags: same code generation)
+
+only = sys.argv[1:]
 for f in sorted(x[:-4] for x in os.listdir(CSRC) if x.endswith('.hip')):
-    out = subprocess.run(['/opt/rocm/bin/hipcc', '-O3', '-std=c++17', '-fPIC', '-ffp-contract=off',
-                          '--offload-arch=gfx950', '-c', f'{f}.hip', '-o', '/tmp/kd_ru.o',
+    if only and f not in only:
+        continue
+    out = subprocess.run(['/opt/rocm/bin/hipcc', *_build.FLAGS, *_build.SOURCE_FLAGS.get(f + '.hip', []),
+                          '-c', f'{f}.hip', '-o', '/tmp/kd_ru.o',
                           '-Rpass-analysis=kernel-resource-usage'], cwd=CSRC,
                          capture_output=True, text=True).stderr
     cur = None
