@@ -33,6 +33,9 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       1 << 27 (production too) enables the small-batch forward (kd_soft.hpp dibr_small_batch),
 //       1 << 28 (production too) the balanced (item-dealing) fused forward tiles,
 //       1 << 18 / 1 << 19 skip kd_bin_count's cull coefficients / its LDS tile counts,
+//       1 << 16 / 1 << 23 kd_soft_lists: skip every list store / the index and type stores (the
+//       host presets the indices to -1 so that the backward reads no garbage),
+//       2048 (production too) DefTet forward: the per-pixel wave kernel instead of the pooled one,
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
 int debug_flags();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
@@ -74,6 +77,14 @@ constexpr int kMaxCtiles = 1024; // coarse tiles per view (LDS bound of the binn
 // ------------------------------------------------------------------------------------------
 // pixel centres, identical to the reference expression `multiplier / width * (2*w + 1 - width)`
 // ------------------------------------------------------------------------------------------
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// outstanding global stores (__syncthreads' workgroup fence drains vmcnt to 0, which serialises a
+// loop of store-heavy tiles on the store latency).  Global memory written before it is NOT
+// visible to the other waves after it.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ float px_cx(float M, int W, int w) {
   return M / (float)W * (float)(2 * w + 1 - W);
 }

@@ -82,19 +82,27 @@ __device__ __forceinline__ bool dt_face_box(const T *fvi, const T *bbox, int64_t
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_dt_bin(int64_t F, int64_t N, int G, const T *fvi,
-                                                    const T *bbox, int *cursor, int *lists) {
+                                                    const T *bbox, int *cursor, int *lists,
+                                                    T *boxes) {
   __shared__ int s_cnt[kDtGridMax * kDtGridMax];
   const int b = blockIdx.y, cells = G * G;
   const int64_t f = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   for (int i = threadIdx.x; i < cells; i += kBlock) s_cnt[i] = 0;
   __syncthreads();
-  T xmin, ymin, xmax, ymax;
+  T xmin = 0, ymin = 0, xmax = 0, ymax = 0;
   int cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
   if (f < F && dt_face_box<T>(fvi, bbox, (int64_t)b * F + f, xmin, ymin, xmax, ymax)) {
     cx0 = dt_cell(xmin, G);
     cx1 = dt_cell(xmax, G);
     cy0 = dt_cell(ymin, G);
     cy1 = dt_cell(ymax, G);
+  }
+  if (boxes && f < F) {  // the walk's box table (a NaN box is in no list: its value is unused)
+    T *q = boxes + ((int64_t)b * F + f) * 4;
+    q[0] = xmin;
+    q[1] = ymin;
+    q[2] = xmax;
+    q[3] = ymax;
   }
   for (int cy = cy0; cy <= cy1; ++cy)
     for (int cx = cx0; cx <= cx1; ++cx) atomicAdd(&s_cnt[cy * G + cx], 1);
@@ -161,6 +169,7 @@ struct DtArgs {
   const T *fvi;     // (B, F, 3, 2)
   const T *feat;    // (B, F, 3, D)
   const int *cursor, *lists;
+  const T *boxes;     // (B, F, 4): xmin, ymin, xmax, ymax of every face (bbox or kd_dt_bin's)
   T *interp;          // (B, P, K, D)
   int64_t *face_idx;  // (B, P, K)
   T *weights;         // (B, P, K, 3)
@@ -168,12 +177,13 @@ struct DtArgs {
   // per slot in face-index order (unsorted) face, depth, w0, w1 instead of interp / weights
   const T *bbox;      // (B, F, 4) or nullptr
   T *depth, *w0, *w1; // (B, P, K) each, or nullptr (sorted mode)
+  int dbg;            // diagnostic ablation flags (kd_common.hpp)
 };
 
 constexpr int kDtWaves = 4;  // pixels per workgroup
 
 template <typename T>
-__host__ __device__ inline size_t dt_wave_lds(int C) {  // depth, w0, w1, face, face rank
+__host__ __device__ constexpr size_t dt_wave_lds(int C) {  // depth, w0, w1, face, face rank
   return (size_t)C * (3 * sizeof(T) + 2 * sizeof(int));
 }
 
@@ -185,16 +195,12 @@ __host__ __device__ inline size_t dt_wave_lds(int C) {  // depth, w0, w1, face, 
 // depth, descending, ties by face index, and each slot writes face index, weights
 // (w0, w1, 1 - (w0 + w1)) and interpolated features; empty slots get -1 / 0.
 template <typename T>
-__global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
-  extern __shared__ __align__(16) char dt_lds[];
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+__device__ void dt_pixel_wave(const DtArgs<T> &a, int b, int64_t p, char *wave_lds) {
+  const int lane = threadIdx.x & 63;
   const int K = a.K, C = a.C;
-  T *dep = (T *)(dt_lds + (size_t)w * dt_wave_lds<T>(C));
+  T *dep = (T *)wave_lds;
   T *lw0 = dep + C, *lw1 = lw0 + C;
   int *fid = (int *)(lw1 + C);
-  const int b = blockIdx.y;
-  const int64_t p = (int64_t)blockIdx.x * kDtWaves + w;
-  if (p >= a.P) return;  // whole wave
   const int64_t pp = (int64_t)b * a.P + p;
   const T x0 = a.px[2 * pp], y0 = a.px[2 * pp + 1];
   const T dmin = a.range[2 * pp], dmax = a.range[2 * pp + 1];
@@ -321,11 +327,274 @@ __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
   }
 }
 
-static size_t dt_workspace(int B, int64_t F) {
+template <typename T>
+__global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
+  extern __shared__ __align__(16) char dt_lds[];
+  const int w = threadIdx.x >> 6;
+  const int64_t p = (int64_t)blockIdx.x * kDtWaves + w;
+  if (p >= a.P) return;  // whole wave
+  dt_pixel_wave<T>(a, blockIdx.y, p, dt_lds + (size_t)w * dt_wave_lds<T>(a.C));
+}
+
+// Pooled forward (knum <= kDtMaxK): one wave (its own workgroup) takes 16 consecutive pixels.
+//   walk      the pixels' cell lists, four pixels at a time (four independent list -> box load
+//             chains in flight), with the box test only (one 16-byte box per lane); the faces
+//             whose half-open box holds the pixel go to the wave's LDS candidate ring, tagged with
+//             the pixel (~25 per pixel on the bench's sphere: the boxes of its thin triangles are
+//             large next to the ~2 hits)
+//   test      whenever the ring holds 64 candidates, the reference's exact test (eps-normalised
+//             divisions, depth range) runs on them with every lane busy -- the per-pixel walk ran
+//             its divisions for every 64-face step with ~3% of the lanes inside a box; hits go to
+//             the wave's hit pool
+//   rank      face rank within the pixel (the reference keeps the first knum hits by face index),
+//             then depth rank (descending, ties by face index) -> slot table
+//   store     the 16 pixels' outputs are one contiguous run per array: written in memory order
+// A pixel with a hit beyond the pool is redone by the per-pixel wave path (dt_pixel_wave, with its
+// bisection for any number of hits), in LDS the pool no longer uses.  Candidate order is
+// irrelevant: selection and output order depend on face index and depth only.
+constexpr int kDtPx = 16;      // pixels per wave (= workgroup)
+constexpr int kDtRing = 512;   // candidate ring (< 64 + 4 x 64 entries live)
+constexpr int kDtHits = 256;   // hit pool per wave
+constexpr int kDtMaxK = 32;    // knum bound of the pooled path (slot table)
+
+template <typename T>
+struct DtPoolLDS {
+  struct Work {
+    int cface[kDtRing];      // candidates: face, pixel
+    uint8_t cpix[kDtRing];
+    int hface[kDtHits];      // hits: face, depth, w0, w1, pixel, face rank within the pixel
+    T hdep[kDtHits], hw0[kDtHits], hw1[kDtHits];
+    uint8_t hpix[kDtHits];
+    short hrank[kDtHits];
+  };
+  union {
+    Work w;
+    char fb[dt_wave_lds<T>(256)];  // the per-pixel fallback's lists (C = 256)
+  } u;
+  T x[kDtPx], y[kDtPx], dmin[kDtPx], dmax[kDtPx];
+  int64_t lofs[kDtPx];
+  int nl[kDtPx], nh[kDtPx];
+  short slot[kDtPx][kDtMaxK];
+  unsigned ovf;  // pixels whose hits did not all fit the pool
+};
+
+template <typename T>
+__device__ __forceinline__ void dt_load_box(const T *boxes, int64_t i, T bx[4]) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 q = *(const float4 *)(boxes + i * 4);
+    bx[0] = q.x;
+    bx[1] = q.y;
+    bx[2] = q.z;
+    bx[3] = q.w;
+  } else {
+    const double2 q0 = *(const double2 *)(boxes + i * 4);
+    const double2 q1 = *(const double2 *)(boxes + i * 4 + 2);
+    bx[0] = q0.x;
+    bx[1] = q0.y;
+    bx[2] = q1.x;
+    bx[3] = q1.y;
+  }
+}
+
+__device__ __forceinline__ int lane_rank(uint64_t m) {  // set lanes of m below this lane
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+template <typename T>
+__global__ __launch_bounds__(kWave) void kd_dt_fwd_pool(DtArgs<T> a) {
+  __shared__ DtPoolLDS<T> s;
+  typename DtPoolLDS<T>::Work &wk = s.u.w;
+  const int lane = threadIdx.x;
+  const int b = blockIdx.y, K = a.K, G = a.G;
+  const int64_t p0 = (int64_t)blockIdx.x * kDtPx;
+  const int npx = (int)min((int64_t)kDtPx, a.P - p0);
+  if (lane < kDtPx) {
+    int n = 0;
+    int64_t lofs = 0;
+    if (lane < npx) {
+      const int64_t pp = (int64_t)b * a.P + p0 + lane;
+      const T x0 = a.px[2 * pp], y0 = a.px[2 * pp + 1];
+      s.x[lane] = x0;
+      s.y[lane] = y0;
+      s.dmin[lane] = a.range[2 * pp];
+      s.dmax[lane] = a.range[2 * pp + 1];
+      const int c = dt_cell(y0, G) * G + dt_cell(x0, G);
+      n = a.cursor[(int64_t)b * G * G + c];
+      lofs = (int64_t)c * a.N + (int64_t)b * a.F;
+    }
+    s.nl[lane] = n;
+    s.lofs[lane] = lofs;
+    s.nh[lane] = 0;
+  }
+  if (lane == 0) s.ovf = 0;
+  wave_lds_sync();
+  const T *boxes = a.boxes + (int64_t)b * a.F * 4;
+  const T *fvi = a.fvi + (int64_t)b * a.F * 6;
+  const T *fvz = a.fvz + (int64_t)b * a.F * 3;
+  const T *bbox = a.bbox ? a.bbox + (int64_t)b * a.F * 4 : nullptr;
+  const T eps = (T)a.eps;
+  int head = 0, tail = 0, nhit = 0;  // wave-uniform
+  // the exact test on ring entries [head, head + m)
+  auto flush = [&](int m) {
+    const int idx = (head + lane) & (kDtRing - 1);
+    bool hit = false;
+    int q = 0, f = 0;
+    T w0 = 0, w1 = 0, depth = 0;
+    if (lane < m && !ablate(a.dbg, 1)) {  // (diagnostics: 1 = no exact tests)
+      q = wk.cpix[idx];
+      f = wk.cface[idx];
+      hit = dt_face_test<T>(fvi + (int64_t)f * 6, fvz + (int64_t)f * 3,
+                            bbox ? bbox + (int64_t)f * 4 : nullptr, s.x[q], s.y[q], s.dmin[q],
+                            s.dmax[q], eps, w0, w1, depth);
+    }
+    const uint64_t hm = __ballot(hit);
+    if (hit) {
+      const int at = nhit + lane_rank(hm);
+      if (at < kDtHits) {
+        wk.hface[at] = f;
+        wk.hdep[at] = depth;
+        wk.hw0[at] = w0;
+        wk.hw1[at] = w1;
+        wk.hpix[at] = (uint8_t)q;
+        atomicAdd(&s.nh[q], 1);
+      } else {
+        atomicOr(&s.ovf, 1u << q);
+      }
+    }
+    nhit += __popcll(hm);
+    head += m;
+    wave_lds_sync();
+  };
+  constexpr int U = 4;
+  for (int g = 0; g < kDtPx / U; ++g) {
+    int n[U], steps = 0;
+    int64_t lofs[U];
+    T x[U], y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = g * U + u;
+      n[u] = s.nl[q];
+      lofs[u] = s.lofs[q];
+      x[u] = s.x[q];
+      y[u] = s.y[q];
+      steps = max(steps, (n[u] + kWave - 1) / kWave);
+    }
+    for (int t = 0; t < steps; ++t) {
+      const int j = t * kWave + lane;
+      int f[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) f[u] = j < n[u] ? a.lists[lofs[u] + j] : -1;
+      if (ablate(a.dbg, 2)) continue;  // diagnostics: list loads only
+      T bx[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (f[u] >= 0) dt_load_box<T>(boxes, f[u], bx[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        // the reference's half-open box test (deftet_cuda.cu:124-127)
+        const bool in = f[u] >= 0 && x[u] >= bx[u][0] && x[u] < bx[u][2] && y[u] >= bx[u][1] &&
+                        y[u] < bx[u][3];
+        const uint64_t m = __ballot(in);
+        if (in) {
+          const int at = (tail + lane_rank(m)) & (kDtRing - 1);
+          wk.cface[at] = f[u];
+          wk.cpix[at] = (uint8_t)(g * U + u);
+        }
+        tail += __popcll(m);
+      }
+      wave_lds_sync();
+      while (tail - head >= kWave) flush(kWave);
+    }
+  }
+  if (tail > head) flush(tail - head);
+  // ranks within each pixel
+  const int nk = min(nhit, kDtHits);
+  const unsigned ovf = s.ovf;
+  for (int i = lane; i < nk; i += kWave) {
+    const int q = wk.hpix[i], fi = wk.hface[i];
+    int r = 0;
+    if (s.nh[q] > K || a.depth)  // the face rank: needed for a cut and for the op form's slots
+      for (int j = 0; j < nk; ++j) r += (wk.hpix[j] == q && wk.hface[j] < fi) ? 1 : 0;
+    wk.hrank[i] = (short)r;
+  }
+  wave_lds_sync();
+  for (int i = lane; i < nk; i += kWave) {
+    const int q = wk.hpix[i];
+    if (wk.hrank[i] >= K || ((ovf >> q) & 1)) continue;
+    int r;
+    if (a.depth) {  // op form: slot = face rank (deftet_cuda.cu:166-180), unsorted
+      r = wk.hrank[i];
+    } else {        // depth descending, then face index (deftet.py:300-303, stable order)
+      const T di = wk.hdep[i];
+      const int fi = wk.hface[i];
+      r = 0;
+      for (int j = 0; j < nk; ++j) {
+        const T dj = wk.hdep[j];
+        r += (wk.hpix[j] == q && wk.hrank[j] < K && (dj > di || (dj == di && wk.hface[j] < fi)))
+                 ? 1
+                 : 0;
+      }
+    }
+    s.slot[q][r] = (short)i;
+  }
+  wave_lds_sync();
+  // stores: element e = (pixel, slot) of the wave's contiguous run, lanes on consecutive elements
+  {
+    const int ne = npx * K, stq = kWave / K, sts = kWave % K;
+    int q = lane / K, sl = lane - (lane / K) * K;
+    const int64_t row0 = ((int64_t)b * a.P + p0) * K;
+    const int D = a.D;
+    const T *feat = a.feat ? a.feat + (int64_t)b * a.F * 3 * D : nullptr;
+    for (int e = lane; e < ne; e += kWave) {
+      if (!((ovf >> q) & 1)) {
+        const int kept = min(s.nh[q], K);
+        const int h = sl < kept ? s.slot[q][sl] : -1;
+        const int64_t o = row0 + e;
+        if (a.depth) {  // op form: empty slots -1 / -inf / 0 / 0 (deftet.cpp:88-94)
+          a.face_idx[o] = h >= 0 ? (int64_t)wk.hface[h] : -1;
+          a.depth[o] = h >= 0 ? wk.hdep[h] : (T)-INFINITY;
+          a.w0[o] = h >= 0 ? wk.hw0[h] : (T)0;
+          a.w1[o] = h >= 0 ? wk.hw1[h] : (T)0;
+        } else if (h >= 0) {
+          const int fi = wk.hface[h];
+          const T w0 = wk.hw0[h], w1 = wk.hw1[h];
+          const T w2 = (T)1 - (w0 + w1);  // deftet.py:304
+          a.face_idx[o] = fi;
+          a.weights[3 * o] = w0;
+          a.weights[3 * o + 1] = w1;
+          a.weights[3 * o + 2] = w2;
+          const T *cf = feat + (int64_t)fi * 3 * D;
+          for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
+            a.interp[o * D + d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+        } else {
+          a.face_idx[o] = -1;
+          a.weights[3 * o] = (T)0;
+          a.weights[3 * o + 1] = (T)0;
+          a.weights[3 * o + 2] = (T)0;
+          for (int d = 0; d < D; ++d) a.interp[o * D + d] = (T)0;
+        }
+      }
+      q += stq;
+      sl += sts;
+      if (sl >= K) {
+        sl -= K;
+        ++q;
+      }
+    }
+  }
+  if (!ovf) return;
+  wave_lds_sync();  // the pool's LDS becomes the fallback's
+  for (int q = 0; q < npx; ++q)
+    if ((ovf >> q) & 1) dt_pixel_wave<T>(a, b, p0 + q, s.u.fb);
+}
+
+static size_t dt_workspace(int B, int64_t F, size_t esize) {
   const int64_t N = (int64_t)B * F;
   const int64_t cells = (int64_t)dt_grid(N) * dt_grid(N);
   return align_up(sizeof(int) * (size_t)B * cells) +
-         align_up(sizeof(int) * (size_t)cells * (size_t)(N > 0 ? N : 1));
+         align_up(sizeof(int) * (size_t)cells * (size_t)(N > 0 ? N : 1)) +
+         align_up(4 * esize * (size_t)N);  // the face boxes
 }
 
 static int dt_capacity(int K) { return K < 256 ? 256 : K; }
@@ -343,7 +612,7 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
   const size_t lds = dt_wave_lds<T>(C) * kDtWaves;
   KD_CHECK_ARG(lds <= 160 * 1024, "deftet: knum too large for the LDS list (fp32 <= 2048, "
                                   "fp64 <= 1280)");
-  const size_t need = dt_workspace(B, F);
+  const size_t need = dt_workspace(B, F, sizeof(T));
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   if (B == 0 || P == 0) return KD_OK;
@@ -351,25 +620,34 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
   const int G = dt_grid(N);
   int *cursor = (int *)ws;
   int *lists = (int *)((char *)ws + align_up(sizeof(int) * (size_t)B * G * G));
+  T *boxes = (T *)((char *)lists + align_up(sizeof(int) * (size_t)G * G * (size_t)(N > 0 ? N : 1)));
   hipError_t e = hipMemsetAsync(cursor, 0, sizeof(int) * (size_t)B * G * G, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "deftet: %s", hipGetErrorString(e));
   if (F > 0) {
     ProfScope prof(K_DT_BIN, stream);
     hipLaunchKernelGGL(kd_dt_bin<T>, dim3((unsigned)((F + kBlock - 1) / kBlock), B),
-                       dim3(kBlock), 0, stream, F, N, G, fvi, bbox, cursor, lists);
+                       dim3(kBlock), 0, stream, F, N, G, fvi, bbox, cursor, lists,
+                       bbox ? nullptr : boxes);
   }
   DtArgs<T> a{B,   P,      F,     N,      K,       D,        C,       G,
               eps, px,     range, fvz,    fvi,     feat,     cursor,  lists,
-              interp, face_idx, weights, bbox, depth, w0, w1};
-  const int64_t gx = (P + kDtWaves - 1) / kDtWaves;
+              bbox ? bbox : boxes, interp, face_idx, weights, bbox, depth, w0, w1,
+              debug_flags()};
+  // the pooled kernel for knum <= 32 (diagnostic flag 2048: the per-pixel wave kernel)
+  const bool pooled = K <= kDtMaxK && !(debug_flags() & 2048);
+  const int64_t gx = pooled ? (P + kDtPx - 1) / kDtPx : (P + kDtWaves - 1) / kDtWaves;
   KD_CHECK_ARG(gx < (1ll << 31), "deftet: too many pixels");
   {
     ProfScope prof(K_DT_FWD, stream);
-    if (lds > 64 * 1024)
-      (void)hipFuncSetAttribute((const void *)kd_dt_fwd<T>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL(kd_dt_fwd<T>, dim3((unsigned)gx, B), dim3(kWave * kDtWaves), lds, stream,
-                       a);
+    if (pooled) {
+      hipLaunchKernelGGL(kd_dt_fwd_pool<T>, dim3((unsigned)gx, B), dim3(kWave), 0, stream, a);
+    } else {
+      if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void *)kd_dt_fwd<T>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kd_dt_fwd<T>, dim3((unsigned)gx, B), dim3(kWave * kDtWaves), lds, stream,
+                         a);
+    }
   }
   e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "deftet fwd: %s", hipGetErrorString(e));
@@ -399,8 +677,7 @@ extern "C" {
 
 size_t kd_deftet_workspace_size(int B, int64_t F, int double_precision) {
   if (B < 0 || F < 0) return 0;
-  (void)double_precision;
-  return dt_workspace(B, F);
+  return dt_workspace(B, F, double_precision ? sizeof(double) : sizeof(float));
 }
 
 int kd_deftet_sparse_render_forward_f32(int B, int64_t P, int64_t F, int knum, int D,

@@ -161,73 +161,123 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_atomic(
   }
 }
 
-// The same backward over given close lists, read in memory order: per 256-pixel block, the
-// uncovered pixels whose first slot holds a face are compacted in LDS; then each half-wave (K <=
-// 32) or wave (K > 32, 64 slots at a time) takes one listed pixel's row of K slots -- consecutive
+// The same backward over given close lists, per 16x16 tile of pixels (grid-stride): the tile's
+// uncovered pixels whose first slot holds a face are compacted in LDS; each half-wave (K <= 32)
+// or wave (K > 32, 64 slots at a time) takes one listed pixel's row of K slots -- consecutive
 // lanes, consecutive elements -- and its lanes up to the row's first -1 (a ballot: the
-// reference's loop stops there, dibr_soft_mask_cuda.cu:273-276) add their pair's terms.  The
-// lane-per-pixel form read each row with one lane (K strided loads per pixel).
+// reference's loop stops there, dibr_soft_mask_cuda.cu:273-276) compute their pair's terms.  The
+// terms are summed per face in an LDS hash table (a face is close to many pixels of a tile) and
+// each (tile, face, coordinate) sum goes out with one float atomic: the per-pair atomics of the
+// lane-per-pixel form (10 M at C3, ~85 % of its time) contended on the faces' lines.  A pair
+// whose face finds no slot (a full table) adds its terms directly.
+constexpr int kListHash = 1024;  // LDS face slots per tile
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
     int B, int H, int W, int64_t F, int K, const T *__restrict__ grad_soft,
     const T *__restrict__ soft, const int64_t *__restrict__ face_idx, const T *__restrict__ prob,
     const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
-    const T *__restrict__ fvi, float sigmainv, float M, T *grad_fvi) {
+    const T *__restrict__ fvi, float sigmainv, float M, T *grad_fvi, int dbg) {
   __shared__ int64_t s_pix[kBlock];
   __shared__ int s_cnt[kBlock / kWave];
-  const int64_t P = (int64_t)H * W;
-  const int64_t total = (int64_t)B * P;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  auto pair = [&](int64_t p, int s) {  // one (pixel, slot) entry holding face >= 0
+  __shared__ int s_key[kListHash];
+  __shared__ T s_acc[kListHash][6];
+  const int ntx = (W + kTile - 1) / kTile, nty = (H + kTile - 1) / kTile;
+  const int64_t ntiles = (int64_t)B * ntx * nty;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  for (int i = tid; i < kListHash; i += kBlock) {
+    s_key[i] = -1;
+#pragma unroll
+    for (int c = 0; c < 6; ++c) s_acc[i][c] = (T)0;
+  }
+  auto pair = [&](int64_t p, int b, int x, int h, int s) {  // one (pixel, slot) entry, face >= 0
     const int64_t e = p * K + s;
-    const int64_t f = cidx[e];
-    const int64_t b = p / P;
-    const int64_t rem = p - b * P;
-    const int h = (int)(rem / W), x = (int)(rem - (int64_t)h * W);
-    const int64_t sf = b * F + f;
+    const int64_t sf = (int64_t)b * F + cidx[e];
     T v[6];
 #pragma unroll
     for (int c = 0; c < 6; ++c) v[c] = fvi[sf * 6 + c];
     T g[6] = {0, 0, 0, 0, 0, 0};
     soft_bwd_terms<T>((T)px_cx(M, W, x), (T)px_cy(M, H, h), v, (int)ctype[e] - 1, prob[e],
                       grad_soft[p], soft[p], sigmainv, M, g);
+    if (ablate(dbg, 1 << 22)) {  // diagnostics: no accumulation (one plain store keeps the math)
+      if (g[0] + g[1] + g[2] + g[3] + g[4] + g[5] == (T)12345) grad_fvi[0] = (T)1;
+      return;
+    }
+    unsigned u = ((unsigned)sf * 2654435761u) >> 22;  // 10 bits
+    int slot = -1;
+    for (int probe = 0; probe < 32; ++probe) {
+      const int old = atomicCAS(&s_key[u], -1, (int)sf);
+      if (old == -1 || old == (int)sf) {
+        slot = (int)u;
+        break;
+      }
+      u = (u + 1) & (kListHash - 1);
+    }
 #pragma unroll
     for (int c = 0; c < 6; ++c)
-      if (g[c] != (T)0) atomicAdd(grad_fvi + sf * 6 + c, g[c]);
+      if (g[c] != (T)0) {
+        if (slot >= 0)
+          atomicAdd(&s_acc[slot][c], g[c]);
+        else
+          atomicAdd(grad_fvi + sf * 6 + c, g[c]);
+      }
   };
-  for (int64_t p0 = (int64_t)blockIdx.x * kBlock; p0 < total; p0 += (int64_t)gridDim.x * kBlock) {
-    const int64_t p = p0 + threadIdx.x;
-    const bool live = p < total && face_idx[p] < 0 && cidx[p * K] >= 0;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int b = (int)(tile / ((int64_t)ntx * nty));
+    const int tl = (int)(tile - (int64_t)b * ntx * nty);
+    const int X0 = (tl % ntx) * kTile, Y0 = (tl / ntx) * kTile;
+    const int px = X0 + (tid & 15), py = Y0 + (tid >> 4);
+    const bool in = px < W && py < H;
+    const int64_t p = ((int64_t)b * H + py) * W + px;
+    const bool live = in && face_idx[p] < 0 && cidx[p * K] >= 0;
     int n;
-    const int pos = wg_compact(live, s_cnt, n);
-    if (live) s_pix[pos] = p;
+    const int pos = wg_compact(live, s_cnt, n);  // (its barriers also order the table reset)
+    if (live) s_pix[pos] = ((int64_t)tid << 48) | p;  // tile pixel + image pixel
     __syncthreads();
+    auto run = [&](int i, int s) {  // pixel i of the list, slot s
+      const int64_t ent = s_pix[i];
+      const int q = (int)(ent >> 48);
+      pair(ent & 0xffffffffffffll, b, X0 + (q & 15), Y0 + (q >> 4), s);
+    };
     if (K <= 32) {  // two rows per wave step (half-waves), rows dealt to the waves in turn
       const int half = lane >> 5, s = lane & 31;
       for (int i0 = 2 * w; i0 < n; i0 += 2 * (kBlock / kWave)) {
         const int i = i0 + half;
-        const int64_t pp = i < n ? s_pix[i] : 0;
-        const bool in = i < n && s < K;
-        const bool stop = !in || cidx[pp * K + s] < 0;
+        const int64_t pp = i < n ? (s_pix[i] & 0xffffffffffffll) : 0;
+        const bool in2 = i < n && s < K;
+        const bool stop = !in2 || cidx[pp * K + s] < 0;
         const uint64_t sm = __ballot(stop);
         const uint32_t hm = (uint32_t)(sm >> (32 * half));  // this half's stops
         const int first = hm ? __builtin_ctz(hm) : 32;
-        if (in && s < first) pair(pp, s);
+        if (in2 && s < first) run(i, s);
       }
     } else {  // one row per wave, 64 slots at a time until its first -1
       for (int i = w; i < n; i += kBlock / kWave) {
-        const int64_t pp = s_pix[i];
+        const int64_t pp = s_pix[i] & 0xffffffffffffll;
         for (int s0 = 0; s0 < K; s0 += kWave) {
           const int s = s0 + lane;
           const bool stop = s >= K || cidx[pp * K + s] < 0;
           const uint64_t sm = __ballot(stop);
           const int first = sm ? __builtin_ctzll(sm) : kWave;
-          if (lane < first) pair(pp, s);
+          if (lane < first) run(i, s);
           if (sm) break;
         }
       }
     }
-    __syncthreads();  // s_pix is reused by the next block of pixels
+    __syncthreads();
+    // flush the tile's face sums (one atomic per nonzero (face, coordinate)) and reset the table
+    for (int i = tid; i < kListHash; i += kBlock) {
+      const int key = s_key[i];
+      if (key < 0) continue;
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const T v = s_acc[i][c];
+        if (v != (T)0) atomicAdd(grad_fvi + (int64_t)key * 6 + c, v);
+        s_acc[i][c] = (T)0;
+      }
+      s_key[i] = -1;
+    }
+    __syncthreads();
   }
 }
 
@@ -278,15 +328,17 @@ int soft_backward(int B, int H, int W, int64_t F, int K, const T *grad_soft, con
   if (total > 0 && nf > 0 && K > 0) {
     const int64_t blocks = (total + kBlock - 1) / kBlock;
     ProfScope prof(K_SOFT_BWD_ATOMIC, stream);
+    const int64_t tiles = (int64_t)B * ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
+    const unsigned tgrid = (unsigned)(tiles < 8192 ? tiles : 8192);
     if (debug_flags() & (1 << 29))  // diagnostics: the lane-per-pixel form
       hipLaunchKernelGGL(kd_soft_bwd_atomic<T>, dim3(grid), dim3(kBlock), 0, stream, B, H, W, F,
                          K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
                          grad_fvi);
     else
-      hipLaunchKernelGGL(kd_soft_bwd_lists<T>, dim3(grid), dim3(kBlock), 0, stream, B, H, W, F,
+      hipLaunchKernelGGL(kd_soft_bwd_lists<T>, dim3(tgrid), dim3(kBlock), 0, stream, B, H, W, F,
                          K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
-                         grad_fvi);
+                         grad_fvi, debug_flags());
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));

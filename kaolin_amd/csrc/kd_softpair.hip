@@ -927,17 +927,27 @@ __global__ __launch_bounds__(kBlock) void kd_soft_reduce(SoftArgs<T> a, SoftPair
 }
 
 // The split pipeline's soft mask and close-face lists, one workgroup per tile (grid-stride over
-// every tile: the lists of a tile without records are all padding): the tile's records are
-// placed in an LDS (slot, pixel) table kReduceSlots slots at a time; each pixel multiplies its
-// slots in order (dibr_soft_mask_cuda.cu:174-181, double-promoted), and the lists -- values
-// (:165-171) and the -1 / 0 / 0 padding of the unused slots (dibr_soft_mask.cpp:86-97) -- are
-// written in memory order: consecutive threads take consecutive elements of each tile row's
-// contiguous (16 pixels x K) block, so the 13 K bytes per pixel go out as whole lines (the
-// per-pixel rows of K elements written by one lane each were a 17x slower store shape).
+// every tile: the lists of a tile without records are all padding): kReduceSlots slots at a time,
+// the tile's records put their values -- probability, face, type -- into LDS (slot, pixel)
+// tables (coalesced record reads); each pixel multiplies its slots in order
+// (dibr_soft_mask_cuda.cu:174-181, double-promoted), and the lists -- values (:165-171) and the
+// -1 / 0 / 0 padding of the unused slots (dibr_soft_mask.cpp:86-97) -- are written in memory
+// order from LDS alone: consecutive threads take consecutive elements (slot pairs: 8 / 16 /
+// 2-byte stores with an even knum) of each tile row's contiguous (16 pixels x K) block, so the
+// 13 K bytes per pixel go out as whole lines (the per-pixel rows of K elements written by one
+// lane each were a 17x slower store shape; gathering each element's record from L2 inside the
+// store loop left the loop latency-bound).  Half tiles of 8 rows (8192 -> 16384 work units, the
+// tables halved: 4 workgroups per CU instead of 2).  Dynamic LDS: T val[128][33],
+// int face_type[128][33], int np[128].
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_lists(SoftArgs<T> a, SoftPairBuf<T> pb) {
-  __shared__ unsigned short s_ri[kReduceSlots][kBlock];  // (slot, pixel) -> record in the tile
-  __shared__ int s_np[kBlock];
+  extern __shared__ unsigned char s_raw[];
+  // [pixel][slot] with an odd row stride: the store loop's lanes read consecutive slots of one
+  // pixel, the product's lanes one slot of consecutive pixels -- both bank-conflict free
+  constexpr int R = kReduceSlots + 1, HP = kBlock / 2;
+  T(*s_val)[R] = (T(*)[R])s_raw;
+  int(*s_ft)[R] = (int(*)[R])(s_raw + sizeof(T) * R * HP);
+  int *s_np = (int *)(s_raw + (sizeof(T) + sizeof(int)) * R * HP);
   const int K = a.K, H = a.fs.H, W = a.fs.W;
   const int tid = threadIdx.x;
   const int64_t nz = a.nzero0 + a.nzero1;  // side job: zero fills (grid-stride, coalesced)
@@ -947,53 +957,97 @@ __global__ __launch_bounds__(kBlock) void kd_soft_lists(SoftArgs<T> a, SoftPairB
     else
       a.zero1[i - a.nzero0] = (T)0;
   }
-  const int64_t ntl = (int64_t)a.fs.B * pb.ntiles;
-  for (int64_t tile = blockIdx.x; tile < ntl; tile += gridDim.x) {
+  // half tiles: rows 0-7 (tile pixels q < 128) and rows 8-15 of a tile, so that the tables are
+  // half the size and twice the workgroups fit a CU (the loop is store / load latency bound)
+  const int64_t nht = 2 * (int64_t)a.fs.B * pb.ntiles;
+  for (int64_t ht = blockIdx.x; ht < nht; ht += gridDim.x) {
+    const int64_t tile = ht >> 1;
+    const int half = (int)(ht & 1), q0 = half * HP;
     const int n = pb.ntile[tile];
     if (n < 0) continue;  // overflowed: kd_soft_ovf_fwd wrote its soft mask and lists
     const int64_t base = pb.tbase[tile];
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
-    const int X0 = (tl % pb.ntx) * kTile, Y0 = (tl / pb.ntx) * kTile;
-    const int nx = min(kTile, W - X0), ny = min(kTile, H - Y0);
+    const int X0 = (tl % pb.ntx) * kTile, Y0 = (tl / pb.ntx) * kTile + half * (kTile / 2);
+    const int nx = min(kTile, W - X0), ny = max(0, min(kTile / 2, H - Y0));
     int64_t lo, hi;
     view_range(a.fs, b, lo, hi);
-    int px, py;
-    tile_pixel(tl % pb.ntx, tl / pb.ntx, tid, px, py);
+    int px = W, py = H;
+    if (tid < HP) tile_pixel(tl % pb.ntx, tl / pb.ntx, q0 + tid, px, py);
     const bool in = px < W && py < H;
     const int64_t p = ((int64_t)b * H + py) * W + px;
     const int np = in ? pb.npix[p] : 0;
-    __syncthreads();  // the previous tile is done with s_np / s_ri
-    s_np[tid] = np;
+    lds_barrier();  // the previous tile is done with the tables
+    if (tid < HP) s_np[tid] = np;
     T prod = (T)1.0;
     for (int s0 = 0; s0 < K; s0 += kReduceSlots) {
       const int S = min(kReduceSlots, K - s0);
-      __syncthreads();  // the previous pass is done with s_ri (and s_np is written)
-      for (int i = tid; i < n; i += kBlock) {
-        const uint32_t sq = ((const uint32_t *)(pb.rec + base + i))[1];  // slot | q << 16
-        const int s = (int)(sq & 0xffffu) - s0;
-        if (s >= 0 && s < S) s_ri[s][(sq >> 16) & 0xffu] = (unsigned short)i;
+      lds_barrier();  // the previous pass is done with the tables (and s_np is written)
+      // four records per thread in flight (the pass is load-latency bound otherwise)
+      for (int i0 = tid; i0 < n; i0 += 4 * kBlock) {
+        SoftPairRec rr[4];
+        T pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = min(i0 + u * kBlock, n - 1);
+          rr[u] = pb.rec[base + i];
+          pv[u] = pb.sprob[base + i];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int s = (int)rr[u].slot - s0, q = (int)rr[u].q - q0;
+          if (i0 + u * kBlock < n && s >= 0 && s < S && q >= 0 && q < HP) {
+            s_val[q][s] = pv[u];
+            s_ft[q][s] = (int)(((int64_t)rr[u].row - lo) << 3) | (rr[u].type + 1);
+          }
+        }
       }
-      __syncthreads();
+      lds_barrier();
       const int e_hi = min(np - s0, S);
-      for (int s = 0; s < e_hi; ++s)
-        prod = (T)((double)prod * (1.0 - (double)pb.sprob[base + s_ri[s][tid]]));
-      // the pass's slots of the tile's rows, in memory order
-      const int per_row = nx * S;
-      for (int e = tid; e < ny * per_row; e += kBlock) {
-        const int r = e / per_row, rem = e - r * per_row;
-        const int i = rem / S, s = rem - i * S;
-        const int q = ((r >> 3) * 2 + (i >> 3)) * kWave + (r & 7) * 8 + (i & 7);
-        const int64_t o = (((int64_t)b * H + Y0 + r) * W + X0 + i) * K + s0 + s;
+      for (int s = 0; s < e_hi; ++s) prod = (T)((double)prod * (1.0 - (double)s_val[tid][s]));
+      // the pass's slots of the half tile's rows, in memory order
+      auto value = [&](int q, int s, T &pv, int64_t &cv, uint8_t &tv) {
         if (s0 + s < s_np[q]) {
-          const int64_t ri = base + s_ri[s][q];
-          const SoftPairRec rr = pb.rec[ri];
-          a.prob[o] = pb.sprob[ri];
-          a.cidx[o] = (int64_t)rr.row - lo;
-          a.ctype[o] = (uint8_t)(rr.type + 1);
+          const int ft = s_ft[q][s];
+          pv = s_val[q][s];
+          cv = (int64_t)(ft >> 3);
+          tv = (uint8_t)(ft & 7);
         } else {
-          a.prob[o] = (T)0;
-          a.cidx[o] = -1;
-          a.ctype[o] = 0;
+          pv = (T)0;
+          cv = -1;
+          tv = 0;
+        }
+      };
+      if (ablate(a.fs.dbg, 1 << 16)) continue;  // diagnostics: no list stores
+      // pixel (r, i) of the half tile -> its table row (tile_geom's q minus q0)
+      auto hq = [](int r, int i) { return ((i >> 3) * kWave) + (r & 7) * 8 + (i & 7); };
+      if ((K & 1) == 0) {  // slot pairs: every pair starts at an even element
+        const int S2 = S >> 1, per_row = nx * S2;
+        for (int e = tid; e < ny * per_row; e += kBlock) {
+          const int r = e / per_row, rem = e - r * per_row;
+          const int i = rem / S2, s = 2 * (rem - i * S2);
+          const int q = hq(r, i);
+          const int64_t o = (((int64_t)b * H + Y0 + r) * W + X0 + i) * K + s0 + s;
+          T p0, p1;
+          int64_t c0, c1;
+          uint8_t t0, t1;
+          value(q, s, p0, c0, t0);
+          value(q, s + 1, p1, c1, t1);
+          if constexpr (sizeof(T) == 4) {
+            *(float2 *)(a.prob + o) = make_float2(p0, p1);
+          } else {
+            *(double2 *)(a.prob + o) = make_double2(p0, p1);
+          }
+          if (ablate(a.fs.dbg, 1 << 23)) continue;  // diagnostics: probabilities only
+          *(longlong2 *)(a.cidx + o) = make_longlong2(c0, c1);
+          *(uint16_t *)(a.ctype + o) = (uint16_t)(t0 | (t1 << 8));
+        }
+      } else {
+        const int per_row = nx * S;
+        for (int e = tid; e < ny * per_row; e += kBlock) {
+          const int r = e / per_row, rem = e - r * per_row;
+          const int i = rem / S, s = rem - i * S;
+          const int64_t o = (((int64_t)b * H + Y0 + r) * W + X0 + i) * K + s0 + s;
+          value(hq(r, i), s, a.prob[o], a.cidx[o], a.ctype[o]);
         }
       }
     }
@@ -1345,9 +1399,17 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   }
   if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
-    if (a.prob)  // soft mask + the close lists, row-coalesced
-      hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), 0, stream, a, pb);
-    else
+    if (a.prob) {  // soft mask + the close lists, row-coalesced (dynamic LDS past 64 KB)
+      KD_CHECK_ARG(fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
+      const size_t dyn = ((sizeof(T) + sizeof(int)) * (kReduceSlots + 1) + sizeof(int)) * kBlock / 2;
+      const hipError_t ea = hipFuncSetAttribute((const void *)kd_soft_lists<T>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                (int)dyn);
+      if (ea != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft lists: %s", hipGetErrorString(ea));
+      if (ablate(debug_flags(), (1 << 16) | (1 << 23)))  // diagnostics: the skipped index stores
+        hipMemsetAsync(a.cidx, 0xFF, sizeof(int64_t) * fs.B * fs.H * fs.W * a.K, stream);  // -1
+      hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), dyn, stream, a, pb);
+    } else
       hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(8192), dim3(kBlock), 0, stream, a, pb);
   } else if (a.prob) {
     return set_error(KD_ERR_INVALID_ARGUMENT, "close lists need the soft mask");

@@ -242,3 +242,71 @@ def test_reference_op_form_raw_vs_oracle(dt, knum, boxes):
         _C.render.mesh.deftet_sparse_render_forward_cuda(
             T(fvz), T(fvi).transpose(-1, -2).contiguous().transpose(-1, -2), T(bbox), T(px),
             T(rr), knum, 1e-8)
+
+
+# --------------------------------------------------------------------------------------------
+# the pooled forward (knum <= 32) against the per-pixel wave kernel (debug flag 2048)
+# --------------------------------------------------------------------------------------------
+def _both_kernels(px, rr, fvz, fvi, feat, knum, raw_boxes=None):
+    from kaolin_amd import _C, _lib
+    from kaolin_amd.render.mesh import deftet_sparse_render
+    out = []
+    for flags in (0, 2048):
+        _lib.load().kd_debug_set(flags)
+        try:
+            if raw_boxes is None:
+                interp, fidx = deftet_sparse_render(T(px), T(rr), T(fvz), T(fvi), T(feat), knum)
+                out.append((N(interp), N(fidx)))
+            else:
+                r = _C.render.mesh.deftet_sparse_render_forward_cuda(
+                    T(fvz), T(fvi), T(raw_boxes), T(px), T(rr), knum, 1e-8)
+                out.append(tuple(N(t) for t in r))
+        finally:
+            _lib.load().kd_debug_set(0)
+    for a, b in zip(*out):
+        np.testing.assert_array_equal(a, b)
+    return out[0]
+
+
+@pytest.mark.parametrize('dt', [np.float32, np.float64])
+@pytest.mark.parametrize('knum', [1, 8, 30, 32])
+def test_pooled_matches_wave_kernel_sphere_grid(dt, knum):
+    """A pixel grid over a rendered sphere (the bench row's shape: neighbouring pixels share
+    cells), a ragged last workgroup (P not a multiple of 64), pixels off the grid's [-1, 1]
+    range and NaN pixels."""
+    from kaolin_amd import workloads
+    v = workloads.sphere_views(60, 31, 96, 96, 1, DEV, dtype=torch.float32 if dt == np.float32
+                               else torch.float64, seed=0, elevation=0.4)
+    fvz = N(v['fvz'])
+    fvi = N(v['fvi'])
+    feat = N(v['feats'])
+    H = W = 91
+    xs = (2 * np.arange(W) + 1 - W) / W * 1.1
+    ys = (H - 2 * np.arange(H) - 1.) / H * 1.1
+    px = np.stack(np.broadcast_arrays(xs[None, :], ys[:, None]), -1).reshape(1, -1, 2).astype(dt)
+    px[0, 5] = np.nan
+    px[0, 77, 1] = np.nan
+    rr = np.broadcast_to(np.array([-1e9, 0.], dt), (1, H * W, 2)).copy()
+    interp, fidx = _both_kernels(px, rr, fvz, fvi, feat, knum)
+    assert (fidx >= 0).any()
+    oi, of, _ = f3.deftet_forward(px, rr, fvz, fvi, feat, knum)
+    np.testing.assert_array_equal(fidx, of)
+    np.testing.assert_array_equal(interp, oi)
+
+
+@pytest.mark.parametrize('dt', [np.float32, np.float64])
+@pytest.mark.parametrize('size', [0.15, 0.6, 2.0])
+def test_pooled_overflow_falls_back(dt, size):
+    """Soups from a few candidates per pixel (all pooled) to hundreds (the 1024-candidate pool
+    overflows, those pixels take the per-pixel path inside the same launch), sorted and raw."""
+    px, rr, fvz, fvi, feat = soup(2, 2000, 333, dt, 11, size=size, nan_faces=3)
+    knum = 24
+    interp, fidx = _both_kernels(px, rr, fvz, fvi, feat, knum)
+    oi, of, _ = f3.deftet_forward(px, rr, fvz, fvi, feat, knum)
+    np.testing.assert_array_equal(fidx, of)
+    np.testing.assert_array_equal(interp, oi)
+    bbox = np.concatenate([fvi.min(2), fvi.max(2)], -1)
+    raw = _both_kernels(px, rr, fvz, fvi, feat, knum, raw_boxes=bbox)
+    ofi, od, oa0, oa1 = f3.deftet_forward_raw(px, rr, fvz, fvi, bbox, knum)
+    for a, b in zip(raw, (ofi, od, oa0, oa1)):
+        np.testing.assert_array_equal(a, b)
