@@ -178,6 +178,7 @@ struct DtArgs {
   const T *bbox;      // (B, F, 4) or nullptr
   T *depth, *w0, *w1; // (B, P, K) each, or nullptr (sorted mode)
   int dbg;            // diagnostic ablation flags (kd_common.hpp)
+  long long *tbuf;    // diagnostics (flag 64): candidate / hit / fallback / flush counters
 };
 
 constexpr int kDtWaves = 4;  // pixels per workgroup
@@ -348,14 +349,17 @@ __global__ __launch_bounds__(kWave *kDtWaves) void kd_dt_fwd(DtArgs<T> a) {
 //             the wave's hit pool
 //   rank      face rank within the pixel (the reference keeps the first knum hits by face index),
 //             then depth rank (descending, ties by face index) -> slot table
-//   store     the 16 pixels' outputs are one contiguous run per array: written in memory order
+//   store     the group's outputs are one contiguous run per array: written in memory order
+// Walk, test, rank and store run per group of four pixels, so the hit pool holds four pixels'
+// hits (~5.5 per pixel at the bench row, more at poles) and the ranking loops stay short.
 // A pixel with a hit beyond the pool is redone by the per-pixel wave path (dt_pixel_wave, with its
 // bisection for any number of hits), in LDS the pool no longer uses.  Candidate order is
 // irrelevant: selection and output order depend on face index and depth only.
-constexpr int kDtPx = 16;      // pixels per wave (= workgroup)
+constexpr int kDtPx = 4;       // pixels per wave (= workgroup)
 constexpr int kDtRing = 512;   // candidate ring (< 64 + 4 x 64 entries live)
 constexpr int kDtHits = 256;   // hit pool per wave
 constexpr int kDtMaxK = 32;    // knum bound of the pooled path (slot table)
+constexpr int kDtMaxD = 4;     // feature bound of the pooled path (interpolated-feature table)
 
 template <typename T>
 struct DtPoolLDS {
@@ -374,7 +378,8 @@ struct DtPoolLDS {
   T x[kDtPx], y[kDtPx], dmin[kDtPx], dmax[kDtPx];
   int64_t lofs[kDtPx];
   int nl[kDtPx], nh[kDtPx];
-  short slot[kDtPx][kDtMaxK];
+  short slot[4][kDtMaxK];  // the current group of four pixels
+  T ival[4][kDtMaxK][kDtMaxD];  // its interpolated features
   unsigned ovf;  // pixels whose hits did not all fit the pool
 };
 
@@ -396,6 +401,21 @@ __device__ __forceinline__ void dt_load_box(const T *boxes, int64_t i, T bx[4]) 
   }
 }
 
+// e / d for the store loops' small operands (e < 2^12, d < 2^10): (e + 0.5) / d is at least
+// 0.5 / d from an integer, far beyond the float product's error
+__device__ __forceinline__ int small_div(int e, float inv_d) {
+  return (int)(((float)e + 0.5f) * inv_d);
+}
+
+// lane j's value to every lane (j wave-uniform)
+__device__ __forceinline__ float lane_bcast(float x, int j) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), j));
+}
+__device__ __forceinline__ double lane_bcast(double x, int j) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), j),
+                          __builtin_amdgcn_readlane(__double2loint(x), j));
+}
+
 __device__ __forceinline__ int lane_rank(uint64_t m) {  // set lanes of m below this lane
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -406,6 +426,14 @@ __global__ __launch_bounds__(kWave) void kd_dt_fwd_pool(DtArgs<T> a) {
   __shared__ DtPoolLDS<T> s;
   typename DtPoolLDS<T>::Work &wk = s.u.w;
   const int lane = threadIdx.x;
+  // diagnostics (flag 64): duration, start, and the ends of the walk / rank / store phases
+  TileClock clk(a.tbuf, 0);
+  clk.start_to(1);
+  auto stamp = [&](int slot) {
+    if (KD_DIAG && a.tbuf && lane == 0)
+      a.tbuf[(int64_t)slot * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x +
+             blockIdx.x] = wall_clock64();
+  };
   const int b = blockIdx.y, K = a.K, G = a.G;
   const int64_t p0 = (int64_t)blockIdx.x * kDtPx;
   const int npx = (int)min((int64_t)kDtPx, a.P - p0);
@@ -447,6 +475,7 @@ __global__ __launch_bounds__(kWave) void kd_dt_fwd_pool(DtArgs<T> a) {
       hit = dt_face_test<T>(fvi + (int64_t)f * 6, fvz + (int64_t)f * 3,
                             bbox ? bbox + (int64_t)f * 4 : nullptr, s.x[q], s.y[q], s.dmin[q],
                             s.dmax[q], eps, w0, w1, depth);
+      if (ablate(a.dbg, 4) && hit) hit = depth == (T)12345;  // diagnostics: tests, no hits
     }
     const uint64_t hm = __ballot(hit);
     if (hit) {
@@ -457,9 +486,16 @@ __global__ __launch_bounds__(kWave) void kd_dt_fwd_pool(DtArgs<T> a) {
         wk.hw0[at] = w0;
         wk.hw1[at] = w1;
         wk.hpix[at] = (uint8_t)q;
-        atomicAdd(&s.nh[q], 1);
-      } else {
-        atomicOr(&s.ovf, 1u << q);
+      }
+    }
+    // per-pixel hit counts and pool overflow by ballots (LDS atomics are priced per lane)
+    const uint64_t hov = __ballot(hit && nhit + lane_rank(hm) >= kDtHits);
+#pragma unroll
+    for (int u = 0; u < kDtPx; ++u) {
+      const uint64_t mu = __ballot(hit && q == u);
+      if (lane == 0 && mu) {
+        s.nh[u] += __popcll(mu & ~hov);
+        if (mu & hov) s.ovf |= 1u << u;
       }
     }
     nhit += __popcll(hm);
@@ -467,13 +503,17 @@ __global__ __launch_bounds__(kWave) void kd_dt_fwd_pool(DtArgs<T> a) {
     wave_lds_sync();
   };
   constexpr int U = 4;
+  const int D = a.D;
+  const T *feat = a.feat ? a.feat + (int64_t)b * a.F * 3 * D : nullptr;
   for (int g = 0; g < kDtPx / U; ++g) {
+    const int qg = g * U;
+    if (qg >= npx) break;  // wave-uniform
     int n[U], steps = 0;
     int64_t lofs[U];
     T x[U], y[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int q = g * U + u;
+      const int q = qg + u;
       n[u] = s.nl[q];
       lofs[u] = s.lofs[q];
       x[u] = s.x[q];
@@ -499,94 +539,141 @@ __global__ __launch_bounds__(kWave) void kd_dt_fwd_pool(DtArgs<T> a) {
         if (in) {
           const int at = (tail + lane_rank(m)) & (kDtRing - 1);
           wk.cface[at] = f[u];
-          wk.cpix[at] = (uint8_t)(g * U + u);
+          wk.cpix[at] = (uint8_t)(qg + u);
         }
         tail += __popcll(m);
       }
       wave_lds_sync();
       while (tail - head >= kWave) flush(kWave);
     }
-  }
-  if (tail > head) flush(tail - head);
-  // ranks within each pixel
-  const int nk = min(nhit, kDtHits);
-  const unsigned ovf = s.ovf;
-  for (int i = lane; i < nk; i += kWave) {
-    const int q = wk.hpix[i], fi = wk.hface[i];
-    int r = 0;
-    if (s.nh[q] > K || a.depth)  // the face rank: needed for a cut and for the op form's slots
-      for (int j = 0; j < nk; ++j) r += (wk.hpix[j] == q && wk.hface[j] < fi) ? 1 : 0;
-    wk.hrank[i] = (short)r;
-  }
-  wave_lds_sync();
-  for (int i = lane; i < nk; i += kWave) {
-    const int q = wk.hpix[i];
-    if (wk.hrank[i] >= K || ((ovf >> q) & 1)) continue;
-    int r;
-    if (a.depth) {  // op form: slot = face rank (deftet_cuda.cu:166-180), unsorted
-      r = wk.hrank[i];
-    } else {        // depth descending, then face index (deftet.py:300-303, stable order)
-      const T di = wk.hdep[i];
-      const int fi = wk.hface[i];
-      r = 0;
-      for (int j = 0; j < nk; ++j) {
-        const T dj = wk.hdep[j];
-        r += (wk.hpix[j] == q && wk.hrank[j] < K && (dj > di || (dj == di && wk.hface[j] < fi)))
-                 ? 1
-                 : 0;
-      }
+    if (tail > head) flush(tail - head);
+    stamp(2);
+    // ranks within each pixel of the group: lane = hit i, the other hits j broadcast from
+    // registers a block of 64 at a time (readlane, no LDS round trip per j)
+    const int nk = min(nhit, kDtHits);
+    const unsigned ovf = s.ovf;
+    bool need_frank = a.depth != nullptr;  // the face rank: for a cut and the op form's slots
+    for (int u = 0; u < U; ++u) need_frank |= s.nh[qg + u] > K;
+    for (int i0 = 0; i0 < nk; i0 += kWave) {
+      const int i = i0 + lane;
+      const int qi = i < nk ? wk.hpix[i] : 255, fi = i < nk ? wk.hface[i] : 0;
+      int r = 0;
+      if (need_frank)
+        for (int j0 = 0; j0 < nk; j0 += kWave) {
+          const int jl = j0 + lane;
+          const int qj = jl < nk ? wk.hpix[jl] : 254, fj = jl < nk ? wk.hface[jl] : 0;
+          const int m = min(kWave, nk - j0);
+          for (int jj = 0; jj < m; ++jj)
+            r += (__builtin_amdgcn_readlane(qj, jj) == qi &&
+                  __builtin_amdgcn_readlane(fj, jj) < fi)
+                     ? 1
+                     : 0;
+        }
+      if (i < nk) wk.hrank[i] = (short)r;
     }
-    s.slot[q][r] = (short)i;
-  }
-  wave_lds_sync();
-  // stores: element e = (pixel, slot) of the wave's contiguous run, lanes on consecutive elements
-  {
-    const int ne = npx * K, stq = kWave / K, sts = kWave % K;
-    int q = lane / K, sl = lane - (lane / K) * K;
-    const int64_t row0 = ((int64_t)b * a.P + p0) * K;
-    const int D = a.D;
-    const T *feat = a.feat ? a.feat + (int64_t)b * a.F * 3 * D : nullptr;
-    for (int e = lane; e < ne; e += kWave) {
-      if (!((ovf >> q) & 1)) {
-        const int kept = min(s.nh[q], K);
-        const int h = sl < kept ? s.slot[q][sl] : -1;
-        const int64_t o = row0 + e;
-        if (a.depth) {  // op form: empty slots -1 / -inf / 0 / 0 (deftet.cpp:88-94)
-          a.face_idx[o] = h >= 0 ? (int64_t)wk.hface[h] : -1;
-          a.depth[o] = h >= 0 ? wk.hdep[h] : (T)-INFINITY;
-          a.w0[o] = h >= 0 ? wk.hw0[h] : (T)0;
-          a.w1[o] = h >= 0 ? wk.hw1[h] : (T)0;
-        } else if (h >= 0) {
-          const int fi = wk.hface[h];
-          const T w0 = wk.hw0[h], w1 = wk.hw1[h];
-          const T w2 = (T)1 - (w0 + w1);  // deftet.py:304
-          a.face_idx[o] = fi;
-          a.weights[3 * o] = w0;
-          a.weights[3 * o + 1] = w1;
-          a.weights[3 * o + 2] = w2;
-          const T *cf = feat + (int64_t)fi * 3 * D;
-          for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
-            a.interp[o * D + d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
-        } else {
-          a.face_idx[o] = -1;
-          a.weights[3 * o] = (T)0;
-          a.weights[3 * o + 1] = (T)0;
-          a.weights[3 * o + 2] = (T)0;
-          for (int d = 0; d < D; ++d) a.interp[o * D + d] = (T)0;
+    wave_lds_sync();
+    for (int i0 = 0; i0 < nk; i0 += kWave) {
+      const int i = i0 + lane;
+      const bool vi = i < nk;
+      const int qi = vi ? wk.hpix[i] : 255, fi = vi ? wk.hface[i] : 0;
+      const int ri = vi ? wk.hrank[i] : K;
+      const T di = vi ? wk.hdep[i] : (T)0;
+      int r = ri;  // op form: slot = face rank (deftet_cuda.cu:166-180), unsorted
+      if (!a.depth) {  // depth descending, then face index (deftet.py:300-303, stable order)
+        r = 0;
+        for (int j0 = 0; j0 < nk; j0 += kWave) {
+          const int jl = j0 + lane;
+          const bool vj = jl < nk;
+          // pixel, or 254 when not kept (face rank >= K)
+          const int qj = vj && wk.hrank[jl] < K ? wk.hpix[jl] : 254;
+          const int fj = vj ? wk.hface[jl] : 0;
+          const T dj = vj ? wk.hdep[jl] : (T)0;
+          const int m = min(kWave, nk - j0);
+          for (int jj = 0; jj < m; ++jj) {
+            const T db = lane_bcast(dj, jj);
+            r += (__builtin_amdgcn_readlane(qj, jj) == qi &&
+                  (db > di || (db == di && __builtin_amdgcn_readlane(fj, jj) < fi)))
+                     ? 1
+                     : 0;
+          }
         }
       }
-      q += stq;
-      sl += sts;
-      if (sl >= K) {
-        sl -= K;
-        ++q;
+      if (vi && ri < K && !((ovf >> qi) & 1) && !ablate(a.dbg, 512))
+        s.slot[qi - qg][r] = (short)i;
+    }
+    wave_lds_sync();
+    stamp(3);
+    // stores: the group's rows are one contiguous run per array.  First the interpolated
+    // features into LDS (their gathers are the only global loads; a load issued after a store
+    // would wait for that store too: vmcnt counts both), then every output in memory order,
+    // consecutive lanes on consecutive elements.
+    const int ng = min(U, npx - qg);
+    const int64_t row0 = ((int64_t)b * a.P + p0 + qg) * K;
+    auto slot_hit = [&](int qq, int sl) {  // -2: redone by the fallback, -1: empty slot
+      const int q = qg + qq;
+      if (((ovf >> q) & 1) && !ablate(a.dbg, 1 << 15)) return -2;
+      const int kept = ablate(a.dbg, 512) || ((ovf >> q) & 1) ? 0 : min(s.nh[q], K);
+      return sl < kept ? (int)s.slot[qq][sl] : -1;
+    };
+    const float invK = 1.f / (float)K;
+    if (a.depth) {  // op form: empty slots -1 / -inf / 0 / 0 (deftet.cpp:88-94)
+      for (int e = lane; e < ng * K; e += kWave) {
+        const int qq = small_div(e, invK), h = slot_hit(qq, e - qq * K);
+        if (h == -2) continue;
+        const int64_t o = row0 + e;
+        a.face_idx[o] = h >= 0 ? (int64_t)wk.hface[h] : -1;
+        a.depth[o] = h >= 0 ? wk.hdep[h] : (T)-INFINITY;
+        a.w0[o] = h >= 0 ? wk.hw0[h] : (T)0;
+        a.w1[o] = h >= 0 ? wk.hw1[h] : (T)0;
+      }
+    } else {
+      const int KD = K * D;
+      const float invKD = 1.f / (float)KD, invD = 1.f / (float)max(D, 1), invK3 = 1.f / (3.f * K);
+      for (int e = lane; e < ng * KD; e += kWave) {
+        const int qq = small_div(e, invKD), rem = e - qq * KD, sl = small_div(rem, invD),
+                  d = rem - sl * D;
+        const int h = slot_hit(qq, sl);
+        if (h < 0) continue;
+        const T w0 = wk.hw0[h], w1 = wk.hw1[h];
+        const T w2 = (T)1 - (w0 + w1);  // deftet.py:304
+        const T *cf = feat + (int64_t)wk.hface[h] * 3 * D;
+        // :312-313, the sum over the 3 corners in order
+        s.ival[qq][sl][d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+      }
+      wave_lds_sync();
+      for (int e = lane; e < ng * K; e += kWave) {
+        const int qq = small_div(e, invK), h = slot_hit(qq, e - qq * K);
+        if (h != -2) a.face_idx[row0 + e] = h >= 0 ? (int64_t)wk.hface[h] : -1;
+      }
+      for (int e = lane; e < ng * K * 3; e += kWave) {
+        const int qq = small_div(e, invK3), rem = e - qq * 3 * K, sl = small_div(rem, 1.f / 3.f),
+                  c = rem - sl * 3;
+        const int h = slot_hit(qq, sl);
+        if (h == -2) continue;
+        T v = (T)0;
+        if (h >= 0) {
+          const T w0 = wk.hw0[h], w1 = wk.hw1[h];
+          v = c == 0 ? w0 : c == 1 ? w1 : (T)1 - (w0 + w1);
+        }
+        a.weights[3 * row0 + e] = v;
+      }
+      for (int e = lane; e < ng * KD; e += kWave) {
+        const int qq = small_div(e, invKD), rem = e - qq * KD, sl = small_div(rem, invD),
+                  d = rem - sl * D;
+        const int h = slot_hit(qq, sl);
+        if (h != -2) a.interp[row0 * D + e] = h >= 0 ? s.ival[qq][sl][d] : (T)0;
       }
     }
+    stamp(4);
+    if (ovf && !ablate(a.dbg, 1 << 15)) {  // wave-uniform (diagnostics: no fallback)
+      wave_lds_sync();  // the pool's LDS becomes the fallback's
+      for (int u = 0; u < ng; ++u)
+        if ((ovf >> (qg + u)) & 1) dt_pixel_wave<T>(a, b, p0 + qg + u, s.u.fb);
+      if (lane == 0) s.ovf = 0;
+    }
+    head = tail = nhit = 0;
+    wave_lds_sync();
   }
-  if (!ovf) return;
-  wave_lds_sync();  // the pool's LDS becomes the fallback's
-  for (int q = 0; q < npx; ++q)
-    if ((ovf >> q) & 1) dt_pixel_wave<T>(a, b, p0 + q, s.u.fb);
 }
 
 static size_t dt_workspace(int B, int64_t F, size_t esize) {
@@ -632,9 +719,10 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
   DtArgs<T> a{B,   P,      F,     N,      K,       D,        C,       G,
               eps, px,     range, fvz,    fvi,     feat,     cursor,  lists,
               bbox ? bbox : boxes, interp, face_idx, weights, bbox, depth, w0, w1,
-              debug_flags()};
-  // the pooled kernel for knum <= 32 (diagnostic flag 2048: the per-pixel wave kernel)
-  const bool pooled = K <= kDtMaxK && !(debug_flags() & 2048);
+              debug_flags(), debug_tile_buffer()};
+  // the pooled kernel (knum <= 32, <= 4 features) only under debug flag 2048: measured slower
+  // than the per-pixel wave kernel
+  const bool pooled = K <= kDtMaxK && D <= kDtMaxD && (debug_flags() & 2048);
   const int64_t gx = pooled ? (P + kDtPx - 1) / kDtPx : (P + kDtWaves - 1) / kDtWaves;
   KD_CHECK_ARG(gx < (1ll << 31), "deftet: too many pixels");
   {

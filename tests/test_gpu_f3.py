@@ -245,7 +245,7 @@ def test_reference_op_form_raw_vs_oracle(dt, knum, boxes):
 
 
 # --------------------------------------------------------------------------------------------
-# the pooled forward (knum <= 32) against the per-pixel wave kernel (debug flag 2048)
+# the pooled forward (knum <= 32, debug flag 2048) against the per-pixel wave kernel
 # --------------------------------------------------------------------------------------------
 def _both_kernels(px, rr, fvz, fvi, feat, knum, raw_boxes=None):
     from kaolin_amd import _C, _lib
