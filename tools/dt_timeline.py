@@ -40,7 +40,7 @@ def main():
     for _ in range(3):
         deftet_sparse_render(px, rr, fvz, fvi, uvs, 30)
     lib.kd_debug_buffer(buf.data_ptr())
-    lib.kd_debug_set(64)
+    lib.kd_debug_set(64 | 2048)  # the pooled kernel is opt-in
     deftet_sparse_render(px, rr, fvz, fvi, uvs, 30)
     torch.cuda.synchronize()
     lib.kd_debug_set(0)

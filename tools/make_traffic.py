@@ -8,28 +8,21 @@ same sum from the raw KiB stored here."""
 import json
 import sys
 
-# device kernel (rocprof name) -> profiling slot name used by bench.py (kd_capi.cpp KernelId)
+# device kernel (rocprof name, template arguments stripped) -> profiling slot name used by
+# bench.py (kd_capi.cpp KernelId)
 SLOT = {
-    'kd::kd_raster_fwd_pairs': 'kd_raster_fwd', 'kd::kd_raster_fwd<float>': 'kd_raster_fwd',
-    'kd::kd_soft_fwd<float, false>': 'kd_soft_fwd', 'kd::kd_soft_fwd<float, true>': 'kd_soft_fwd',
-    'kd::kd_soft_pairs<float>': 'kd_soft_pairs',
-    'kd::kd_soft_pairs<float, true, 6>': 'kd_soft_pairs',
-    'kd::kd_soft_pairs<float, false, 8>': 'kd_soft_pairs',
-    'kd::kd_soft_bwd_items<float, 1>': 'kd_soft_bwd_pairs',
-    'kd::kd_raster_bwd_tile<float, 3>': 'kd_raster_bwd_tile',
-    'kd::kd_soft_pair_math<float, true, false>': 'kd_soft_pair_math',
-    'kd::kd_soft_reduce<float>': 'kd_soft_reduce',
-    'kd::kd_soft_bwd_pairs<float>': 'kd_soft_bwd_pairs',
-    'kd::kd_prepare_fwd<float>': 'kd_prepare_fwd', 'kd::kd_prepare_bwd<float>': 'kd_prepare_bwd',
-    'kd::kd_zero2<float>': 'kd_zero',
-    'kd::kd_raster_bwd_tile<float, 4>': 'kd_raster_bwd_tile',
-    'kd::kd_bin_count<float>': 'kd_bin_count', 'kd::kd_bin_scan': 'kd_bin_scan',
-    'kd::kd_bin_scan<float>': 'kd_bin_scan',
-    'kd::kd_soft_ovf_fwd<float, true>': 'kd_soft_ovf_fwd', 'kd::kd_soft_ovf_bwd<float>': 'kd_soft_ovf_bwd',
-    'kd::kd_bin_scatter<float>': 'kd_bin_scatter',
-    'kd::kd_dibr_bwd<float>': 'kd_dibr_bwd', 'kd::kd_dibr_bwd<float, false>': 'kd_dibr_bwd',
-    'kd::kd_dibr_fwd_tiles': 'kd_dibr_fwd',
-    'kd::kd_dibr_fwd_tiles<false>': 'kd_dibr_fwd',
+    'kd::kd_raster_fwd_pairs': 'kd_raster_fwd', 'kd::kd_raster_fwd': 'kd_raster_fwd',
+    'kd::kd_soft_fwd': 'kd_soft_fwd', 'kd::kd_soft_pairs': 'kd_soft_pairs',
+    'kd::kd_soft_bwd_items': 'kd_soft_bwd_pairs', 'kd::kd_soft_bwd_pairs': 'kd_soft_bwd_pairs',
+    'kd::kd_soft_bwd_lists': 'kd_soft_bwd_pairs',
+    'kd::kd_raster_bwd_tile': 'kd_raster_bwd_tile', 'kd::kd_soft_pair_math': 'kd_soft_pair_math',
+    'kd::kd_soft_reduce': 'kd_soft_reduce', 'kd::kd_soft_lists': 'kd_soft_reduce',
+    'kd::kd_prepare_fwd': 'kd_prepare_fwd', 'kd::kd_prepare_bwd': 'kd_prepare_bwd',
+    'kd::kd_zero2': 'kd_zero', 'kd::kd_bin_count': 'kd_bin_count', 'kd::kd_bin_scan': 'kd_bin_scan',
+    'kd::kd_bin_scatter': 'kd_bin_scatter', 'kd::kd_soft_ovf_fwd': 'kd_soft_ovf_fwd',
+    'kd::kd_soft_ovf_bwd': 'kd_soft_ovf_bwd', 'kd::kd_dibr_bwd': 'kd_dibr_bwd',
+    'kd::kd_dibr_fwd_tiles': 'kd_dibr_fwd', 'kd::kd_dibr_fwd_tiles_f64': 'kd_dibr_fwd',
+    'kd::kd_dibr_fwd_st': 'kd_dibr_fwd',
 }
 
 
@@ -37,7 +30,7 @@ def main(summary, out, config, dtype='f32', views=8, lists=False):
     src = json.load(open(summary))
     kern = {}
     for name, m in src.items():
-        slot = SLOT.get(name)
+        slot = SLOT.get(name.split('<')[0].split('(')[0].replace('void ', ''))
         if slot is None or 'hbm_bytes_raw' not in m:
             continue
         kern[slot] = {'device_kernel': name,
