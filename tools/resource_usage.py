@@ -25,11 +25,13 @@ for f in sorted(x[:-4] for x in os.listdir(CSRC) if x.endswith('.hip')):
             continue
         for key, pat in (('vgpr', r'VGPRs: (\d+)'), ('scratch', r'ScratchSize \[bytes/lane\]: (\d+)'),
                          ('lds', r'LDS Size \[bytes/block\]: (\d+)'),
-                         ('occ', r'Occupancy \[waves/SIMD\]: (\d+)')):
+                         ('occ', r'Occupancy \[waves/SIMD\]: (\d+)'),
+                         ('sspill', r'SGPRs Spill: (\d+)'), ('vspill', r'VGPRs Spill: (\d+)')):
             m = re.search(pat, line)
             if m and cur is not None:
                 cur[key] = m.group(1)
         if cur and 'lds' in cur:  # the last field of a kernel's remark block
             print(f"{cur['name'][:64]:64s} vgpr={cur.get('vgpr')} scratch={cur.get('scratch')} "
-                  f"lds={cur.get('lds')} occ={cur.get('occ')}")
+                  f"lds={cur.get('lds')} occ={cur.get('occ')} "
+                  f"spill(s/v)={cur.get('sspill')}/{cur.get('vspill')}")
             cur = None
