@@ -476,6 +476,11 @@ int kd_rast_interpolate_f64(int batch, int height, int width, int64_t num_faces,
  * (B, F, 3, D) (NULL: skipped).
  * ------------------------------------------------------------------------------------------- */
 size_t kd_deftet_workspace_size(int batch, int64_t num_faces, int double_precision);
+/* The same plus the pixel sort of the cell-major forward (knum <= 32): a forward given at least
+ * this many bytes runs the cell-major kernels; with kd_deftet_workspace_size's bytes it runs the
+ * per-pixel kernel (same results). */
+size_t kd_deftet_workspace_size_p(int batch, int64_t num_pixels, int64_t num_faces,
+                                  int double_precision);
 int kd_deftet_sparse_render_forward_f32(int batch, int64_t num_pixels, int64_t num_faces,
                                         int knum, int feat_dim, const float *pixel_coords,
                                         const float *render_ranges, const float *fvz,

@@ -109,6 +109,8 @@ def load():
             lib.kd_mask_iou_workspace_size.restype = c_size
             lib.kd_deftet_workspace_size.argtypes = [c_int, c_i64, c_int]
             lib.kd_deftet_workspace_size.restype = c_size
+            lib.kd_deftet_workspace_size_p.argtypes = [c_int, c_i64, c_i64, c_int]
+            lib.kd_deftet_workspace_size_p.restype = c_size
             lib.kd_texture_mapping_backward_workspace_size.argtypes = [c_int, c_i64, c_int, c_int,
                                                                        c_int]
             lib.kd_texture_mapping_backward_workspace_size.restype = c_size

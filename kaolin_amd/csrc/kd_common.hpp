@@ -35,7 +35,8 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       1 << 18 / 1 << 19 skip kd_bin_count's cull coefficients / its LDS tile counts,
 //       1 << 16 / 1 << 23 kd_soft_lists: skip every list store / the index and type stores (the
 //       host presets the indices to -1 so that the backward reads no garbage),
-//       2048 (production too) DefTet forward: the pooled kernel instead of the per-pixel waves,
+//       1024 / 2048 (production too) DefTet forward: the cell-major / the pooled kernel instead
+//       of the per-pixel waves,
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
 int debug_flags();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr

@@ -121,6 +121,11 @@ __global__ __launch_bounds__(kBlock) void kd_dt_bin(int64_t F, int64_t N, int G,
     }
 }
 
+template <typename T>
+__device__ __forceinline__ bool dt_face_weights(T ax, T ay, T bx, T by, T cx, T cy, T z0, T z1,
+                                                T z2, T x0, T y0, T dmin, T dmax, T eps, T &w0,
+                                                T &w1, T &depth);
+
 // The reference's per-face test (deftet_cuda.cu:114-160): half-open box of the corner min / max,
 // eps-normalised barycentrics (copysignf of the float eps, also for fp64 data), all >= 0, depth
 // in [min, max).
@@ -141,6 +146,15 @@ __device__ __forceinline__ bool dt_face_test(const T *v, const T *z, const T *bb
     ymax = nmax3(ay, by, cy);
   }
   if (!(x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax)) return false;
+  return dt_face_weights<T>(ax, ay, bx, by, cx, cy, z[0], z[1], z[2], x0, y0, dmin, dmax, eps, w0,
+                            w1, depth);
+}
+
+// The test past the box (deftet_cuda.cu:128-160), on corner values.
+template <typename T>
+__device__ __forceinline__ bool dt_face_weights(T ax, T ay, T bx, T by, T cx, T cy, T z0, T z1,
+                                                T z2, T x0, T y0, T dmin, T dmax, T eps, T &w0,
+                                                T &w1, T &depth) {
   const T aex = ax - x0, aey = ay - y0, bex = bx - x0, bey = by - y0;
   const T cex = cx - x0, cey = cy - y0;
   const T _w0 = bex * cey - bey * cex;
@@ -152,8 +166,8 @@ __device__ __forceinline__ bool dt_face_test(const T *v, const T *z, const T *bb
   w1 = _w1 / (norm + ne);
   const T w2 = _w2 / (norm + ne);
   if (!(w0 >= (T)0 && w1 >= (T)0 && w2 >= (T)0)) return false;
-  depth = w0 * z[0] + w1 * z[1] + w2 * z[2];  // :156
-  return depth < dmax && depth >= dmin;       // :158
+  depth = w0 * z0 + w1 * z1 + w2 * z2;   // :156
+  return depth < dmax && depth >= dmin;  // :158
 }
 
 template <typename T>
@@ -676,12 +690,289 @@ __global__ __launch_bounds__(kWave) void kd_dt_fwd_pool(DtArgs<T> a) {
   }
 }
 
-static size_t dt_workspace(int B, int64_t F, size_t esize) {
+// ---------------------------------------------------------------------------------------------
+// Cell-major forward (knum <= kDtCellK, debug flag 1024, a workspace with room for the pixel
+// sort: kd_deftet_workspace_size_p).  Every pixel of one grid cell walks the same face list, so:
+//   kd_dt_pix_count    cell of every pixel, counted per (view, cell) with one atomic per distinct
+//                      cell of a wave (ballot groups: neighbouring pixels share cells); the
+//                      pixel's position in its cell
+//   kd_dt_pix_scan     per view: exclusive scans of the cell counts (pixel offsets) and of their
+//                      64-pixel chunks (work items)
+//   kd_dt_pix_scatter  pixels in cell order
+//   kd_dt_fwd_cell     one wave per work item: lane = pixel (up to 64 of one cell).  The cell's
+//                      list is read 64 faces at a time -- lane j loads face j's box, corners and
+//                      depths -- and broadcast face by face (readlane): every pixel lane runs the
+//                      reference's box test, and the exact test where it is inside.  A round trip
+//                      serves 64 pixels instead of one.  Each lane keeps the knum hits with the
+//                      smallest face indices in LDS (the reference keeps the first knum by index:
+//                      a further hit replaces the largest kept index when it is smaller), ranks
+//                      them (depth descending, ties by face index; op form: by face index) and the
+//                      wave writes each pixel's rows in turn, lanes across the row.
+//   kd_dt_interp       the interpolated features from face_idx / weights (flat, one thread per
+//                      (pixel, slot); the gathers would otherwise sit between the stores)
+constexpr int kDtCellK = 32;
+
+__host__ __device__ inline int64_t dt_max_items(int64_t P, int G) {
+  return (P + kWave - 1) / kWave + (int64_t)G * G;
+}
+
+struct DtCellBuf {
+  int *cell_cnt;   // [B][G*G]
+  int *cell_off;   // [B][G*G]
+  int *n_items;    // [B]
+  int2 *items;     // [B][max_items] (cell, chunk)
+  int2 *pix_cell;  // [B][P] (cell, position in the cell)
+  int *sorted;     // [B][P] pixel indices in cell order
+  int64_t max_items;
+};
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_dt_pix_count(int64_t P, int G, const T *px,
+                                                          DtCellBuf cb) {
+  const int b = blockIdx.y, lane = threadIdx.x & 63;
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  int c = -1;
+  if (p < P) {
+    const int64_t pp = (int64_t)b * P + p;
+    c = dt_cell(px[2 * pp + 1], G) * G + dt_cell(px[2 * pp], G);
+  }
+  int *cnt = cb.cell_cnt + (int64_t)b * G * G;
+  uint64_t todo = __ballot(c >= 0);
+  int pos = 0;
+  while (todo) {  // wave-uniform: one group of lanes in one cell per pass
+    const int leader = __builtin_ctzll(todo);
+    const int c0 = __builtin_amdgcn_readlane(c, leader);
+    const uint64_t m = __ballot(c == c0);
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&cnt[c0], __popcll(m));
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (c == c0) pos = base + lane_rank(m);
+    todo &= ~m;
+  }
+  if (p < P) cb.pix_cell[(int64_t)b * P + p] = make_int2(c, pos);
+}
+
+__global__ __launch_bounds__(kBlock) void kd_dt_pix_scan(int G, DtCellBuf cb) {
+  __shared__ int s_scan[kBlock / kWave];
+  const int b = blockIdx.x, tid = threadIdx.x, cells = G * G;
+  const int per = (cells + kBlock - 1) / kBlock;  // 16 (G = 64) or 4 (G = 32)
+  const int *cnt = cb.cell_cnt + (int64_t)b * cells;
+  int np = 0, nc = 0;
+  for (int k = 0; k < per; ++k) {
+    const int c = tid * per + k;
+    const int n = c < cells ? cnt[c] : 0;
+    np += n;
+    nc += (n + kWave - 1) / kWave;
+  }
+  int tot_p, tot_c;
+  int op = wg_exclusive_scan(np, s_scan, tot_p);
+  int oc = wg_exclusive_scan(nc, s_scan, tot_c);
+  int *off = cb.cell_off + (int64_t)b * cells;
+  int2 *items = cb.items + (int64_t)b * cb.max_items;
+  for (int k = 0; k < per; ++k) {
+    const int c = tid * per + k;
+    if (c >= cells) break;
+    const int n = cnt[c];
+    off[c] = op;
+    op += n;
+    for (int j = 0; j < (n + kWave - 1) / kWave; ++j) items[oc + j] = make_int2(c, j);
+    oc += (n + kWave - 1) / kWave;
+  }
+  if (tid == 0) cb.n_items[b] = tot_c;
+}
+
+__global__ __launch_bounds__(kBlock) void kd_dt_pix_scatter(int64_t P, int G, DtCellBuf cb) {
+  const int b = blockIdx.y;
+  const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= P) return;
+  const int2 cp = cb.pix_cell[(int64_t)b * P + p];
+  cb.sorted[(int64_t)b * P + cb.cell_off[(int64_t)b * G * G + cp.x] + cp.y] = (int)p;
+}
+
+// LDS of kd_dt_fwd_cell per wave: kept hits [64 pixels][KP] (KP odd: lane = pixel walks a row
+// with an odd word stride, conflict-free), face / depth / w0 / w1 and the rank (bytes).
+__host__ __device__ inline int dt_cell_kp(int K) { return K | 1; }
+template <typename T>
+__host__ __device__ inline size_t dt_cell_lds(int K) {
+  const int kp = dt_cell_kp(K);
+  return (size_t)kWave * kp * (sizeof(int) + 3 * sizeof(T)) + (size_t)kWave * (kp + 3) / 4 * 4 + 16;
+}
+
+template <typename T>
+__device__ __forceinline__ T bcast(T x, int j) {
+  return lane_bcast(x, j);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kWave) void kd_dt_fwd_cell(DtArgs<T> a, DtCellBuf cb) {
+  extern __shared__ __align__(16) char dc_lds[];
+  const int lane = threadIdx.x, b = blockIdx.y, K = a.K, KP = dt_cell_kp(K), G = a.G;
+  TileClock clk(a.tbuf, 0);  // diagnostics (flag 64): duration, start, list length
+  clk.start_to(1);
+  if ((int)blockIdx.x >= cb.n_items[b]) return;  // wave-uniform
+  T *hd = (T *)dc_lds;  // [64][KP] each
+  T *h0 = hd + kWave * KP, *h1 = h0 + kWave * KP;
+  int *hf = (int *)(h1 + kWave * KP);
+  uint8_t *rk = (uint8_t *)(hf + kWave * KP);
+  const int RB = (KP + 3) / 4 * 4;  // rank row bytes
+  const int2 item = cb.items[(int64_t)b * cb.max_items + blockIdx.x];
+  const int c = item.x;
+  const int ncell = cb.cell_cnt[(int64_t)b * G * G + c];
+  const int k = item.y * kWave + lane;
+  const bool live = k < ncell;
+  int p = 0;
+  T x0 = 0, y0 = 0, dmin = 0, dmax = 0;
+  if (live) {
+    p = cb.sorted[(int64_t)b * a.P + cb.cell_off[(int64_t)b * G * G + c] + k];
+    const int64_t pp = (int64_t)b * a.P + p;
+    x0 = a.px[2 * pp];
+    y0 = a.px[2 * pp + 1];
+    dmin = a.range[2 * pp];
+    dmax = a.range[2 * pp + 1];
+  }
+  const int nl = a.cursor[(int64_t)b * G * G + c];
+  if (KD_DIAG && a.tbuf && lane == 0) a.tbuf[2 * (int64_t)gridDim.x * gridDim.y + blockIdx.x] = nl;
+  const int *list = a.lists + (int64_t)c * a.N + (int64_t)b * a.F;
+  const T *boxes = a.boxes + (int64_t)b * a.F * 4;
+  const T *fvi = a.fvi + (int64_t)b * a.F * 6;
+  const T *fvz = a.fvz + (int64_t)b * a.F * 3;
+  const T eps = (T)a.eps;
+  int nh = 0, maxf = -1, maxs = 0;  // per lane: kept hits, the largest kept face index and its slot
+  T *myd = hd + lane * KP, *my0 = h0 + lane * KP, *my1 = h1 + lane * KP;
+  int *myf = hf + lane * KP;
+  for (int j0 = 0; j0 < nl; j0 += kWave) {
+    const int j = j0 + lane;
+    int f = -1;
+    T bx[4] = {0, 0, 0, 0}, v[6] = {0, 0, 0, 0, 0, 0}, z[3] = {0, 0, 0};
+    if (j < nl) {
+      f = list[j];
+      dt_load_box<T>(boxes, f, bx);
+#pragma unroll
+      for (int q = 0; q < 6; ++q) v[q] = fvi[(int64_t)f * 6 + q];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) z[q] = fvz[(int64_t)f * 3 + q];
+    }
+    const int m = ablate(a.dbg, 2) ? 0 : min(kWave, nl - j0);  // (diagnostics: no face loop)
+    for (int jj = 0; jj < m; ++jj) {
+      // the reference's half-open box test (deftet_cuda.cu:124-127)
+      const T bx0 = bcast(bx[0], jj), by0 = bcast(bx[1], jj);
+      const T bx1 = bcast(bx[2], jj), by1 = bcast(bx[3], jj);
+      const bool in = live && x0 >= bx0 && x0 < bx1 && y0 >= by0 && y0 < by1;
+      if (!__ballot(in) || ablate(a.dbg, 1)) continue;  // wave-uniform (diag: box tests only)
+      const T ax = bcast(v[0], jj), ay = bcast(v[1], jj), bxx = bcast(v[2], jj);
+      const T byy = bcast(v[3], jj), cx = bcast(v[4], jj), cy = bcast(v[5], jj);
+      const T z0 = bcast(z[0], jj), z1 = bcast(z[1], jj), z2 = bcast(z[2], jj);
+      const int fj = __builtin_amdgcn_readlane(f, jj);
+      T w0, w1, depth;
+      if (in && dt_face_weights<T>(ax, ay, bxx, byy, cx, cy, z0, z1, z2, x0, y0, dmin, dmax, eps,
+                                   w0, w1, depth)) {
+        int slot = -1;
+        if (nh < K) {
+          slot = nh++;
+          if (fj > maxf) {
+            maxf = fj;
+            maxs = slot;
+          }
+        } else if (fj < maxf) {  // keep the K smallest face indices
+          slot = maxs;
+        }
+        if (slot >= 0) {
+          myf[slot] = fj;
+          myd[slot] = depth;
+          my0[slot] = w0;
+          my1[slot] = w1;
+          if (nh == K && slot == maxs) {  // a replacement: find the new largest index
+            maxf = -1;
+            for (int e = 0; e < K; ++e)
+              if (myf[e] > maxf) {
+                maxf = myf[e];
+                maxs = e;
+              }
+          }
+        }
+      }
+    }
+  }
+  // ranks: sorted form -- depth descending, then face index (deftet.py:300-303, stable order);
+  // op form -- face index (the reference kernel's insertion order, deftet_cuda.cu:166-180)
+  for (int e = 0; e < nh; ++e) {
+    const int fe = myf[e];
+    const T de = myd[e];
+    int r = 0;
+    for (int q = 0; q < nh; ++q) {
+      const int fq = myf[q];
+      r += (a.depth ? fq < fe : (myd[q] > de || (myd[q] == de && fq < fe))) ? 1 : 0;
+    }
+    rk[lane * RB + e] = (uint8_t)r;
+  }
+  wave_lds_sync();
+  // rows, pixel by pixel: lanes across the row; entry e goes to slot rank[e], slots >= n are empty
+  const uint64_t lv = __ballot(live);
+  for (int i = 0; i < kWave; ++i) {
+    if (!((lv >> i) & 1)) continue;  // wave-uniform
+    const int pi = __builtin_amdgcn_readlane(p, i), ni = __builtin_amdgcn_readlane(nh, i);
+    const int64_t row0 = ((int64_t)b * a.P + pi) * K;
+    const uint8_t *ri = rk + i * RB;
+    if (lane < K) {
+      const bool h = lane < ni;
+      const int slot = h ? ri[lane] : lane;
+      const int64_t o = row0 + slot;
+      if (a.depth) {  // op form: empty slots -1 / -inf / 0 / 0 (deftet.cpp:88-94)
+        a.face_idx[o] = h ? (int64_t)hf[i * KP + lane] : -1;
+        a.depth[o] = h ? hd[i * KP + lane] : (T)-INFINITY;
+        a.w0[o] = h ? h0[i * KP + lane] : (T)0;
+        a.w1[o] = h ? h1[i * KP + lane] : (T)0;
+      } else {
+        a.face_idx[o] = h ? (int64_t)hf[i * KP + lane] : -1;
+      }
+    }
+    if (!a.depth)
+      for (int t = lane; t < 3 * K; t += kWave) {
+        const int e = small_div(t, 1.f / 3.f), cc = t - 3 * e;
+        const bool h = e < ni;
+        T val = (T)0;
+        if (h) {
+          const T w0 = h0[i * KP + e], w1 = h1[i * KP + e];
+          val = cc == 0 ? w0 : cc == 1 ? w1 : (T)1 - (w0 + w1);  // deftet.py:304
+        }
+        a.weights[3 * (row0 + (h ? ri[e] : e)) + cc] = val;
+      }
+  }
+}
+
+// interp (B, P, K, D) from face_idx and weights: deftet.py:312-313, the sum over the 3 corners
+template <typename T>
+__global__ __launch_bounds__(kBlock) void kd_dt_interp(int64_t PK, int64_t F, int D,
+                                                       const int64_t *face_idx, const T *weights,
+                                                       const T *feat, T *interp, int64_t n) {
+  for (int64_t o = (int64_t)blockIdx.x * kBlock + threadIdx.x; o < n;
+       o += (int64_t)gridDim.x * kBlock) {
+    const int64_t f = face_idx[o];
+    T *out = interp + o * D;
+    if (f < 0) {
+      for (int d = 0; d < D; ++d) out[d] = (T)0;
+      continue;
+    }
+    const T w0 = weights[3 * o], w1 = weights[3 * o + 1], w2 = weights[3 * o + 2];
+    const T *cf = feat + ((o / PK) * F + f) * 3 * D;
+    for (int d = 0; d < D; ++d) out[d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+  }
+}
+
+// Workspace: [cursor | cell_cnt] (one memset), the cell lists, the face boxes; with P >= 0 also
+// the cell-major forward's pixel sort (kd_deftet_workspace_size_p).
+static size_t dt_workspace(int B, int64_t F, size_t esize, int64_t P = -1) {
   const int64_t N = (int64_t)B * F;
-  const int64_t cells = (int64_t)dt_grid(N) * dt_grid(N);
-  return align_up(sizeof(int) * (size_t)B * cells) +
-         align_up(sizeof(int) * (size_t)cells * (size_t)(N > 0 ? N : 1)) +
-         align_up(4 * esize * (size_t)N);  // the face boxes
+  const int G = dt_grid(N);
+  const int64_t cells = (int64_t)G * G;
+  size_t n = align_up(2 * sizeof(int) * (size_t)B * cells) +
+             align_up(sizeof(int) * (size_t)cells * (size_t)(N > 0 ? N : 1)) +
+             align_up(4 * esize * (size_t)N);  // the face boxes
+  if (P >= 0)
+    n += align_up(sizeof(int) * (size_t)B * cells) + align_up(sizeof(int) * (size_t)B) +
+         align_up(sizeof(int2) * (size_t)B * dt_max_items(P, G)) +
+         align_up(sizeof(int2) * (size_t)B * P) + align_up(sizeof(int) * (size_t)B * P);
+  return n;
 }
 
 static int dt_capacity(int K) { return K < 256 ? 256 : K; }
@@ -705,10 +996,16 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
   if (B == 0 || P == 0) return KD_OK;
   const int64_t N = (int64_t)B * F;
   const int G = dt_grid(N);
-  int *cursor = (int *)ws;
-  int *lists = (int *)((char *)ws + align_up(sizeof(int) * (size_t)B * G * G));
-  T *boxes = (T *)((char *)lists + align_up(sizeof(int) * (size_t)G * G * (size_t)(N > 0 ? N : 1)));
-  hipError_t e = hipMemsetAsync(cursor, 0, sizeof(int) * (size_t)B * G * G, stream);
+  const size_t cells = (size_t)G * G;
+  char *w = (char *)ws;
+  int *cursor = (int *)w;
+  int *cell_cnt = cursor + (size_t)B * cells;
+  w += align_up(2 * sizeof(int) * (size_t)B * cells);
+  int *lists = (int *)w;
+  w += align_up(sizeof(int) * cells * (size_t)(N > 0 ? N : 1));
+  T *boxes = (T *)w;
+  w += align_up(4 * sizeof(T) * (size_t)N);
+  hipError_t e = hipMemsetAsync(cursor, 0, 2 * sizeof(int) * (size_t)B * cells, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "deftet: %s", hipGetErrorString(e));
   if (F > 0) {
     ProfScope prof(K_DT_BIN, stream);
@@ -720,12 +1017,51 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
               eps, px,     range, fvz,    fvi,     feat,     cursor,  lists,
               bbox ? bbox : boxes, interp, face_idx, weights, bbox, depth, w0, w1,
               debug_flags(), debug_tile_buffer()};
-  // the pooled kernel (knum <= 32, <= 4 features) only under debug flag 2048: measured slower
-  // than the per-pixel wave kernel
+  // kernel choice: the per-pixel waves, unless debug flag 1024 selects the cell-major forward
+  // (knum <= 32, a workspace that holds the pixel sort: kd_deftet_workspace_size_p) or 2048 the
+  // pooled one -- both bit-identical and measured slower
+  const bool cellmajor = K <= kDtCellK && wsb >= dt_workspace(B, F, sizeof(T), P) &&
+                         (debug_flags() & 1024) && !(debug_flags() & 2048);
   const bool pooled = K <= kDtMaxK && D <= kDtMaxD && (debug_flags() & 2048);
-  const int64_t gx = pooled ? (P + kDtPx - 1) / kDtPx : (P + kDtWaves - 1) / kDtWaves;
-  KD_CHECK_ARG(gx < (1ll << 31), "deftet: too many pixels");
-  {
+  if (cellmajor) {
+    KD_CHECK_ARG(P < (1ll << 31), "deftet: too many pixels");
+    DtCellBuf cb;
+    cb.cell_cnt = cell_cnt;
+    cb.cell_off = (int *)w;
+    w += align_up(sizeof(int) * (size_t)B * cells);
+    cb.n_items = (int *)w;
+    w += align_up(sizeof(int) * (size_t)B);
+    cb.max_items = dt_max_items(P, G);
+    cb.items = (int2 *)w;
+    w += align_up(sizeof(int2) * (size_t)B * cb.max_items);
+    cb.pix_cell = (int2 *)w;
+    w += align_up(sizeof(int2) * (size_t)B * P);
+    cb.sorted = (int *)w;
+    const unsigned pb = (unsigned)((P + kBlock - 1) / kBlock);
+    {
+      ProfScope prof(K_DT_BIN, stream);
+      hipLaunchKernelGGL(kd_dt_pix_count<T>, dim3(pb, B), dim3(kBlock), 0, stream, P, G, px, cb);
+      hipLaunchKernelGGL(kd_dt_pix_scan, dim3(B), dim3(kBlock), 0, stream, G, cb);
+      hipLaunchKernelGGL(kd_dt_pix_scatter, dim3(pb, B), dim3(kBlock), 0, stream, P, G, cb);
+    }
+    {
+      ProfScope prof(K_DT_FWD, stream);
+      const size_t lds = dt_cell_lds<T>(K);
+      if (lds > 64 * 1024)
+        (void)hipFuncSetAttribute((const void *)kd_dt_fwd_cell<T>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL(kd_dt_fwd_cell<T>, dim3((unsigned)cb.max_items, B), dim3(kWave), lds,
+                         stream, a, cb);
+      const int64_t n = (int64_t)B * P * K;
+      if (!depth && D > 0)
+        hipLaunchKernelGGL(kd_dt_interp<T>,
+                           dim3((unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 1 << 20)),
+                           dim3(kBlock), 0, stream, P * K, F, D, face_idx, weights, feat, interp,
+                           n);
+    }
+  } else {
+    const int64_t gx = pooled ? (P + kDtPx - 1) / kDtPx : (P + kDtWaves - 1) / kDtWaves;
+    KD_CHECK_ARG(gx < (1ll << 31), "deftet: too many pixels");
     ProfScope prof(K_DT_FWD, stream);
     if (pooled) {
       hipLaunchKernelGGL(kd_dt_fwd_pool<T>, dim3((unsigned)gx, B), dim3(kWave), 0, stream, a);
@@ -766,6 +1102,10 @@ extern "C" {
 size_t kd_deftet_workspace_size(int B, int64_t F, int double_precision) {
   if (B < 0 || F < 0) return 0;
   return dt_workspace(B, F, double_precision ? sizeof(double) : sizeof(float));
+}
+size_t kd_deftet_workspace_size_p(int B, int64_t P, int64_t F, int double_precision) {
+  if (B < 0 || F < 0 || P < 0) return 0;
+  return dt_workspace(B, F, double_precision ? sizeof(double) : sizeof(float), P);
 }
 
 int kd_deftet_sparse_render_forward_f32(int B, int64_t P, int64_t F, int knum, int D,
