@@ -1402,10 +1402,13 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
     if (a.prob) {  // soft mask + the close lists, row-coalesced (dynamic LDS past 64 KB)
       KD_CHECK_ARG(fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
       const size_t dyn = ((sizeof(T) + sizeof(int)) * (kReduceSlots + 1) + sizeof(int)) * kBlock / 2;
-      const hipError_t ea = hipFuncSetAttribute((const void *)kd_soft_lists<T>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                (int)dyn);
-      if (ea != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft lists: %s", hipGetErrorString(ea));
+      if (dyn > 64 * 1024) {  // (34 KB fp32, 51 KB fp64: within the default limit)
+        const hipError_t ea = hipFuncSetAttribute((const void *)kd_soft_lists<T>,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  (int)dyn);
+        if (ea != hipSuccess)
+          return set_error(KD_ERR_LAUNCH, "soft lists: %s", hipGetErrorString(ea));
+      }
       if (ablate(debug_flags(), (1 << 16) | (1 << 23)))  // diagnostics: the skipped index stores
         hipMemsetAsync(a.cidx, 0xFF, sizeof(int64_t) * fs.B * fs.H * fs.W * a.K, stream);  // -1
       hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), dyn, stream, a, pb);
