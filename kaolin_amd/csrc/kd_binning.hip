@@ -123,7 +123,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 #pragma unroll
     for (int z = 0; z < NS; ++z) {
       const BinBuffers &bb = jobs.bb[z0 + z];
-      if (bb.clear && tid < bb.n_clear) bb.clear[tid] = 0;
+      if (bb.clear)
+        for (int i = tid; i < bb.n_clear; i += kBlock) bb.clear[i] = 0;
       for (int i = tid; i < bb.n_clear_b; i += kBlock) bb.clear_b[i] = 0;
     }
   }

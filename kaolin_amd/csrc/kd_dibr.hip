@@ -117,7 +117,8 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   d.rbb.cull_eps = eps;
   d.sbb.cull = nullptr;
   d.sbb.clear = d.pb.counters;
-  d.sbb.n_clear = kPairClear;
+  // the counters (and, when helper workgroups are requested, their jobs / FIFOs)
+  d.sbb.n_clear = (debug_flags() & (256 | 512)) ? kHelpClear : kPairClear;
   if (iou.gt) {  // the IoU accumulators start at zero (kd_bin_count)
     d.sbb.clear_b = (int *)iou.acc;
     d.sbb.n_clear_b = 4 * kIouParts * B;

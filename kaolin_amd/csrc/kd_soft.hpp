@@ -213,6 +213,41 @@ struct PairItem {
 // under kd_set_pool_limits) a tile whose reservation does not fit computes its soft mask without
 // records (`ovf` list, kd_soft_ovf_fwd) and its backward recomputes the pairs
 // (kd_soft_ovf_bwd).
+// Helper workgroups of the fused fp32 forward (kd_dibr_fwd_help, kd_softpair.hip).  A silhouette
+// tile's pair math (one workgroup: ~20 us of issue-bound fp64 arithmetic for ~5000 records) is
+// the tail of the forward -- at one view its whole length.  A tile with more than kHelpMin
+// records publishes a job: its records in chunks of kHelpChunk, claimed with a device atomic by
+// the owner itself and by helper workgroups launched after the tiles.  Jobs stay on the owner's
+// XCD (a FIFO of job entries per XCD): owner and helpers share one L2, so the records and
+// probabilities need no device-scope cache write-back / invalidation (those fences, measured,
+// cost more than the whole forward), only stores completed before the atomics that publish them.
+// The owner waits only for chunks a running workgroup has claimed; tiles never wait for anything
+// before their pair math, so every helper's exit condition (every tile past pass A, its FIFO
+// drained) is reached.
+struct HelpJob {
+  unsigned long long word;  // n << 32 | (tile + 1); 0 until published
+  int claim;                // chunks claimed
+  int done;                 // chunks finished by helpers
+  int pad[12];              // one job per 64-byte line (its claims are contended)
+};
+static_assert(sizeof(HelpJob) == 64, "HelpJob: 64 bytes (16 ints of the counters region)");
+constexpr int kHelpMin = 1024;    // records of a tile that publishes a job
+constexpr int kHelpChunk = 512;   // records per claimed chunk
+constexpr int kHelpFan = 8;       // FIFO entries (helpers invited) per job, at most
+constexpr int kHelpJobs = 256;
+constexpr int kHelpXcds = 8;      // FIFOs (XCC_ID & 7)
+constexpr int kHelpFifoX = 256;   // entries per FIFO
+constexpr int kHelpers = 64;      // helper workgroups per launch, at most
+// SoftPairBuf::counters: [0..5] as below; the helpers' shared words each on its own 128-byte
+// line (away from the tiles' item counters): [kHelpPassed] tiles past pass A, [kHelpNJobs] jobs
+// reserved, [kHelpTail + 32 x] / [kHelpHead + 32 x] tail / head of XCD x's FIFO; then the jobs
+// and the FIFOs (ints zeroed by kd_bin_count: kHelpClear)
+constexpr int kHelpPassed = 32, kHelpNJobs = 64, kHelpTail = 96;
+constexpr int kHelpHead = kHelpTail + 32 * kHelpXcds;
+constexpr int kHelpJobsAt = kHelpHead + 32 * kHelpXcds;
+constexpr int kHelpFifoAt = kHelpJobsAt + 16 * kHelpJobs;
+constexpr int kHelpClear = kHelpFifoAt + kHelpXcds * kHelpFifoX;
+
 template <typename T>
 struct SoftPairBuf {
   SoftPairRec *rec;    // [cap]
@@ -227,6 +262,8 @@ struct SoftPairBuf {
                        // forward ran kd_dibr_fwd_st, overflow entries are 4 tile + quadrant); then the 64-bit
                        // record cursor (all zeroed by kd_bin_count: n_clear = 6)
   unsigned long long *cursor;
+  HelpJob *jobs;       // [kHelpJobs] (after the counters; see kHelpClear)
+  int32_t *fifo;       // [kHelpFifo] job + 1 per entry, 0 until written
   int64_t ntiles, npixels, cap, lim;  // lim: records a forward may use (kd_set_pool_limits)
   int fixed;  // knum <= 32 and the whole pool usable: tile t owns records [t * 256 K, +256 K)
   int ntx;

@@ -66,7 +66,7 @@ size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int 
   s += align_up(sizeof(PairItem) * (size_t)(recs / kBlock + 4 * tiles));
   s += align_up(sizeof(int32_t) * (size_t)tiles);
   s += align_up(sizeof(int32_t) * (size_t)(4 * tiles));
-  s += align_up(sizeof(int32_t) * 8);
+  s += align_up(sizeof(int32_t) * kHelpClear);  // counters, helper jobs and FIFO
   return s;
 }
 
@@ -99,7 +99,9 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   off += align_up(sizeof(int32_t) * (size_t)(4 * tiles));
   pb.counters = (int32_t *)(base + off);
   pb.cursor = (unsigned long long *)(pb.counters + 4);
-  off += align_up(sizeof(int32_t) * 8);
+  pb.jobs = (HelpJob *)(pb.counters + kHelpJobsAt);
+  pb.fifo = pb.counters + kHelpFifoAt;
+  off += align_up(sizeof(int32_t) * kHelpClear);
   return pb;
 }
 
@@ -505,6 +507,9 @@ struct SoftPairsLDS {
   double iou[8];  // iou_tile_terms
   SoftItemsLDS it;  // BAL / ST pass A (soft_round_items)
   int wbox[4][4];   // per wave: the box of its pixels that can still take a face (walk filter)
+  int job, claim;   // HELP: the tile's published job, the owner's current chunk
+  int hact, hc, hn, hjob;  // helper workgroups: thread 0's decision, broadcast
+  int64_t htile;
 };
 
 // Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
@@ -516,7 +521,193 @@ struct SoftPairsLDS {
 // share its 64 pixels (wave 0 owns them: soft values, product, IoU terms), pass A deals its
 // chunks to the four waves (soft_round_items), the pair math runs on all 256 threads; the
 // quadrant's records sit in its quarter of the tile's room, with the tile frame's pixel index.
-template <typename T, bool FUSED, bool ST = false, bool BAL = false>
+// ------------------------------------------------------------------------------------------
+// helper workgroups of the fused forward (kd_soft.hpp HelpJob).  Polling reads are returning
+// atomics (a CAS with a value the word never holds).  Owner and helpers run on one XCD: a
+// producer's stores are complete (s_waitcnt vmcnt(0): in its XCD's L2) before the atomic that
+// publishes them, and a consumer drops its CU's L1 (buffer_inv sc0) before reading them.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int poll_i32(int *p) {
+  return atomicCAS(p, (int)0x80000000, (int)0x80000000);
+}
+__device__ __forceinline__ unsigned long long poll_u64(unsigned long long *p) {
+  return atomicCAS(p, ~0ull, ~0ull);
+}
+__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void drop_l1() { asm volatile("buffer_inv sc0" ::: "memory"); }
+__device__ __forceinline__ int xcc_id() {
+  return (int)__builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & (kHelpXcds - 1);
+}
+
+// The pair math of records [i0, i1) of the tile whose records start at `base` (tile column tx,
+// row ty): distance type and probability, bit-identical to the reference (kd_softdist.hpp).
+template <typename T>
+__device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
+                                                int64_t base, int tx, int ty, int i0, int i1) {
+  const FaceSet<T> &fs = a.fs;
+  const float M = fs.M;
+  const SoftPairRec *rec = pb.rec + base;
+  T *sp = pb.sprob + base;
+  for (int i = i0 + (int)threadIdx.x; i < i1 && !ablate(fs.dbg, 32); i += kBlock) {
+    const SoftPairRec r = rec[i];
+    T v[6];
+    load_corners(fs, (int64_t)r.row, v);
+    int px, py;
+    tile_pixel(tx, ty, r.q, px, py);
+    const T x0 = (T)px_cx(M, fs.W, px), y0 = (T)px_cy(M, fs.H, py);
+    int et = 0;
+    T prob = (T)0;
+    soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
+    sp[i] = prob;
+    pb.rec[base + i].type = (uint8_t)et;
+    // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
+  }
+}
+
+// Owner side, after pass A (every tile of a helped launch calls it once, n uniform): a tile with
+// more than kHelpMin records (fixed pool layout) publishes a job -- its records in its XCD's L2,
+// the job word, up to kHelpFan entries in its XCD's FIFO -- and then counts itself past pass A.
+// Returns the job (or -1: the tile does its own pair math as without helpers).
+template <typename T>
+__device__ __forceinline__ int help_publish(const SoftPairBuf<T> &pb, int64_t tile, int n,
+                                            int *s_job) {
+  const bool heavy = n > kHelpMin && pb.fixed;
+  if (heavy) stores_done();  // this thread's records (pass A) are in the L2
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int j = -1;
+    if (heavy) {
+      j = atomicAdd(&pb.counters[kHelpNJobs], 1);
+      if (j < kHelpJobs) {
+        const int x = xcc_id();
+        const int nch = (n + kHelpChunk - 1) / kHelpChunk;
+        const int ne = min(nch - 1, kHelpFan);
+        atomicExch(&pb.jobs[j].word,
+                   ((unsigned long long)(unsigned)n << 32) | (unsigned long long)(tile + 1));
+        // FIFO entries: reserved without passing its end (a job without entries is the
+        // owner's alone)
+        int *tail = &pb.counters[kHelpTail + 32 * x];
+        int t0 = poll_i32(tail);
+        while (t0 + ne <= kHelpFifoX) {
+          const int o = atomicCAS(tail, t0, t0 + ne);
+          if (o == t0) break;
+          t0 = o;
+        }
+        if (t0 + ne <= kHelpFifoX)
+          for (int e = 0; e < ne; ++e) atomicExch(&pb.fifo[x * kHelpFifoX + t0 + e], j + 1);
+      } else {
+        j = -1;
+      }
+    }
+    if (heavy) stores_done();  // (the entries before the count)
+    atomicAdd(&pb.counters[kHelpPassed], 1);
+    *s_job = j;
+  }
+  __syncthreads();
+  return *s_job;
+}
+
+// Owner side: claim chunks of job `job` (the next claim in flight during the math), then wait
+// for the chunks helpers claimed (each is being worked on by a running workgroup).
+template <typename T>
+__device__ __forceinline__ void help_owner_math(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
+                                                int job, int64_t base, int tx, int ty, int n,
+                                                int *s_claim) {
+  const int nch = (n + kHelpChunk - 1) / kHelpChunk;
+  int *claim = &pb.jobs[job].claim;
+  if (threadIdx.x == 0) *s_claim = atomicAdd(claim, 1);
+  __syncthreads();
+  int c = *s_claim, mine = 0;
+  while (c < nch) {
+    __syncthreads();  // every thread has read *s_claim
+    int nxt = 0;
+    if (threadIdx.x == 0) nxt = atomicAdd(claim, 1);
+    pair_math_range<T>(a, pb, base, tx, ty, c * kHelpChunk, min(n, (c + 1) * kHelpChunk));
+    ++mine;
+    if (threadIdx.x == 0) *s_claim = nxt;
+    __syncthreads();
+    c = *s_claim;
+  }
+  if (mine < nch) {
+    if (threadIdx.x == 0)
+      while (poll_i32(&pb.jobs[job].done) < nch - mine) __builtin_amdgcn_s_sleep(2);
+    __syncthreads();
+    drop_l1();  // the helpers' probabilities (in the L2)
+  }
+}
+
+// A helper workgroup: take an entry of its XCD's FIFO (a job), claim its chunks until none is
+// left, repeat; exit once every tile is past pass A and the FIFO is drained (the owners finish
+// what is left).
+template <typename T>
+__device__ __forceinline__ void help_loop(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
+                                          int ntot, SoftPairsLDS<true> &S) {
+  zero_side_job(a);
+  const int x = xcc_id();
+  int *tailp = &pb.counters[kHelpTail + 32 * x], *headp = &pb.counters[kHelpHead + 32 * x];
+  const int *fifo = pb.fifo + x * kHelpFifoX;
+  int jj = -1, jn = 0, jnch = 0, seen = 0;  // thread 0: the current job, the last head seen
+  int64_t jtile = 0;
+  while (true) {
+    if (threadIdx.x == 0) {
+      int act = 3, c = 0;  // 1 work chunk c, 0 retry now, 2 exit, 3 sleep and retry
+      if (jj >= 0) {
+        c = atomicAdd(&pb.jobs[jj].claim, 1);
+        if (c < jnch) act = 1;
+        else jj = -1;
+      }
+      if (jj < 0) {
+        const int tail = poll_i32(tailp);
+        // (head only moves up to tail: a tail at the last head seen means nothing new)
+        const int head = tail > seen ? poll_i32(headp) : tail;
+        seen = head;
+        if (head >= tail && poll_i32(&pb.counters[kHelpPassed]) >= ntot) {
+          // every tile is past pass A, so every entry is in: read the FIFO again (issued after
+          // the count returned -- the branch depends on it) to see whether it is drained
+          act = poll_i32(headp) >= poll_i32(tailp) ? 2 : 0;
+        } else if (head < tail) {
+          act = 0;
+          if (atomicCAS(headp, head, head + 1) == head) {
+            int e;
+            while ((e = poll_i32(const_cast<int *>(fifo) + head)) == 0)
+              __builtin_amdgcn_s_sleep(1);
+            jj = e - 1;
+            unsigned long long wd;
+            while ((wd = poll_u64(&pb.jobs[jj].word)) == 0ull) __builtin_amdgcn_s_sleep(1);
+            jn = (int)(wd >> 32);
+            jtile = (int64_t)(wd & 0xffffffffull) - 1;
+            jnch = (jn + kHelpChunk - 1) / kHelpChunk;
+            c = atomicAdd(&pb.jobs[jj].claim, 1);
+            if (c < jnch) act = 1;
+            else jj = -1;
+          }
+        }
+      }
+      S.hact = act;
+      S.hc = c;
+      S.hn = jn;
+      S.hjob = jj;
+      S.htile = jtile;
+    }
+    __syncthreads();
+    const int act = S.hact, c = S.hc, n = S.hn, job = S.hjob;
+    const int64_t tile = S.htile;
+    __syncthreads();
+    if (act == 2) return;
+    if (act == 3) __builtin_amdgcn_s_sleep(48);  // idle: ~1.3 us between polls
+    if (act == 0) __builtin_amdgcn_s_sleep(2);   // lost a race for the FIFO head
+    if (act != 1) continue;
+    drop_l1();  // the owner's records (in the L2)
+    const int tl = (int)(tile % pb.ntiles);
+    pair_math_range<T>(a, pb, tile * kBlock * (int64_t)a.K, tl % pb.ntx, tl / pb.ntx,
+                       c * kHelpChunk, min(n, (c + 1) * kHelpChunk));
+    stores_done();  // probabilities and types in the L2
+    __syncthreads();
+    if (threadIdx.x == 0) atomicAdd(&pb.jobs[job].done, 1);
+  }
+}
+
+template <typename T, bool FUSED, bool ST = false, bool BAL = false, bool HELP = false>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                 int b, int tl, int nbin, SoftPairsLDS<FUSED> &S,
                                                 int quad = 0) {
@@ -527,7 +718,6 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   const int H = fs.H, W = fs.W, K = a.K;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const bool own = !ST || w == 0;  // this thread writes its pixel's results
-  const float M = fs.M;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   const int nview = (int)(hi - lo);
@@ -718,28 +908,18 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   }
   if constexpr (FUSED) {
     zero_side_job(a);
+    const int job = HELP ? help_publish<T>(pb, tile, n, &S.job) : -1;
     if (n == 0) {
       iou_tile_terms<T>(a, b, tl, p, t.inimg && own, sval, S.iou);
       return;
     }
-    // pair math over this tile's records (record order: coalesced reads)
+    // pair math over this tile's records (record order: coalesced reads; diag 32: none)
     const int tx = tl % pb.ntx, ty = tl / pb.ntx;
-    const SoftPairRec *rec = pb.rec + base;
-    T *sp = pb.sprob + base;
-    for (int i = tid; i < n && !ablate(fs.dbg, 32); i += kBlock) {  // (diag 32: no pair math)
-      const SoftPairRec r = rec[i];
-      T v[6];
-      load_corners(fs, (int64_t)r.row, v);
-      int px, py;
-      tile_pixel(tx, ty, r.q, px, py);
-      const T x0 = (T)px_cx(M, W, px), y0 = (T)px_cy(M, H, py);
-      int et = 0;
-      T prob = (T)0;
-      soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
-      sp[i] = prob;
-      pb.rec[base + i].type = (uint8_t)et;
-      // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
-    }
+    const T *sp = pb.sprob + base;
+    if (HELP && job >= 0)
+      help_owner_math<T>(a, pb, job, base, tx, ty, n, &S.claim);
+    else
+      pair_math_range<T>(a, pb, base, tx, ty, 0, n);
     __syncthreads();  // the workgroup's probabilities are visible to it
     if (KD_DIAG && fs.tbuf && tid == 0)  // diagnostics: end of the pair math
       fs.tbuf[6ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
@@ -816,6 +996,25 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
   soft_pairs_tile<float, true, false, BAL>(a, pb, b, tl, -1, U.s);
+}
+
+// kd_dibr_fwd_tiles with helper workgroups (kd_soft.hpp HelpJob): a 1-D grid of the B x tiles
+// tile workgroups (dispatch slot d = blockIdx.x, the same heaviest-first, XCD-aware order) and
+// then `nhelp` helpers, which work on the published pair math of the silhouette tiles.
+__global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_help(RasterFwdArgs<float> ra,
+                                                             SoftArgs<float> a,
+                                                             SoftPairBuf<float> pb) {
+  __shared__ DibrTileLDS<float> U;
+  const int ntot = (int)(pb.ntiles * ra.fs.B);
+  if ((int)blockIdx.x >= ntot) {
+    help_loop<float>(a, pb, ntot, U.s);
+    return;
+  }
+  int b, tl, nbin;
+  tile_of_slot(ra.bb, ra.fs.H, ra.fs.W, (int)blockIdx.x, ntot, b, tl, nbin, ra.fs.dbg);
+  raster_pairs_tile<float>(ra, b, tl, nbin, U.r);
+  __syncthreads();  // the raster phase is done with the LDS
+  soft_pairs_tile<float, true, false, false, true>(a, pb, b, tl, -1, U.s);
 }
 
 // The small-batch form of kd_dibr_fwd_tiles (few views: the grid of 16x16 tiles is about one
@@ -1448,6 +1647,34 @@ bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) 
          !(debug_flags() & ((1 << 26) | 4096));
 }
 
+// Helper workgroups for kd_dibr_fwd_help (0: the plain tile kernel).  Needs the fixed pool
+// layout (a job's records start at tile * 256 K), the per-launch help region zeroed by the
+// binning (kHelpClear) and an occupancy that leaves the tiles slots beside the helpers: the
+// helpers are at most half of the chip's resident workgroups of this kernel, so tiles -- which
+// never wait -- always find slots, and every helper's exit condition is reached.
+// Opt-in (debug flag 256; 512: the helped kernel without helper workgroups, returned as -1):
+// measured slower than the plain tile kernel at every view count (C3, same box: 1 view forward
+// 82.6 us against 67.5, 2 views 123 against 72, 8 views 210 against 157; without helper
+// workgroups 72.4 / 161.5 -- the owners' claims alone cost ~5 us), see DESIGN.md section 4.
+static int help_workgroups(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a,
+                           const SoftPairBuf<float> &pb) {
+  if (!(a.fs.dbg & (256 | 512)) || a.fs.tbuf || !pb.fixed || a.K > kFuseSlots ||
+      a.bb.n_clear < kHelpClear || (a.fs.dbg & (1 << 28)) || pb.ntiles * ra.fs.B >= (1 << 30))
+    return 0;
+  static int slots = -1;  // resident kd_dibr_fwd_help workgroups of the device (first call)
+  if (slots < 0) {
+    int dev = 0, ncu = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kd_dibr_fwd_help, kBlock, 0) !=
+            hipSuccess)
+      ncu = per = 0;
+    slots = ncu * per;
+  }
+  if (a.fs.dbg & 512) return -1;  // A/B: the helped tile kernel without helper workgroups
+  return std::min(kHelpers, slots / 2);
+}
+
 int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
                           hipStream_t stream) {
   ra.fs.dbg = a.fs.dbg = debug_flags();
@@ -1463,6 +1690,11 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
     else
       hipLaunchKernelGGL(kd_dibr_fwd_st<false>, dim3((unsigned)nwg), dim3(kBlock), 0, stream, ra,
                          a, pb);
+  } else if (const int nh = help_workgroups(ra, a, pb)) {
+    ProfScope prof(K_DIBR_FWD, stream);
+    const int64_t ntot = pb.ntiles * ra.fs.B;
+    hipLaunchKernelGGL(kd_dibr_fwd_help, dim3((unsigned)(ntot + std::max(nh, 0))), dim3(kBlock),
+                       0, stream, ra, a, pb);
   } else {
     ProfScope prof(K_DIBR_FWD, stream);
     const dim3 grid((unsigned)pb.ntiles, ra.fs.B);

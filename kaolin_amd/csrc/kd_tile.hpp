@@ -36,14 +36,12 @@ struct TileGeom {
   int SX0, SX1, SY0, SY1;      // this wave's sub-list filter
 };
 
-// (view, fine tile) of this workgroup: the bins' heaviest-first order (tile_order) when the
-// bins were built, else (blockIdx.y, blockIdx.x).
-__device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W, int &b,
-                                              int &tile, int &nbin, int dbg = 0) {
+// (view, fine tile) of dispatch slot d of n tile slots: the bins' heaviest-first order
+// (tile_order) when the bins were built, else slot order.
+__device__ __forceinline__ void tile_of_slot(const BinBuffers &bb, int H, int W, int d, int n,
+                                             int &b, int &tile, int &nbin, int dbg = 0) {
   if (bb.order && bb.nchunk > 0) {
     const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    const int n = gridDim.x * gridDim.y;
-    int d = blockIdx.y * gridDim.x + blockIdx.x;
     // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (d % 8), and the order holds a
     // coarse tile's fine tiles consecutively; within each group of 32 workgroups fine tile j of
     // coarse tile g runs at d = 8 j + g, so the tiles sharing a coarse bin share one L2.
@@ -52,6 +50,19 @@ __device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W
     b = v.x / ntiles;
     tile = v.x - b * ntiles;
     nbin = v.y;
+  } else {
+    const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    b = d / ntiles;
+    tile = d - b * ntiles;
+    nbin = -1;
+  }
+}
+// ... of this workgroup of a (tiles, views) grid
+__device__ __forceinline__ void tile_of_block(const BinBuffers &bb, int H, int W, int &b,
+                                              int &tile, int &nbin, int dbg = 0) {
+  if (bb.order && bb.nchunk > 0) {
+    tile_of_slot(bb, H, W, blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, b, tile,
+                 nbin, dbg);
   } else {
     b = blockIdx.y;
     tile = blockIdx.x;

@@ -77,10 +77,14 @@ if t[5].any():  # soft phase split: pass A (walk + records), pair math, product 
     rend = t[3]
     pa = np.where(t[5] > 0, (t[5] - rend) / 100.0, 0)
     pm = np.where((t[6] > 0) & (t[5] > 0), (t[6] - t[5]) / 100.0, 0)
-    print('slowest tiles: slot | raster us | soft: passA pairmath rest | soft_nbin unc')
+    print('slowest tiles: slot | raster us | soft: passA pairmath rest | soft_nbin unc | '
+          'raster_nbin | view tx ty')
     for i in np.argsort(end)[::-1][:15]:
+        tv = int(tile[i]) // (ntx * nty)
+        tt = int(tile[i]) % (ntx * nty)
         print(f'  {i:5d} | {rdur[i]:6.1f} | {pa[i]:6.1f} {pm[i]:6.1f} '
-              f'{dur[i] - rdur[i] - pa[i] - pm[i]:6.1f} | {t[4][i]:5d} {u_slot[i]:4d}')
+              f'{dur[i] - rdur[i] - pa[i] - pm[i]:6.1f} | {t[4][i]:5d} {u_slot[i]:4d} | '
+              f'{nbin[i]:5d} | {tv} {tt % ntx} {tt // ntx}')
     print(f'sums (ms): passA {pa.sum() / 1e3:.2f} pairmath {pm.sum() / 1e3:.2f}')
 late = np.argsort(end)[::-1][:10]
 print('latest ending (slot, start, dur):', [(int(i), round(float(start[i]), 1),
