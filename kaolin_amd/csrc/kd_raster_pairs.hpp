@@ -93,7 +93,9 @@ template <typename T>
 struct RasterPairsLDS {
   TileLists L;
   T geo[9][kCap];        // ax ay bx by cx cy (scaled), az bz cz
-  float4 cull[2][kCap];  // raster_cull_coefs (kd_binning), face frame
+  // raster_cull_coefs (kd_binning), face frame.  fp64: read from global memory in pass A
+  // instead (8 KB less LDS: five workgroups per CU instead of four)
+  float4 cull[2][sizeof(T) == 8 ? 1 : kCap];
   unsigned short pair[4][kRasterPairCap];  // (q << 8) | sub-list entry
   unsigned long long key[4][64];
   unsigned long long zx[sizeof(T) == 8 ? 4 : 1][64];  // fp64: ordered exact maximum depth
@@ -152,8 +154,10 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     s_geo[6][k] = zz[0];
     s_geo[7][k] = zz[a.fvz_cs];
     s_geo[8][k] = zz[2 * a.fvz_cs];
-    s_cull[0][k] = a.bb.cull[2 * fi];
-    s_cull[1][k] = a.bb.cull[2 * fi + 1];
+    if constexpr (!kF64) {
+      s_cull[0][k] = a.bb.cull[2 * fi];
+      s_cull[1][k] = a.bb.cull[2 * fi + 1];
+    }
   };
   // the pixel origin of sub-list s (items mode)
   auto sub_x0 = [&](int s) { return NS == 1 ? t.WX0 : t.X0 + (s & 1) * 8; };
@@ -239,7 +243,14 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
         // face frame -> this sub-tile: columns shift by WX0 - span.x0, rows by the centre offset
         const float xo = (float)(ox - sp.x0);
         const float dref = ysb - px_cy(M, H, sp.y0);
-        const float4 cl = s_cull[0][k], ch = s_cull[1][k];
+        float4 cl, ch;
+        if constexpr (kF64) {
+          cl = a.bb.cull[2 * (lo + L.f[k])];
+          ch = a.bb.cull[2 * (lo + L.f[k]) + 1];
+        } else {
+          cl = s_cull[0][k];
+          ch = s_cull[1][k];
+        }
         const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {

@@ -1058,8 +1058,9 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_st(RasterFwdArgs<float>
 
 // The fp64 DIB-R forward in one launch: the pair raster (fp64 test, fp64-culled candidates, the
 // exact-depth winner of RasterPairsLDS<double>) and the fused soft mask per tile, as
-// kd_dibr_fwd_tiles does for fp32 (36 KB of LDS: four workgroups per CU).
-__global__ __launch_bounds__(kBlock, 4) void kd_dibr_fwd_tiles_f64(RasterFwdArgs<double> ra,
+// kd_dibr_fwd_tiles does for fp32 (the culling data read from global memory in pass A: 29 KB of
+// LDS, five workgroups per CU).
+__global__ __launch_bounds__(kBlock, 5) void kd_dibr_fwd_tiles_f64(RasterFwdArgs<double> ra,
                                                                  SoftArgs<double> a,
                                                                  SoftPairBuf<double> pb) {
   __shared__ DibrTileLDS<double> U;
