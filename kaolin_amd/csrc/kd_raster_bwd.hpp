@@ -95,9 +95,13 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
   T *grad_fvi = ra.grad_fvi;
   T *grad_feat = ra.grad_feat;
   constexpr int SMAX = 6 + 3 * DMAX;
+  // fp64: the table holds one pass of terms at a time -- the 6 geometry terms, then the 3 D
+  // feature terms -- so it is 20 KB instead of 32 and the kernel keeps five workgroups per CU
+  constexpr bool kSplit = sizeof(T) == 8;
+  constexpr int CW = kSplit ? (3 * DMAX > 6 ? 3 * DMAX : 6) : SMAX;  // table columns
   // odd row stride (in 4-byte words): a pixel's row write (lanes on different rows, one term)
   // and a slot's column sums (lanes on one row, consecutive terms) are both bank-conflict free
-  constexpr int SROW = (SMAX * (int)sizeof(T) / 4) % 2 ? SMAX : SMAX + 1;
+  constexpr int SROW = (CW * (int)sizeof(T) / 4) % 2 ? CW : CW + 1;
   constexpr int HT = kBlock;  // slots >= distinct faces of a tile
   __shared__ int s_key[HT];
   __shared__ int s_n[HT];  // pixels per slot (their ranks come from the counter)
@@ -152,43 +156,55 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
   const int pos = wg_compact(occ, s_cnt, nocc);
   if (occ) s_list[pos] = tid;
   __syncthreads();
-  // the pixel's terms go to its position in slot order, so a slot's terms are contiguous rows
-  if (h >= 0) {
-    const int ps = s_off[h] + rank;
+  // the pixel's terms go to its position in slot order, so a slot's terms are contiguous rows;
+  // pass q holds terms [c0, c1) (one pass of all S terms unless kSplit)
+  for (int q = 0; q < (kSplit ? 2 : 1); ++q) {
+    const int c0 = kSplit && q ? 6 : 0, c1 = kSplit && !q ? 6 : S;
+    if (q) __syncthreads();  // the previous pass's sums are done with the table
+    if (h >= 0) {
+      const int ps = s_off[h] + rank;
+      if (c0 == 0) {
 #pragma unroll
-    for (int j = 0; j < 6; ++j) s_con[ps][j] = c[j];
-#pragma unroll
-    for (int ii = 0; ii < 3; ++ii)
-#pragma unroll
-      for (int d = 0; d < DMAX; ++d)
-        if (d < D) s_con[ps][6 + ii * D + d] = c[6 + ii * DMAX + d];
-  }
-  __syncthreads();
-  // VTX: items 0..2 of a face are its corners (terms 2k, 2k+1 -> the corner's vertex)
-  const int SI = VTX ? S - 3 : S;
-  for (int idx = tid; idx < nocc * SI; idx += kBlock) {
-    const int i = idx / SI, j = idx - i * SI;
-    const int slot = s_list[i];
-    const int ns = s_n[slot];
-    const int o = s_off[slot];
-    const int64_t row = (int64_t)b * F + s_key[slot];
-    if (VTX && j < 3) {
-      T vx = (T)0, vy = (T)0;
-      for (int r = 0; r < ns; ++r) {  // independent reads: pipelined
-        vx += s_con[o + r][2 * j];
-        vy += s_con[o + r][2 * j + 1];
+        for (int j = 0; j < 6; ++j) s_con[ps][j] = c[j];
       }
-      vertex_add(ra.vo, row, j, vx, vy);
-      continue;
+      if (c1 > 6) {
+#pragma unroll
+        for (int ii = 0; ii < 3; ++ii)
+#pragma unroll
+          for (int d = 0; d < DMAX; ++d)
+            if (d < D) s_con[ps][6 + ii * D + d - c0] = c[6 + ii * DMAX + d];
+      }
     }
-    const int jj = VTX ? j + 3 : j;
-    T v = (T)0;
-    for (int r = 0; r < ns; ++r) v += s_con[o + r][jj];  // independent reads: pipelined
-    if (v == (T)0 || ablate(dbg, 128)) continue;
-    if (jj < 6)
-      atomicAdd(grad_fvi + row * 6 + jj, v);
-    else if (grad_feat)
-      atomicAdd(grad_feat + row * 3 * D + (jj - 6), v);
+    __syncthreads();
+    // items of the pass: VTX corners 0..2 of a face (terms 2k, 2k+1 -> the corner's vertex),
+    // then single terms g0..c1-1
+    const int ncorner = VTX && c0 == 0 ? 3 : 0;
+    const int g0 = ncorner ? 6 : c0;
+    const int SI = ncorner + (c1 - g0);
+    for (int idx = tid; idx < nocc * SI; idx += kBlock) {
+      const int i = idx / SI, j = idx - i * SI;
+      const int slot = s_list[i];
+      const int ns = s_n[slot];
+      const int o = s_off[slot];
+      const int64_t row = (int64_t)b * F + s_key[slot];
+      if (VTX && j < ncorner) {
+        T vx = (T)0, vy = (T)0;
+        for (int r = 0; r < ns; ++r) {  // independent reads: pipelined
+          vx += s_con[o + r][2 * j];
+          vy += s_con[o + r][2 * j + 1];
+        }
+        vertex_add(ra.vo, row, j, vx, vy);
+        continue;
+      }
+      const int jj = g0 + (j - ncorner);
+      T v = (T)0;
+      for (int r = 0; r < ns; ++r) v += s_con[o + r][jj - c0];  // independent reads: pipelined
+      if (v == (T)0 || ablate(dbg, 128)) continue;
+      if (jj < 6)
+        atomicAdd(grad_fvi + row * 6 + jj, v);
+      else if (grad_feat)
+        atomicAdd(grad_feat + row * 3 * D + (jj - 6), v);
+    }
   }
 }
 
