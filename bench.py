@@ -42,8 +42,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # (MI355X_MICROARCH.md issue-cost table: v_add_f32 / v_fma_f32 4 cycles) at the 2.4 GHz peak clock
 VALU_SIMDS, VALU_CYCLES, CLOCK_HZ = 1024, 4, 2.4e9
 
-# name -> (n_lon, n_lat, H, W, global batch, elevation); SURVEY.md §8(d) configs C2-C5
+# name -> (n_lon, n_lat, H, W, global batch, elevation); SURVEY.md §8(d) configs C1-C5 (C1: the
+# reference's CPU-runnable plumbing case, used by the CPU tests of the sharded step)
 CONFIGS = {
+    'c1': (25, 21, 128, 128, 1, 0.3),
     'c2': (100, 51, 256, 256, 4, 0.3),
     'c3': (250, 101, 512, 512, 8, 0.3),
     'c4': (250, 101, 1024, 1024, 8, 0.3),
@@ -204,24 +206,89 @@ def make_step(wl, use_graph):
 
 
 def timed(step, steps, warmup, dev, world):
+    """W untimed steps, then exactly K steps between barrier + synchronize on both sides; the
+    wall time is the max over ranks.  Each timed step is also bracketed by HIP events on the
+    current stream (the replay, and for a GraphedStep at N > 1 the all-reduce after it), so the
+    line carries the median step and the all-reduce's own time.  Returns (elapsed s, {'step_ms':
+    [...], 'allreduce_ms': [...] or None})."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    split = isinstance(step, distributed.GraphedStep) and world > 1
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
+    for e in ev:
+        e[0].record()
+        if split:
+            step.replay()
+            e[1].record()
+            step.exchange()
+        else:
+            step()
+        e[2].record()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = [e[0].elapsed_time(e[2]) for e in ev]
+    ar_ms = [e[1].elapsed_time(e[2]) for e in ev] if split else None
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed
+    return elapsed, {'step_ms': step_ms, 'allreduce_ms': ar_ms}
+
+
+def _median_over_ranks(xs, dev, world):
+    """The median of this rank's samples, max over the ranks (None without samples)."""
+    if not xs:
+        return None
+    m = statistics.median(xs)
+    if world > 1:
+        t = torch.tensor([m], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        m = float(t.item())
+    return m
+
+
+def kernel_map(wl, steps, use_graph, lists):
+    """Per-kernel durations from the library's HIP events on the launch stream: recorded while a
+    second copy of the step's graph is captured (the events are graph nodes) and read after each
+    of `steps` replays -- the launches the timed region runs, in the same back-to-back order.
+    Without a graph (or if the capture with events fails): eager launches of the step.
+    Returns ({name: (total ms, launches)}, source, face_idx)."""
+    if use_graph:
+        try:
+            _lib.profile_collect()
+            gs = distributed.GraphedStep(wl.params, wl.forward_backward, params_to_reduce=[],
+                                         capture_hook=_lib.profile_enable)
+            tot = {}
+            for _ in range(steps):
+                face_idx = gs.replay()
+                torch.cuda.synchronize()
+                for k, (ms, c) in _lib.profile_collect(keep=True).items():
+                    a, n = tot.get(k, (0.0, 0))
+                    tot[k] = (a + ms, n + c)
+            _lib.profile_collect()
+            del gs
+            if tot:
+                return tot, 'hip graph replays (library events captured as graph nodes)', face_idx
+        except Exception as e:  # noqa: BLE001 -- fall back to eager launches
+            _lib.profile_enable(False)
+            _lib.profile_collect()
+            torch.cuda.synchronize()
+            print(f'[bench] graph event capture failed ({type(e).__name__}: {e}); eager map',
+                  file=sys.stderr)
+    with dibr.close_lists(lists):
+        _lib.profile_enable(True)
+        for _ in range(steps):
+            face_idx = wl.eager_step()
+        torch.cuda.synchronize()
+        _lib.profile_enable(False)
+    return _lib.profile_collect(), 'eager launches', face_idx
 
 
 def load_pmc(path, config, dtype, lists, views):
@@ -291,8 +358,11 @@ def main():
     with dibr.close_lists(args.lists):
         wl = Workload(args, dev, first, n, total)
         step, launch = make_step(wl, use_graph)
-        elapsed = timed(step, args.steps, args.warmup, dev, world)
+        graphed = isinstance(step, distributed.GraphedStep)
+        elapsed, evt = timed(step, args.steps, args.warmup, dev, world)
     ms_per_step = elapsed * 1e3 / args.steps
+    step_median = _median_over_ranks(evt['step_ms'], dev, world)
+    ar_median = _median_over_ranks(evt['allreduce_ms'], dev, world) if world > 1 else None
     H, W = wl.H, wl.W
     pixels = total * H * W
     value = pixels * args.steps / elapsed / 1e6
@@ -303,20 +373,14 @@ def main():
         with dibr.close_lists(args.lists):
             wl2 = Workload(args, dev, rank * B_global, B_global, B_global * world)
             step2, _ = make_step(wl2, use_graph)
-            el2 = timed(step2, args.steps, args.warmup, dev, world)
+            el2, _ = timed(step2, args.steps, args.warmup, dev, world)
         weak = {'value': round(B_global * world * H * W * args.steps / el2 / 1e6, 2),
                 'ms_per_step': round(el2 * 1e3 / args.steps, 4), 'views_per_gpu': B_global,
                 'global_batch': B_global * world}
         del step2, wl2
 
-    # ---- per-kernel durations: HIP events recorded on the launch stream, eager pass ---------
-    with dibr.close_lists(args.lists):
-        _lib.profile_enable(True)
-        for _ in range(args.steps):
-            face_idx = wl.eager_step()
-        torch.cuda.synchronize(dev)
-        _lib.profile_enable(False)
-    prof = _lib.profile_collect()
+    # ---- per-kernel durations: HIP events on the launch stream, over graph replays ---------
+    prof, prof_src, face_idx = kernel_map(wl, args.steps, graphed, args.lists)
     covered = int((face_idx >= 0).sum().item())
 
     fvz, fvi, nz = wl.inputs()
@@ -416,6 +480,12 @@ def main():
     out = {
         'metric': METRIC, 'value': round(value, 2), 'unit': 'Mpixels/s', 'n_gpus': world,
         'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms_per_step, 4),
+        'ms_per_step_median': None if step_median is None else round(step_median, 4),
+        'allreduce_us': None if ar_median is None else round(ar_median * 1e3, 2),
+        'timing': 'value and ms_per_step: K steps between barrier + synchronize, wall clock, max '
+                  'over ranks; ms_per_step_median: median of the per-step HIP event times (max '
+                  'over ranks); allreduce_us: median per-step time of the RCCL all-reduce after '
+                  'the graph replay (N > 1)',
         'higher_is_better': True, 'scaling': 'weak' if weak_main else 'strong',
         'vs_baseline': None, 'dtype': args.dtype,
         'data': 'synthetic (seeded ' + ('triangle soup' if soup else 'uv-sphere, orbit cameras')
@@ -438,6 +508,7 @@ def main():
         'weak_scaling': weak,
         'cpu_baseline': cpu,
         'kernels': kernels,
+        'kernels_source': prof_src,
     }
     if rank == 0:
         print(json.dumps(out))

@@ -53,13 +53,29 @@ int kd_version(void);
  * kd_profile_kernel_name(id) names them.  Not for use under stream capture. */
 void kd_profile_enable(int on);
 int kd_profile_collect(double *total_ms, int64_t *launches, int n);
+/* The same; keep != 0 leaves the recorded events in place (events recorded while a HIP graph
+ * was captured are graph nodes: read them again after every replay, then once with keep = 0). */
+int kd_profile_collect_keep(double *total_ms, int64_t *launches, int n, int keep);
 const char *kd_profile_kernel_name(int id);
 
-/* Diagnostics only: ablation switches read by the kernels (0 = production), and (flag 64) a
- * device int64 array of 3 * views * tiles entries receiving per-tile durations (100 MHz ticks)
- * of the raster forward / soft forward / soft backward tile kernels. */
+/* Diagnostics only: ablation switches read by the kernels of the diagnostic build
+ * (libkaolin_dibr_diag.so), and (flag 64) a device int64 array of 3 * views * tiles entries
+ * receiving per-tile durations (100 MHz ticks) of the raster forward / soft forward / soft
+ * backward tile kernels.  The production library reads no flags: kd_debug_set returns
+ * KD_ERR_INVALID_ARGUMENT there for any nonzero value. */
 int kd_debug_set(int flags);
 int kd_debug_buffer(void *device_ptr);
+
+/* Launch forms (a test hook; 0 by default).  dibr_rasterization's forward and backward run as one
+ * launch each; the same tile bodies also run as separate launches, which other entry points use
+ * (the op forms, knum > 32, D > 3).  A test sets these bits to run dibr_rasterization through the
+ * separate launches and compare.  Bits: KD_FORM_SPLIT_FWD raster then soft mask as two launches,
+ * KD_FORM_SPLIT_BWD the two backwards as two launches, KD_FORM_SOFT_SPLIT the soft mask's pass A,
+ * pair math and product as three launches (the K-list pipeline without the lists). */
+#define KD_FORM_SPLIT_FWD 1
+#define KD_FORM_SPLIT_BWD 2
+#define KD_FORM_SOFT_SPLIT 4
+int kd_set_test_forms(int forms);
 
 /* Pool limits (a test and tuning hook; both 1 by default).  The workspaces hold two bounded
  * pools whose layout depends only on the call's sizes: the coarse bins (16 entries per face row)
@@ -476,11 +492,6 @@ int kd_rast_interpolate_f64(int batch, int height, int width, int64_t num_faces,
  * (B, F, 3, D) (NULL: skipped).
  * ------------------------------------------------------------------------------------------- */
 size_t kd_deftet_workspace_size(int batch, int64_t num_faces, int double_precision);
-/* The same plus the pixel sort of the cell-major forward (knum <= 32): a forward given at least
- * this many bytes runs the cell-major kernels; with kd_deftet_workspace_size's bytes it runs the
- * per-pixel kernel (same results). */
-size_t kd_deftet_workspace_size_p(int batch, int64_t num_pixels, int64_t num_faces,
-                                  int double_precision);
 int kd_deftet_sparse_render_forward_f32(int batch, int64_t num_pixels, int64_t num_faces,
                                         int knum, int feat_dim, const float *pixel_coords,
                                         const float *render_ranges, const float *fvz,

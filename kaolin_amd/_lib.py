@@ -109,8 +109,6 @@ def load():
             lib.kd_mask_iou_workspace_size.restype = c_size
             lib.kd_deftet_workspace_size.argtypes = [c_int, c_i64, c_int]
             lib.kd_deftet_workspace_size.restype = c_size
-            lib.kd_deftet_workspace_size_p.argtypes = [c_int, c_i64, c_i64, c_int]
-            lib.kd_deftet_workspace_size_p.restype = c_size
             lib.kd_texture_mapping_backward_workspace_size.argtypes = [c_int, c_i64, c_int, c_int,
                                                                        c_int]
             lib.kd_texture_mapping_backward_workspace_size.restype = c_size
@@ -121,6 +119,8 @@ def load():
             lib.kd_profile_enable.restype = None
             lib.kd_profile_collect.argtypes = [c_p, c_p, c_int]
             lib.kd_profile_collect.restype = c_int
+            lib.kd_profile_collect_keep.argtypes = [c_p, c_p, c_int, c_int]
+            lib.kd_profile_collect_keep.restype = c_int
             lib.kd_profile_kernel_name.argtypes = [c_int]
             lib.kd_profile_kernel_name.restype = ctypes.c_char_p
             lib.kd_debug_set.argtypes = [c_int]
@@ -129,10 +129,12 @@ def load():
             lib.kd_debug_buffer.restype = c_int
             lib.kd_set_pool_limits.argtypes = [ctypes.c_double, ctypes.c_double]
             lib.kd_set_pool_limits.restype = c_int
+            lib.kd_set_test_forms.argtypes = [c_int]
+            lib.kd_set_test_forms.restype = c_int
             lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
             lib.kd_prepare_vertices_ranges.restype = c_i64
-            # diagnostics only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
-            if os.environ.get('KD_DEBUG_FLAGS'):
+            # diagnostic build only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
+            if os.environ.get('KD_DEBUG_FLAGS') and LIB_PATH.endswith('_diag.so'):
                 lib.kd_debug_set(int(os.environ['KD_DEBUG_FLAGS'], 0))
             for base, sig in _SIGS.items():
                 for sfx in ('f32', 'f64'):
@@ -175,6 +177,16 @@ def set_pool_limits(bins=1.0, pairs=1.0):
 
 _pool_limited = False
 
+# kd_set_test_forms bits (include/kaolin_dibr.h KD_FORM_*)
+FORM_SPLIT_FWD, FORM_SPLIT_BWD, FORM_SOFT_SPLIT = 1, 2, 4
+
+
+def set_test_forms(forms=0):
+    """Run dibr_rasterization through the separate launches its one-launch kernels fuse
+    (kd_set_test_forms, a test hook); 0 restores the default."""
+    if load().kd_set_test_forms(int(forms)) != KD_OK:
+        raise RuntimeError(load().kd_last_error().decode(errors='replace'))
+
 
 def pool_limits_active():
     """True while set_pool_limits holds a pool below its full size (the test hook)."""
@@ -192,13 +204,15 @@ def profile_enable(on=True):
     load().kd_profile_enable(1 if on else 0)
 
 
-def profile_collect():
-    """{kernel name: (total ms, launches)} for the launches recorded since the last collect."""
+def profile_collect(keep=False):
+    """{kernel name: (total ms, launches)} for the launches recorded since the last collect
+    (keep: leave the events for another read -- those of a captured graph, after each replay)."""
     lib = load()
     n = 32
     ms = (ctypes.c_double * n)()
     cnt = (ctypes.c_int64 * n)()
-    k = lib.kd_profile_collect(ctypes.cast(ms, c_p), ctypes.cast(cnt, c_p), n)
+    k = lib.kd_profile_collect_keep(ctypes.cast(ms, c_p), ctypes.cast(cnt, c_p), n,
+                                    1 if keep else 0)
     return {lib.kd_profile_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(k) if cnt[i]}
 
 

@@ -413,11 +413,16 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
   {
     ProfScope prof(K_BIN_COUNT, stream);
     const dim3 grid_s(bb.nchunk, fs.B, 1);
-    if (shared && two)
-      hipLaunchKernelGGL((kd_bin_count<T, 2, 2>), grid_s, dim3(kBlock), 0, stream, jobs);
-    else if (shared)
-      hipLaunchKernelGGL((kd_bin_count<T, 1, 2>), grid_s, dim3(kBlock), 0, stream, jobs);
-    else if (two)
+    bool done = false;
+    if constexpr (KD_DIAG) {
+      if (shared && two)
+        hipLaunchKernelGGL((kd_bin_count<T, 2, 2>), grid_s, dim3(kBlock), 0, stream, jobs);
+      else if (shared)
+        hipLaunchKernelGGL((kd_bin_count<T, 1, 2>), grid_s, dim3(kBlock), 0, stream, jobs);
+      done = shared;
+    }
+    if (done) {
+    } else if (two)
       hipLaunchKernelGGL((kd_bin_count<T, 2, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
     else
       hipLaunchKernelGGL((kd_bin_count<T, 1, 1>), grid_c, dim3(kBlock), 0, stream, jobs);

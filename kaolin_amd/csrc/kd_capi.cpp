@@ -14,7 +14,11 @@ char *error_buffer() {
 }
 
 std::atomic<int> g_debug{0};
+#if KD_DIAG
 int debug_flags() { return g_debug.load(); }
+#endif
+std::atomic<int> g_forms{0};
+int test_forms() { return g_forms.load(); }
 std::atomic<long long *> g_tbuf{nullptr};
 std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
 float pool_limit_bins() { return g_lim_bins.load(); }
@@ -78,7 +82,16 @@ int kd_version(void) { return 1; }
 void kd_profile_enable(int on) { kd::g_prof.store(on != 0); }
 
 int kd_debug_set(int flags) {
+  if (!KD_DIAG && flags != 0)
+    return kd::set_error(KD_ERR_INVALID_ARGUMENT, "debug flags: diagnostic build only");
   kd::g_debug.store(flags);
+  return KD_OK;
+}
+
+int kd_set_test_forms(int forms) {
+  if (forms & ~(KD_FORM_SPLIT_FWD | KD_FORM_SPLIT_BWD | KD_FORM_SOFT_SPLIT))
+    return kd::set_error(KD_ERR_INVALID_ARGUMENT, "unknown launch form bits 0x%x", forms);
+  kd::g_forms.store(forms);
   return KD_OK;
 }
 
@@ -96,11 +109,14 @@ int kd_debug_buffer(void *device_ptr) {
   return KD_OK;
 }
 
-int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
+int kd_profile_collect_keep(double *total_ms, int64_t *launches, int n, int keep) {
   std::vector<kd::Rec> recs;
   {
     std::lock_guard<std::mutex> lk(kd::g_prof_mu);
-    recs.swap(kd::g_recs);
+    if (keep)
+      recs = kd::g_recs;
+    else
+      recs.swap(kd::g_recs);
   }
   for (auto &r : recs) {
     float ms = 0.f;
@@ -109,10 +125,16 @@ int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
       if (total_ms) total_ms[r.id] += ms;
       if (launches) launches[r.id] += 1;
     }
-    (void)hipEventDestroy(r.start);
-    (void)hipEventDestroy(r.stop);
+    if (!keep) {
+      (void)hipEventDestroy(r.start);
+      (void)hipEventDestroy(r.stop);
+    }
   }
   return kd::K_NUM_KERNELS;
+}
+
+int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
+  return kd_profile_collect_keep(total_ms, launches, n, 0);
 }
 
 const char *kd_profile_kernel_name(int id) {

@@ -23,22 +23,29 @@ namespace kd {
 #endif
 __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG && (flags & bit); }
 
-// Diagnostic ablation switches (kd_debug_set, copied into FaceSet::dbg; diagnostic build only).
+// Diagnostic ablation switches (kd_debug_set, copied into FaceSet::dbg; diagnostic build only:
+// the production library's debug_flags() is the constant 0, so no host path there selects a kernel
+// from them).
 // Bits: 1 skip the per-pixel face tests of the forward kernels, 2 skip staging face data,
 //       4 skip the per-batch work entirely (bin walk only), 8 fp32 raster: lane-per-pixel
 //       kernel instead of the pair pipeline, 16 / 32 skip the per-pair pass of the fp32
 //       raster / soft mask, 64 record per-tile durations into the kd_debug_buffer array,
 //       8192 skip the fp32 raster's per-pixel epilogue (winner reload, output writes),
 //       32 also skips the fused soft mask's pair math (kd_softpair.hip soft_pairs_tile),
-//       1 << 27 (production too) enables the small-batch forward (kd_soft.hpp dibr_small_batch),
-//       1 << 28 (production too) the balanced (item-dealing) fused forward tiles,
 //       1 << 18 / 1 << 19 skip kd_bin_count's cull coefficients / its LDS tile counts,
 //       1 << 16 / 1 << 23 kd_soft_lists: skip every list store / the index and type stores (the
 //       host presets the indices to -1 so that the backward reads no garbage),
-//       1024 / 2048 (production too) DefTet forward: the cell-major / the pooled kernel instead
-//       of the per-pixel waves,
+//       1 << 20 256-face binning chunks, 1 << 21 one count workgroup for both face sets,
+//       1 << 29 the lane-per-pixel K-list backward,
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
+#if KD_DIAG
 int debug_flags();
+#else
+constexpr int debug_flags() { return 0; }
+#endif
+// kd_set_test_forms (KD_FORM_* of kaolin_dibr.h): run dibr_rasterization through the separate
+// launches its one-launch kernels fuse (a test hook of both builds)
+int test_forms();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
 
 // Per-workgroup duration (wall clock, 100 MHz ticks) for diagnostics: written by thread 0 when
@@ -67,7 +74,6 @@ constexpr int kBlock = 256;      // 4 waves
 constexpr int kTile = 16;        // fine tile: 16x16 pixels per workgroup, 8x8 per wave
 constexpr int kChunk = 512;      // faces per binning workgroup (two per thread) ...
 // ... or one per thread when the batch is small, so the binning grids still fill the chip
-int debug_flags();
 inline int bin_chunk(int B, int64_t max_per_view) {  // (debug flag 1 << 20: always 256)
   return (int64_t)B * ((max_per_view + kChunk - 1) / kChunk) < 256 || (debug_flags() & (1 << 20))
              ? kChunk / 2

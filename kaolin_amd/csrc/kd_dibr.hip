@@ -23,9 +23,7 @@ namespace kd {
 
 size_t dibr_workspace_bytes(int B, int H, int W, int64_t F, int K, int esize) {
   const int64_t N = (int64_t)B * F;
-  const int ct0 = dibr_ct0(B, H, W, esize);
-  return bin_workspace_bytes(B, H, W, N, F, ct0) +
-         soft_pair_workspace_bytes(B, H, W, N, F, K, esize, ct0);
+  return bin_workspace_bytes(B, H, W, N, F) + soft_pair_workspace_bytes(B, H, W, N, F, K, esize);
 }
 
 template <typename T>
@@ -38,11 +36,10 @@ struct DibrBuffers {
 template <typename T>
 static DibrBuffers<T> dibr_carve(void *ws, int B, int H, int W, int64_t F, int K) {
   const int64_t N = (int64_t)B * F;
-  const int ct0 = dibr_ct0(B, H, W, sizeof(T));
   DibrBuffers<T> d;
   size_t off = 0;
-  d.rbb = bin_carve(ws, off, B, H, W, N, F, ct0);
-  d.sbb = bin_carve(ws, off, B, H, W, N, F, ct0);  // soft_pair_workspace_bytes starts with these
+  d.rbb = bin_carve(ws, off, B, H, W, N, F);
+  d.sbb = bin_carve(ws, off, B, H, W, N, F);  // soft_pair_workspace_bytes starts with these
   d.pb = soft_pair_carve<T>(ws, off, B, H, W, K);
   return d;
 }
@@ -94,7 +91,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   KD_CHECK_ARG(!iou.gt || (iou.loss && iou.stats && iou.acc), "mask_iou: NULL output");
   KD_CHECK_ARG(!iou.gt || (K <= kFuseSlots && pool_limit_pairs() >= 1.f &&
-                            !(debug_flags() & 4096)),
+                            !(test_forms() & KD_FORM_SOFT_SPLIT)),
                "fused mask_iou needs knum <= 32 (the one-launch soft mask)");
   const int64_t nf = (int64_t)B * F;
   if (!want_grad) gz_fvi = gz_feat = nullptr;
@@ -117,8 +114,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   d.rbb.cull_eps = eps;
   d.sbb.cull = nullptr;
   d.sbb.clear = d.pb.counters;
-  // the counters (and, when helper workgroups are requested, their jobs / FIFOs)
-  d.sbb.n_clear = (debug_flags() & (256 | 512)) ? kHelpClear : kPairClear;
+  d.sbb.n_clear = kPairClear;  // the pair pipeline's counters and record cursor
   if (iou.gt) {  // the IoU accumulators start at zero (kd_bin_count)
     d.sbb.clear_b = (int *)iou.acc;
     d.sbb.n_clear_b = 4 * kIouParts * B;
@@ -190,7 +186,7 @@ static int dibr_bwd(int B, int H, int W, int64_t F, int D, const T *grad_interp,
     sa.iou_stats = iou.stats;
     sa.iou_grad = iou.grad;
     sa.iou_B = B;
-    if (grad_interp && D <= 3 && !(debug_flags() & (1 << 24))) {
+    if (grad_interp && D <= 3 && !(test_forms() & KD_FORM_SPLIT_BWD)) {
       // both backwards in one launch (kd_dibr_bwd)
       const RasterBwdArgs<T> ra{B,   H,    W,   F,    D,     grad_interp, face_idx,
                                 weights, fvi, feat, eps, gfvi, gfeat, debug_flags()};

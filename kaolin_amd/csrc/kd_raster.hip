@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void kd_raster_bwd_tile(RasterBwdArgs<T> ra
 // the pair pipeline with edge culling (fp32 and fp64; debug flag 8: the lane-per-pixel kernel)
 template <typename T>
 bool raster_uses_cull() {
-  return !(debug_flags() & 8);
+  return !(KD_DIAG != 0 && (debug_flags() & 8) != 0);
 }
 
 template <typename T>
@@ -196,7 +196,7 @@ int raster_launch(RasterFwdArgs<T> &a, hipStream_t stream) {
     ProfScope prof(K_RASTER_FWD, stream);
     if (a.bb.cull)
       hipLaunchKernelGGL(kd_raster_fwd_pairs<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
-    else
+    else if constexpr (KD_DIAG)  // (diagnostic flag 8: the lane-per-pixel kernel)
       hipLaunchKernelGGL(kd_raster_fwd<T>, dim3(ntiles, fs.B), dim3(kBlock), 0, stream, a);
   }
   const hipError_t e = hipGetLastError();

@@ -103,20 +103,12 @@ struct RasterPairsLDS {
 };
 
 // Tile tl of view b (nbin: faces of its coarse bin, or -1).  Each thread owns pixel
-// (t.px, t.py) of tile_geom(H, W, tl) and writes its outputs.
-// BAL (balanced): the (sub-tile, 64-face chunk) items of every batch -- the four sub-lists' chunks
-// -- are dealt to the four waves in turn, so a sub-tile whose list is long (the pole, a dense
-// silhouette) is tested by all four waves; the pairs carry their sub-tile and the winners meet in
-// its LDS key row.  Without BAL each wave tests its own sub-tile's chunks.
-// ST (small-batch mode, kd_dibr_fwd_st): the workgroup covers quadrant `quad` of the tile only
-// (tile_geom_st); its four waves share the quadrant's 64 pixels and its one list (every wave built
-// the same sub-list), the chunks dealt as with BAL, and wave 0 writes the outputs.
-template <typename T, bool ST = false, bool BAL = false>
+// (t.px, t.py) of tile_geom(H, W, tl) and writes its outputs; wave w tests its own sub-tile's
+// 64-face chunks.
+template <typename T>
 __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int b, int tl,
-                                                  int nbin, RasterPairsLDS<T> &S, int quad = 0) {
+                                                  int nbin, RasterPairsLDS<T> &S) {
   constexpr bool kF64 = sizeof(T) == 8;
-  constexpr bool kItems = ST || BAL;  // chunks dealt to the waves as (sub-tile, chunk) items
-  constexpr int NS = ST ? 1 : 4;       // sub-lists of the workgroup
   TileLists &L = S.L;
   auto &s_geo = S.geo;
   auto &s_cull = S.cull;
@@ -129,11 +121,11 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  TileGeom t = ST ? tile_geom_st(H, W, tl, quad) : tile_geom(H, W, tl);
+  TileGeom t = tile_geom(H, W, tl);
   t.nbin = nbin;
-  const int kw = ST ? 0 : w;  // LDS key row of this wave's pixels
+  const int kw = w;  // LDS key row of this wave's pixels
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
-  if (!ST || w == 0) {  // (the walk's first barrier orders these before any pass B)
+  {  // (the walk's first barrier orders these before any pass B)
     s_key[kw][lane] = 0ull;
     if (kF64) S.zx[kF64 ? kw : 0][lane] = 0ull;
     if (lane == 0) s_nan[kw] = 0ull;
@@ -159,9 +151,6 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
       s_cull[1][k] = a.bb.cull[2 * fi + 1];
     }
   };
-  // the pixel origin of sub-list s (items mode)
-  auto sub_x0 = [&](int s) { return NS == 1 ? t.WX0 : t.X0 + (s & 1) * 8; };
-  auto sub_y0 = [&](int s) { return NS == 1 ? t.WY0 : t.Y0 + (s >> 1) * 8; };
   // B: the reference's per-pixel test (rasterization_cuda.cu:131-162) over the current batch
   auto test_batch = [&](int total) {
     if (ablate(fs.dbg, 16)) return;
@@ -169,12 +158,10 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     for (int e0 = 0; e0 < total; e0 += kWave) {
       const int e = e0 + lane;
       if (e < total) {
-        const int pr = s_pair[w][e];
-        // pair: (sub-list << 14) | (pixel << 8) | entry (items mode); (pixel << 8) | entry
-        const int ps = kItems ? (NS == 1 ? 0 : pr >> 14) : w;
-        const int q = (pr >> 8) & 63, k = L.sub[ps][pr & 255];
-        const int ox = kItems ? sub_x0(ps) : t.WX0, oy = kItems ? sub_y0(ps) : t.WY0;
-        const int krow = kItems ? ps : kw;
+        const int pr = s_pair[w][e];  // pair: (pixel << 8) | entry
+        const int q = (pr >> 8) & 63, k = L.sub[w][pr & 255];
+        const int ox = t.WX0, oy = t.WY0;
+        const int krow = kw;
         const float x0 = sx * (float)(2 * (ox + (q & 7)) + 1 - W);
         const float y0 = sy * (float)(H - 2 * (oy + (q >> 3)) - 1);
         T w0, w1, w2, z0;
@@ -203,35 +190,15 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   };
   auto round = [&](int nsub, int) {
     if (ablate(fs.dbg, 1)) return;
-    if (!kItems && nsub == 0) return;
+    if (nsub == 0) return;
     int total = 0;
-    // items mode: item i = (sub-list s, chunk c) in sub-list order, wave w takes i = w, w + 4, ...
-    int nci[4] = {0, 0, 0, 0}, nitems = 0;
-    if (kItems) {
-#pragma unroll
-      for (int s = 0; s < NS; ++s) {
-        nci[s] = (L.nsub[s] + kWave - 1) / kWave;
-        nitems += nci[s];
-      }
-    }
 #pragma unroll 1
-    for (int it = kItems ? w : 0; kItems ? it < nitems : it < 4; it += kItems ? 4 : 1) {
-      int s = w, c = it;
-      if (kItems) {
-        s = 0;  // (unrolled: nci stays in registers)
-#pragma unroll
-        for (int q = 0; q < NS - 1; ++q)
-          if (s == q && c >= nci[q]) {
-            c -= nci[q];
-            s = q + 1;
-          }
-      } else if (c * kWave >= nsub) {
-        break;
-      }
-      const int ls = NS == 1 ? 0 : s;  // the sub-list (ST: every wave built the same one)
-      const int ns = kItems ? L.nsub[ls] : nsub;
-      const int ox = kItems ? sub_x0(s) : t.WX0, oy = kItems ? sub_y0(s) : t.WY0;
-      const float ysb = kItems ? px_cy(M, H, oy) : ysub;
+    for (int c = 0; c < 4; ++c) {
+      if (c * kWave >= nsub) break;
+      const int ls = w;
+      const int ns = nsub;
+      const int ox = t.WX0, oy = t.WY0;
+      const float ysb = ysub;
       // A: lane = face (chunk entry c*64 + lane): culled row intervals -> 64-bit pixel mask
       const int j = c * kWave + lane;
       uint64_t fm = 0ull;
@@ -254,8 +221,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
         const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
 #pragma unroll
         for (int r = 0; r < 8; ++r) {
-          // (items mode: the item's sub-tile's row offsets)
-          const float d = (kItems ? px_cy(M, H, oy + r) - ysb : drow[r]) + dref;
+          const float d = drow[r] + dref;
           const float plo = fmaxf(fmaf(cl.y, d, l0), fmaf(cl.w, d, l2)) - kSlack;
           const float phi = fminf(fmaf(ch.y, d, h0), fmaf(ch.w, d, h2)) + kSlack;
           const int xs = max((int)ceilf(__builtin_amdgcn_fmed3f(plo, -1.f, 9.f)), rx0);
@@ -271,7 +237,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
       const int incl = wave_incl_scan(cnt);
       int end_tot = total + __builtin_amdgcn_readlane(incl, 63);
       int pos = total + incl - cnt;
-      const int qbits = (kItems && NS > 1 ? (s << 14) : 0) | (lane << 8) | (c << 6);
+      const int qbits = (lane << 8) | (c << 6);
       while (true) {
         while (m && pos < kRasterPairCap) {
           s_pair[w][pos++] = (unsigned short)(qbits | (int)__builtin_ctzll(m));
@@ -288,7 +254,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   };
   tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
 
-  if (!t.inimg || (ST && w != 0) || ablate(fs.dbg, 8192)) return;
+  if (!t.inimg || ablate(fs.dbg, 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
   int best = -1;

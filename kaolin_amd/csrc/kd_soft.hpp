@@ -213,41 +213,6 @@ struct PairItem {
 // under kd_set_pool_limits) a tile whose reservation does not fit computes its soft mask without
 // records (`ovf` list, kd_soft_ovf_fwd) and its backward recomputes the pairs
 // (kd_soft_ovf_bwd).
-// Helper workgroups of the fused fp32 forward (kd_dibr_fwd_help, kd_softpair.hip).  A silhouette
-// tile's pair math (one workgroup: ~20 us of issue-bound fp64 arithmetic for ~5000 records) is
-// the tail of the forward -- at one view its whole length.  A tile with more than kHelpMin
-// records publishes a job: its records in chunks of kHelpChunk, claimed with a device atomic by
-// the owner itself and by helper workgroups launched after the tiles.  Jobs stay on the owner's
-// XCD (a FIFO of job entries per XCD): owner and helpers share one L2, so the records and
-// probabilities need no device-scope cache write-back / invalidation (those fences, measured,
-// cost more than the whole forward), only stores completed before the atomics that publish them.
-// The owner waits only for chunks a running workgroup has claimed; tiles never wait for anything
-// before their pair math, so every helper's exit condition (every tile past pass A, its FIFO
-// drained) is reached.
-struct HelpJob {
-  unsigned long long word;  // n << 32 | (tile + 1); 0 until published
-  int claim;                // chunks claimed
-  int done;                 // chunks finished by helpers
-  int pad[12];              // one job per 64-byte line (its claims are contended)
-};
-static_assert(sizeof(HelpJob) == 64, "HelpJob: 64 bytes (16 ints of the counters region)");
-constexpr int kHelpMin = 1024;    // records of a tile that publishes a job
-constexpr int kHelpChunk = 512;   // records per claimed chunk
-constexpr int kHelpFan = 8;       // FIFO entries (helpers invited) per job, at most
-constexpr int kHelpJobs = 256;
-constexpr int kHelpXcds = 8;      // FIFOs (XCC_ID & 7)
-constexpr int kHelpFifoX = 256;   // entries per FIFO
-constexpr int kHelpers = 64;      // helper workgroups per launch, at most
-// SoftPairBuf::counters: [0..5] as below; the helpers' shared words each on its own 128-byte
-// line (away from the tiles' item counters): [kHelpPassed] tiles past pass A, [kHelpNJobs] jobs
-// reserved, [kHelpTail + 32 x] / [kHelpHead + 32 x] tail / head of XCD x's FIFO; then the jobs
-// and the FIFOs (ints zeroed by kd_bin_count: kHelpClear)
-constexpr int kHelpPassed = 32, kHelpNJobs = 64, kHelpTail = 96;
-constexpr int kHelpHead = kHelpTail + 32 * kHelpXcds;
-constexpr int kHelpJobsAt = kHelpHead + 32 * kHelpXcds;
-constexpr int kHelpFifoAt = kHelpJobsAt + 16 * kHelpJobs;
-constexpr int kHelpClear = kHelpFifoAt + kHelpXcds * kHelpFifoX;
-
 template <typename T>
 struct SoftPairBuf {
   SoftPairRec *rec;    // [cap]
@@ -255,15 +220,12 @@ struct SoftPairBuf {
   int64_t *tbase;      // [tiles] first record of each tile
   int32_t *npix;       // [P] close faces of each uncovered pixel (split pipeline)
   int32_t *ntile;      // [tiles] records of each tile
-  PairItem *items;     // [cap / 256 + 4 tiles]
+  PairItem *items;     // [cap / 256 + tiles]
   int32_t *tiles;      // [tiles] tiles with records (split pipeline's reduce)
-  int32_t *ovf;        // [4 tiles] tiles (small batch: 4 tile + quadrant) that computed their soft mask without records
-  int32_t *counters;   // [4]: items, tiles with records, overflow tiles, small-batch flag (1: the
-                       // forward ran kd_dibr_fwd_st, overflow entries are 4 tile + quadrant); then the 64-bit
+  int32_t *ovf;        // [tiles] tiles that computed their soft mask without records
+  int32_t *counters;   // [4]: items, tiles with records, overflow tiles, (unused); then the 64-bit
                        // record cursor (all zeroed by kd_bin_count: n_clear = 6)
   unsigned long long *cursor;
-  HelpJob *jobs;       // [kHelpJobs] (after the counters; see kHelpClear)
-  int32_t *fifo;       // [kHelpFifo] job + 1 per entry, 0 until written
   int64_t ntiles, npixels, cap, lim;  // lim: records a forward may use (kd_set_pool_limits)
   int fixed;  // knum <= 32 and the whole pool usable: tile t owns records [t * 256 K, +256 K)
   int ntx;
@@ -285,23 +247,6 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
 // the backward over the records of soft_pairs_launch(grad = true), adding into a.grad_fvi
 template <typename T>
 int soft_pairs_backward_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream);
-// Small-batch mode of dibr_rasterization (fp32): few enough 16x16 tiles that the tile grid is
-// about one round of workgroup slots -- the forward then runs one workgroup per 8x8 quadrant over
-// 16-pixel coarse bins (kd_dibr_fwd_st).  A function of the call's sizes and the debug flags
-// only, so the forward and the backward carve the same workspace.  Measured at C3 (1 / 2 views,
-// rocprof + bench, same box): forward 60 / 96 us against 67 / 73 for the tile kernel, but the
-// 16-px bins cost 12 us more binning -- the step is no faster (0.126 vs 0.119 ms at 1 view; with
-// 32-px bins, debug flag 1 << 30, 0.118), so it runs only on request (debug flag 1 << 27).
-constexpr int64_t kSmallBatchTiles = 2048;  // B x 16x16 tiles
-inline bool dibr_small_batch(int B, int H, int W, int esize) {
-  const int64_t tiles = (int64_t)B * ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-  return esize == 4 && tiles > 0 && tiles <= kSmallBatchTiles && (debug_flags() & (1 << 27));
-}
-// its coarse bins: 16 px (each quadrant walks a quarter of a 32-px bin's area); debug flag
-// 1 << 30 keeps 32 px (A/B)
-inline int dibr_ct0(int B, int H, int W, int esize) {
-  return dibr_small_batch(B, H, W, esize) && !(debug_flags() & (1 << 30)) ? kTile : kCoarseTile0;
-}
 // The raster forward (fp32 pair pipeline) and the fused soft mask in one launch, when both apply.
 template <typename T>
 struct RasterFwdArgs;

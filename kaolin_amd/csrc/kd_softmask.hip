@@ -331,11 +331,15 @@ int soft_backward(int B, int H, int W, int64_t F, int K, const T *grad_soft, con
     const int64_t tiles = (int64_t)B * ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     const unsigned grid = (unsigned)(blocks < 8192 ? blocks : 8192);
     const unsigned tgrid = (unsigned)(tiles < 8192 ? tiles : 8192);
-    if (debug_flags() & (1 << 29))  // diagnostics: the lane-per-pixel form
-      hipLaunchKernelGGL(kd_soft_bwd_atomic<T>, dim3(grid), dim3(kBlock), 0, stream, B, H, W, F,
-                         K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
-                         grad_fvi);
-    else
+    bool atomic_form = false;  // diagnostics: the lane-per-pixel form (flag 1 << 29)
+    if constexpr (KD_DIAG) {
+      atomic_form = (debug_flags() & (1 << 29)) != 0;
+      if (atomic_form)
+        hipLaunchKernelGGL(kd_soft_bwd_atomic<T>, dim3(grid), dim3(kBlock), 0, stream, B, H, W,
+                           F, K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
+                           grad_fvi);
+    }
+    if (!atomic_form)
       hipLaunchKernelGGL(kd_soft_bwd_lists<T>, dim3(tgrid), dim3(kBlock), 0, stream, B, H, W, F,
                          K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
                          grad_fvi, debug_flags());

@@ -61,12 +61,11 @@ size_t soft_pair_workspace_bytes(int B, int H, int W, int64_t N, int64_t F, int 
   s += align_up(sizeof(int64_t) * (size_t)tiles);
   s += align_up(sizeof(int32_t) * (size_t)P);
   s += align_up(sizeof(int32_t) * (size_t)tiles);
-  // items: a workgroup's n records take ceil(n / 256) items; the small-batch forward runs four
-  // workgroups per tile.  Overflow entries: up to one per (tile, quadrant).
-  s += align_up(sizeof(PairItem) * (size_t)(recs / kBlock + 4 * tiles));
+  // items: a tile's n records take ceil(n / 256) items.  Overflow entries: up to one per tile.
+  s += align_up(sizeof(PairItem) * (size_t)(recs / kBlock + tiles));
   s += align_up(sizeof(int32_t) * (size_t)tiles);
-  s += align_up(sizeof(int32_t) * (size_t)(4 * tiles));
-  s += align_up(sizeof(int32_t) * kHelpClear);  // counters, helper jobs and FIFO
+  s += align_up(sizeof(int32_t) * (size_t)tiles);
+  s += align_up(sizeof(int32_t) * kPairClear);  // counters and the record cursor
   return s;
 }
 
@@ -92,16 +91,14 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   pb.ntile = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.items = (PairItem *)(base + off);
-  off += align_up(sizeof(PairItem) * (size_t)(pb.cap / kBlock + 4 * tiles));
+  off += align_up(sizeof(PairItem) * (size_t)(pb.cap / kBlock + tiles));
   pb.tiles = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.ovf = (int32_t *)(base + off);
-  off += align_up(sizeof(int32_t) * (size_t)(4 * tiles));
+  off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.counters = (int32_t *)(base + off);
   pb.cursor = (unsigned long long *)(pb.counters + 4);
-  pb.jobs = (HelpJob *)(pb.counters + kHelpJobsAt);
-  pb.fifo = pb.counters + kHelpFifoAt;
-  off += align_up(sizeof(int32_t) * kHelpClear);
+  off += align_up(sizeof(int32_t) * kPairClear);
   return pb;
 }
 
@@ -284,90 +281,6 @@ __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub,
                    tile_q, tile_q);
 }
 
-// Balanced pass A (BAL, and the small-batch mode ST): one batch of the walk, its (sub-list s,
-// 64-face chunk c) items dealt to the waves in turn (item i = w, w + 4, ...), so a long sub-list
-// is worked on by every wave.  Slots follow the face order across the chunks: each item counts its
-// chunk's hits per pixel (capped at the pixel's remaining room), the counts of the sub-list's lower
-// chunks give each chunk's first slot, and the pixel's close-face count kid advances by the batch's
-// total (at most K).  NS = 4: sub-list s is sub-tile s's (pixel thread s * 64 + lane of the tile);
-// NS = 1 (ST): one sub-list (every wave built the same) for quadrant `quad`.  Called by every
-// thread of the workgroup (barriers inside).
-struct SoftItemsLDS {
-  uint64_t umask[4];                   // uncovered pixels of each sub-tile
-  unsigned char kid[4][kWave];         // close faces so far per pixel (knum <= kFuseSlots)
-  unsigned char hits[4][4][kWave];     // per (sub-tile, chunk) selected hits of the batch
-};
-
-template <int NS>
-__device__ __forceinline__ void soft_round_items(const TileLists &L, int K, const TileGeom &t,
-                                                 int64_t lo, int quad, SoftItemsLDS &B,
-                                                 uint64_t *s_pm, unsigned short *s_off,
-                                                 int *s_nrec, SoftPairRec *rec,
-                                                 unsigned short (*s_ridx)[kBlock]) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int nci[4] = {0, 0, 0, 0}, nitems = 0;
-#pragma unroll
-  for (int s = 0; s < NS; ++s) {
-    nci[s] = B.umask[s] ? (L.nsub[s] + kWave - 1) / kWave : 0;
-    nitems += nci[s];
-  }
-  auto origin = [&](int s, int &ox, int &oy) {
-    ox = NS == 1 ? t.WX0 : t.X0 + (s & 1) * 8;
-    oy = NS == 1 ? t.WY0 : t.Y0 + (s >> 1) * 8;
-  };
-  // item it -> (sub-list s, chunk c) (unrolled: nci stays in registers)
-  auto item = [&](int it, int &s, int &c) {
-    s = 0;
-    c = it;
-#pragma unroll
-    for (int q = 0; q < NS - 1; ++q)
-      if (s == q && c >= nci[q]) {
-        c -= nci[q];
-        s = q + 1;
-      }
-  };
-  // the item's hits of this pixel lane (chunk_hits' ballots run on the whole wave: lane j is
-  // also face j of the chunk)
-  auto hits = [&](int s, int c) {
-    int ox, oy;
-    origin(s, ox, oy);
-    const uint64_t h = chunk_hits(L, s, L.nsub[s], c, ox, oy);
-    const bool unc = (B.umask[s] >> lane) & 1ull;
-    return (unc && B.kid[s][lane] < K) ? h : 0ull;
-  };
-  // phase 1: counts (at most 16 items: 4 sub-lists x 256 faces)
-  for (int it = w; it < nitems; it += 4) {
-    int s, c;
-    item(it, s, c);
-    const int n = __popcll(hits(s, c));
-    B.hits[s][c][lane] = (unsigned char)min(n, K - (int)B.kid[s][lane]);
-  }
-  __syncthreads();
-  // phase 2: each chunk's first slot from its sub-list's lower chunks; the masks are recomputed
-  // (cheaper than holding them across the barrier at this register budget)
-  for (int it = w; it < nitems; it += 4) {
-    int s, c;
-    item(it, s, c);
-    int slot = B.kid[s][lane];
-    for (int v = 0; v < c; ++v) slot += B.hits[s][v][lane];
-    const int need = K - slot;
-    uint64_t h = hits(s, c);  // (whole wave: chunk_hits' ballots)
-    if (need <= 0)
-      h = 0ull;
-    else if (__popcll(h) > need)
-      h = lowest_bits(h, need);
-    if (__ballot(h != 0ull))
-      soft_chunk_write(L, s, h, c, lo, slot, s_pm, s_off, s_nrec, rec, s_ridx,
-                       (NS == 1 ? quad : s) * kWave + lane, (NS == 1 ? 0 : s) * kWave + lane);
-  }
-  __syncthreads();  // every wave has read kid / hits
-  if (w < NS) {
-    int tot = B.kid[w][lane];
-    for (int v = 0; v < nci[w]; ++v) tot += B.hits[w][v][lane];
-    B.kid[w][lane] = (unsigned char)min(K, tot);
-  }
-}
-
 // The streaming form of one chunk (a tile without records): the pixel lane visits the same
 // faces in slot order and hands each (face row, slot) to fn.
 template <typename PairFn>
@@ -393,17 +306,14 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
   const int novf = pb.counters[2];
-  const bool st = pb.counters[3] == 1;  // entries are 4 tile + quadrant (kd_dibr_fwd_st)
   for (int i = blockIdx.x; i < novf; i += gridDim.x) {
-    const int64_t ent = pb.ovf[i];
-    const int64_t tile = st ? ent >> 2 : ent;
+    const int64_t tile = pb.ovf[i];
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
     int64_t lo, hi;
     view_range(fs, b, lo, hi);
-    const TileGeom t = st ? tile_geom_st(H, W, tl, (int)(ent & 3)) : tile_geom(H, W, tl);
+    const TileGeom t = tile_geom(H, W, tl);
     const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-    // (ST: wave 0 owns the quadrant's pixels; the other waves only walk)
-    const bool unc = t.inimg && (!st || threadIdx.x < kWave) && a.face_idx[p] < 0;
+    const bool unc = t.inimg && a.face_idx[p] < 0;
     const bool wave_unc = __ballot(unc) != 0ull;
     const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
     int my_kid = 0;
@@ -433,7 +343,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
     if (__syncthreads_or(unc))
       tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg, done);
     if (unc && my_kid > 0 && a.soft) a.soft[p] = (T)(1.0 - (double)prod);
-    if (!FUSED && a.prob && t.inimg && (!st || threadIdx.x < kWave))
+    if (!FUSED && a.prob && t.inimg)
       for (int s = my_kid; s < K; ++s) {  // the -1 / 0 / 0 padding (kd_soft_lists skips the tile)
         a.prob[p * K + s] = (T)0;
         a.cidx[p * K + s] = -1;
@@ -505,40 +415,13 @@ struct SoftPairsLDS {
   int64_t base;
   int nrec, ibase, box[4];
   double iou[8];  // iou_tile_terms
-  SoftItemsLDS it;  // BAL / ST pass A (soft_round_items)
   int wbox[4][4];   // per wave: the box of its pixels that can still take a face (walk filter)
-  int job, claim;   // HELP: the tile's published job, the owner's current chunk
-  int hact, hc, hn, hjob;  // helper workgroups: thread 0's decision, broadcast
-  int64_t htile;
 };
 
 // Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
 // (t.px, t.py) of tile_geom(H, W, tl); a.face_idx of that pixel is read by the same thread (the
 // fused forward wrote it in the same workgroup, same thread).
-// BAL (FUSED only): pass A deals the batch's (sub-tile, chunk) items to the waves in turn
-// (soft_round_items), so a silhouette sub-tile with a long list is worked on by every wave.
-// ST (small-batch mode, FUSED only): quadrant `quad` of the tile (tile_geom_st); the four waves
-// share its 64 pixels (wave 0 owns them: soft values, product, IoU terms), pass A deals its
-// chunks to the four waves (soft_round_items), the pair math runs on all 256 threads; the
-// quadrant's records sit in its quarter of the tile's room, with the tile frame's pixel index.
-// ------------------------------------------------------------------------------------------
-// helper workgroups of the fused forward (kd_soft.hpp HelpJob).  Polling reads are returning
-// atomics (a CAS with a value the word never holds).  Owner and helpers run on one XCD: a
-// producer's stores are complete (s_waitcnt vmcnt(0): in its XCD's L2) before the atomic that
-// publishes them, and a consumer drops its CU's L1 (buffer_inv sc0) before reading them.
-// ------------------------------------------------------------------------------------------
-__device__ __forceinline__ int poll_i32(int *p) {
-  return atomicCAS(p, (int)0x80000000, (int)0x80000000);
-}
-__device__ __forceinline__ unsigned long long poll_u64(unsigned long long *p) {
-  return atomicCAS(p, ~0ull, ~0ull);
-}
-__device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void drop_l1() { asm volatile("buffer_inv sc0" ::: "memory"); }
-__device__ __forceinline__ int xcc_id() {
-  return (int)__builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11)) & (kHelpXcds - 1);
-}
-
+//
 // The pair math of records [i0, i1) of the tile whose records start at `base` (tile column tx,
 // row ty): distance type and probability, bit-identical to the reference (kd_softdist.hpp).
 template <typename T>
@@ -564,184 +447,23 @@ __device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const Soft
   }
 }
 
-// Owner side, after pass A (every tile of a helped launch calls it once, n uniform): a tile with
-// more than kHelpMin records (fixed pool layout) publishes a job -- its records in its XCD's L2,
-// the job word, up to kHelpFan entries in its XCD's FIFO -- and then counts itself past pass A.
-// Returns the job (or -1: the tile does its own pair math as without helpers).
-template <typename T>
-__device__ __forceinline__ int help_publish(const SoftPairBuf<T> &pb, int64_t tile, int n,
-                                            int *s_job) {
-  const bool heavy = n > kHelpMin && pb.fixed;
-  if (heavy) stores_done();  // this thread's records (pass A) are in the L2
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    int j = -1;
-    if (heavy) {
-      j = atomicAdd(&pb.counters[kHelpNJobs], 1);
-      if (j < kHelpJobs) {
-        const int x = xcc_id();
-        const int nch = (n + kHelpChunk - 1) / kHelpChunk;
-        const int ne = min(nch - 1, kHelpFan);
-        atomicExch(&pb.jobs[j].word,
-                   ((unsigned long long)(unsigned)n << 32) | (unsigned long long)(tile + 1));
-        // FIFO entries: reserved without passing its end (a job without entries is the
-        // owner's alone)
-        int *tail = &pb.counters[kHelpTail + 32 * x];
-        int t0 = poll_i32(tail);
-        while (t0 + ne <= kHelpFifoX) {
-          const int o = atomicCAS(tail, t0, t0 + ne);
-          if (o == t0) break;
-          t0 = o;
-        }
-        if (t0 + ne <= kHelpFifoX)
-          for (int e = 0; e < ne; ++e) atomicExch(&pb.fifo[x * kHelpFifoX + t0 + e], j + 1);
-      } else {
-        j = -1;
-      }
-    }
-    if (heavy) stores_done();  // (the entries before the count)
-    atomicAdd(&pb.counters[kHelpPassed], 1);
-    *s_job = j;
-  }
-  __syncthreads();
-  return *s_job;
-}
-
-// Owner side: claim chunks of job `job` (the next claim in flight during the math), then wait
-// for the chunks helpers claimed (each is being worked on by a running workgroup).
-template <typename T>
-__device__ __forceinline__ void help_owner_math(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
-                                                int job, int64_t base, int tx, int ty, int n,
-                                                int *s_claim) {
-  const int nch = (n + kHelpChunk - 1) / kHelpChunk;
-  int *claim = &pb.jobs[job].claim;
-  if (threadIdx.x == 0) *s_claim = atomicAdd(claim, 1);
-  __syncthreads();
-  int c = *s_claim, mine = 0;
-  while (c < nch) {
-    __syncthreads();  // every thread has read *s_claim
-    int nxt = 0;
-    if (threadIdx.x == 0) nxt = atomicAdd(claim, 1);
-    pair_math_range<T>(a, pb, base, tx, ty, c * kHelpChunk, min(n, (c + 1) * kHelpChunk));
-    ++mine;
-    if (threadIdx.x == 0) *s_claim = nxt;
-    __syncthreads();
-    c = *s_claim;
-  }
-  if (mine < nch) {
-    if (threadIdx.x == 0)
-      while (poll_i32(&pb.jobs[job].done) < nch - mine) __builtin_amdgcn_s_sleep(2);
-    __syncthreads();
-    drop_l1();  // the helpers' probabilities (in the L2)
-  }
-}
-
-// A helper workgroup: take an entry of its XCD's FIFO (a job), claim its chunks until none is
-// left, repeat; exit once every tile is past pass A and the FIFO is drained (the owners finish
-// what is left).
-template <typename T>
-__device__ __forceinline__ void help_loop(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
-                                          int ntot, SoftPairsLDS<true> &S) {
-  zero_side_job(a);
-  const int x = xcc_id();
-  int *tailp = &pb.counters[kHelpTail + 32 * x], *headp = &pb.counters[kHelpHead + 32 * x];
-  const int *fifo = pb.fifo + x * kHelpFifoX;
-  int jj = -1, jn = 0, jnch = 0, seen = 0;  // thread 0: the current job, the last head seen
-  int64_t jtile = 0;
-  while (true) {
-    if (threadIdx.x == 0) {
-      int act = 3, c = 0;  // 1 work chunk c, 0 retry now, 2 exit, 3 sleep and retry
-      if (jj >= 0) {
-        c = atomicAdd(&pb.jobs[jj].claim, 1);
-        if (c < jnch) act = 1;
-        else jj = -1;
-      }
-      if (jj < 0) {
-        const int tail = poll_i32(tailp);
-        // (head only moves up to tail: a tail at the last head seen means nothing new)
-        const int head = tail > seen ? poll_i32(headp) : tail;
-        seen = head;
-        if (head >= tail && poll_i32(&pb.counters[kHelpPassed]) >= ntot) {
-          // every tile is past pass A, so every entry is in: read the FIFO again (issued after
-          // the count returned -- the branch depends on it) to see whether it is drained
-          act = poll_i32(headp) >= poll_i32(tailp) ? 2 : 0;
-        } else if (head < tail) {
-          act = 0;
-          if (atomicCAS(headp, head, head + 1) == head) {
-            int e;
-            while ((e = poll_i32(const_cast<int *>(fifo) + head)) == 0)
-              __builtin_amdgcn_s_sleep(1);
-            jj = e - 1;
-            unsigned long long wd;
-            while ((wd = poll_u64(&pb.jobs[jj].word)) == 0ull) __builtin_amdgcn_s_sleep(1);
-            jn = (int)(wd >> 32);
-            jtile = (int64_t)(wd & 0xffffffffull) - 1;
-            jnch = (jn + kHelpChunk - 1) / kHelpChunk;
-            c = atomicAdd(&pb.jobs[jj].claim, 1);
-            if (c < jnch) act = 1;
-            else jj = -1;
-          }
-        }
-      }
-      S.hact = act;
-      S.hc = c;
-      S.hn = jn;
-      S.hjob = jj;
-      S.htile = jtile;
-    }
-    __syncthreads();
-    const int act = S.hact, c = S.hc, n = S.hn, job = S.hjob;
-    const int64_t tile = S.htile;
-    __syncthreads();
-    if (act == 2) return;
-    if (act == 3) __builtin_amdgcn_s_sleep(48);  // idle: ~1.3 us between polls
-    if (act == 0) __builtin_amdgcn_s_sleep(2);   // lost a race for the FIFO head
-    if (act != 1) continue;
-    drop_l1();  // the owner's records (in the L2)
-    const int tl = (int)(tile % pb.ntiles);
-    pair_math_range<T>(a, pb, tile * kBlock * (int64_t)a.K, tl % pb.ntx, tl / pb.ntx,
-                       c * kHelpChunk, min(n, (c + 1) * kHelpChunk));
-    stores_done();  // probabilities and types in the L2
-    __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(&pb.jobs[job].done, 1);
-  }
-}
-
-template <typename T, bool FUSED, bool ST = false, bool BAL = false, bool HELP = false>
+template <typename T, bool FUSED>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
-                                                int b, int tl, int nbin, SoftPairsLDS<FUSED> &S,
-                                                int quad = 0) {
-  static_assert(!(ST || BAL) || FUSED, "the balanced / small-batch modes are the fused soft mask");
-  constexpr bool kItems = ST || BAL;
+                                                int b, int tl, int nbin, SoftPairsLDS<FUSED> &S) {
   TileLists &L = S.L;
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
-  const bool own = !ST || w == 0;  // this thread writes its pixel's results
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   const int nview = (int)(hi - lo);
-  TileGeom t = ST ? tile_geom_st(H, W, tl, quad) : tile_geom(H, W, tl);
+  TileGeom t = tile_geom(H, W, tl);
   t.nbin = nbin;
   if (KD_DIAG && fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, bin) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-  bool unc;
-  if constexpr (ST) {  // wave 0 wrote the quadrant's face_idx: it hands the mask to the others
-    if (w == 0) {
-      const uint64_t m = __ballot(t.inimg && a.face_idx[p] < 0);
-      if (lane == 0) S.it.umask[0] = m;
-    }
-    __syncthreads();
-    unc = (S.it.umask[0] >> lane) & 1ull;
-  } else {
-    unc = t.inimg && a.face_idx[p] < 0;
-    if (BAL) {  // (the walk's first barrier orders these before pass A)
-      const uint64_t m = __ballot(unc);
-      if (lane == 0) S.it.umask[w] = m;
-    }
-  }
+  const bool unc = t.inimg && a.face_idx[p] < 0;
   const bool wave_unc = __ballot(unc) != 0ull;
   const int64_t tile = (int64_t)b * pb.ntiles + tl;
   int my_kid = 0;
@@ -756,7 +478,6 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     S.nrec = 0;
     S.base = -1;
   }
-  if (kItems && (BAL || w == 0)) S.it.kid[w][lane] = 0;
   {
     const uint64_t um = __ballot(unc);
     t.wave_live = t.wave_live && um != 0ull;
@@ -777,7 +498,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     atomicMin(&s_box[2], t.SY0);
     atomicMax(&s_box[3], t.SY1);
   }
-  const int U = __syncthreads_count(unc && own);
+  const int U = __syncthreads_count(unc);
   bool ovf = false;
   if (U > 0) {
     // the tile's room in the pool: its own 256 K records (`fixed`), or, reserved with one device
@@ -785,7 +506,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     // latency overlaps the walk's first loads (records are written after a barrier of
     // tile_rounds)
     if (pb.fixed) {
-      if (tid == 0) S.base = tile * kBlock * K + (ST ? (int64_t)quad * kWave * K : 0);
+      if (tid == 0) S.base = tile * kBlock * K;
     } else if (tid == 0) {
       const BinGeom &g = a.bb.g;
       const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
@@ -803,10 +524,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     t.FY1 = s_box[3];
     auto stage = [&](int, int64_t) {};  // pass A needs the spans only
     auto round = [&](int nsub, int) {
-      if constexpr (kItems) {
-        soft_round_items<ST ? 1 : 4>(L, K, t, lo, quad, S.it, S.pm[w], S.off[w], &S.nrec,
-                                     pb.rec + S.base, S.ridx);
-      } else if (wave_unc && !ablate(fs.dbg, 1024)) {
+      if (wave_unc && !ablate(fs.dbg, 1024)) {
         for (int c = 0; c * kWave < nsub; ++c)
           soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], &S.nrec,
                              pb.rec + S.base, FUSED ? S.ridx : nullptr);
@@ -818,8 +536,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     // enlarged span reaches none of them cannot enter any list, so the next batches' tile list
     // and sub-lists hold only faces that can (exact, like the first filter)
     auto done = [&]() {
-      const int kk = kItems ? (int)S.it.kid[ST ? 0 : w][lane] : my_kid;
-      const bool open = unc && kk < K;
+      const bool open = unc && my_kid < K;
       const uint64_t om = __ballot(open);
       int bx0 = 1 << 30, bx1 = -1, by0 = 1 << 30, by1 = -1;
       if (om) {
@@ -869,18 +586,17 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     if (KD_DIAG && fs.tbuf && tid == 0 && FUSED)  // diagnostics: end of pass A
       fs.tbuf[5ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
           wall_clock64();
-    if (kItems) my_kid = S.it.kid[ST ? 0 : w][lane];
   }
   if (ovf) {  // no records: kd_soft_ovf_fwd computes the tile's soft mask, kd_soft_ovf_bwd its
-              // backward (ST: the quadrant's, entry 4 tile + quadrant)
+              // backward
     my_kid = 0;
     if (tid == 0) {
-      pb.ovf[atomicAdd(&pb.counters[2], 1)] = ST ? (int32_t)(4 * tile + quad) : (int32_t)tile;
+      pb.ovf[atomicAdd(&pb.counters[2], 1)] = (int32_t)tile;
       S.nrec = 0;
     }
   }
   T sval = unc ? (T)0.0 : (T)1.0;  // this pixel's soft value (FUSED: the product below)
-  if (t.inimg && own) {
+  if (t.inimg) {
     if (!FUSED) pb.npix[p] = my_kid;  // the split pipeline's reduce
     if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
     else if (a.soft && my_kid == 0) a.soft[p] = (T)0.0;
@@ -891,7 +607,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   __syncthreads();
   const int n = S.nrec;
   const int64_t base = S.base;
-  if (tid == 0 && !ST) {  // (ST: four workgroups share the tile; the fused path never reads these)
+  if (tid == 0) {
     pb.ntile[tile] = ovf ? -1 : n;  // -1: kd_soft_ovf_fwd streams the tile (lists included)
     pb.tbase[tile] = n > 0 ? base : 0;
   }
@@ -908,26 +624,22 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   }
   if constexpr (FUSED) {
     zero_side_job(a);
-    const int job = HELP ? help_publish<T>(pb, tile, n, &S.job) : -1;
     if (n == 0) {
-      iou_tile_terms<T>(a, b, tl, p, t.inimg && own, sval, S.iou);
+      iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
       return;
     }
     // pair math over this tile's records (record order: coalesced reads; diag 32: none)
     const int tx = tl % pb.ntx, ty = tl / pb.ntx;
     const T *sp = pb.sprob + base;
-    if (HELP && job >= 0)
-      help_owner_math<T>(a, pb, job, base, tx, ty, n, &S.claim);
-    else
-      pair_math_range<T>(a, pb, base, tx, ty, 0, n);
+    pair_math_range<T>(a, pb, base, tx, ty, 0, n);
     __syncthreads();  // the workgroup's probabilities are visible to it
     if (KD_DIAG && fs.tbuf && tid == 0)  // diagnostics: end of the pair math
       fs.tbuf[6ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
           wall_clock64();
     // soft = 1 - prod(1 - p) in slot order (dibr_soft_mask_cuda.cu:174-181, double-promoted)
-    if (unc && my_kid > 0 && own) {
+    if (unc && my_kid > 0) {
       constexpr int U8 = 8;
-      const int rq = ST ? lane : tid;  // the pixel's column of the record table
+      const int rq = tid;  // the pixel's column of the record table
       T prod = (T)1.0;
       for (int s0 = 0; s0 < my_kid; s0 += U8) {
         T pv[U8];
@@ -940,7 +652,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       sval = (T)(1.0 - (double)prod);
       a.soft[p] = sval;
     }
-    iou_tile_terms<T>(a, b, tl, p, t.inimg && own, sval, S.iou);
+    iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
   }
 }
 
@@ -969,11 +681,7 @@ union DibrTileLDS {
 // DIAG (debug flag 64 with a debug buffer): per dispatch slot the tile, its bin counts, start,
 // duration and raster-phase end (tools/soft_timeline.py).  A separate instantiation: the clock's
 // live registers alone make the kernel spill.
-// BAL: both phases deal their (sub-tile, chunk) items to the four waves in turn (balanced;
-// debug flag 1 << 28).  Measured at C3, 1 / 2 / 8 views: 73 / 81 / 176 us against 67 / 74 / 160
-// for the per-wave form (its extra barriers and per-item bookkeeping cost more than the balance
-// gains), so the production launch is the per-wave form.
-template <bool DIAG, bool BAL>
+template <bool DIAG>
 __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
                                                               SoftArgs<float> a,
                                                               SoftPairBuf<float> pb) {
@@ -990,70 +698,12 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
     const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
     a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
   }
-  raster_pairs_tile<float, false, BAL>(ra, b, tl, nbin, U.r);
+  raster_pairs_tile<float>(ra, b, tl, nbin, U.r);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
-  soft_pairs_tile<float, true, false, BAL>(a, pb, b, tl, -1, U.s);
-}
-
-// kd_dibr_fwd_tiles with helper workgroups (kd_soft.hpp HelpJob): a 1-D grid of the B x tiles
-// tile workgroups (dispatch slot d = blockIdx.x, the same heaviest-first, XCD-aware order) and
-// then `nhelp` helpers, which work on the published pair math of the silhouette tiles.
-__global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_help(RasterFwdArgs<float> ra,
-                                                             SoftArgs<float> a,
-                                                             SoftPairBuf<float> pb) {
-  __shared__ DibrTileLDS<float> U;
-  const int ntot = (int)(pb.ntiles * ra.fs.B);
-  if ((int)blockIdx.x >= ntot) {
-    help_loop<float>(a, pb, ntot, U.s);
-    return;
-  }
-  int b, tl, nbin;
-  tile_of_slot(ra.bb, ra.fs.H, ra.fs.W, (int)blockIdx.x, ntot, b, tl, nbin, ra.fs.dbg);
-  raster_pairs_tile<float>(ra, b, tl, nbin, U.r);
-  __syncthreads();  // the raster phase is done with the LDS
-  soft_pairs_tile<float, true, false, false, true>(a, pb, b, tl, -1, U.s);
-}
-
-// The small-batch form of kd_dibr_fwd_tiles (few views: the grid of 16x16 tiles is about one
-// round of workgroup slots, so the kernel's length is its heaviest tile, not the chip's work):
-// one workgroup per 8x8 quadrant of a tile, over 16-pixel coarse bins, its four waves splitting
-// the quadrant's face chunks in both phases and its pair math (ST bodies above).  A tile's
-// serial work -- the silhouette and pole tiles' walk, pairs and pair math -- spreads over four
-// workgroups and four times the waves.  Same records, outputs and backward as the tile kernel.
-// DIAG: the per-slot timeline of kd_dibr_fwd_tiles<true> (tools/soft_timeline.py), slot = workgroup.
-template <bool DIAG>
-__global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_st(RasterFwdArgs<float> ra,
-                                                            SoftArgs<float> a,
-                                                            SoftPairBuf<float> pb) {
-  __shared__ DibrTileLDS<float> U;
-  TileClock clk(DIAG ? a.fs.tbuf : nullptr, 1);
-  if (DIAG) clk.start_to(2);
-  int b, tl, nbin, quad;
-  // the overflow kernels' mode flag (counters[3], zeroed by kd_bin_count): overflow entries are
-  // (tile, quadrant) pairs
-  if (blockIdx.x == 0 && threadIdx.x == 0) pb.counters[3] = 1;
-  // dispatch order: the raster bins' heaviest first, or (debug flag 1 << 25, A/B) the soft bins'
-  const bool soft_order = (ra.fs.dbg & (1 << 25)) != 0;
-  if (!st_of_block(soft_order ? a.bb : ra.bb, ra.fs.B, ra.fs.H, ra.fs.W, b, tl, nbin, quad)) {
-    zero_side_job(a);  // (the grid is padded to whole groups of 32)
-    return;
-  }
-  if (DIAG && a.fs.tbuf && threadIdx.x == 0) {
-    const int64_t nb = gridDim.x, slot = blockIdx.x;
-    a.fs.tbuf[slot] = ((long long)nbin << 32) | (long long)(4 * (b * pb.ntiles + tl) + quad);
-    const BinGeom &g = a.bb.g;
-    const int tx = tl % pb.ntx, ty = tl / pb.ntx;
-    const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
-    a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
-  }
-  raster_pairs_tile<float, true>(ra, b, tl, soft_order ? -1 : nbin, U.r, quad);
-  __syncthreads();  // the raster phase is done with the LDS
-  if (DIAG && a.fs.tbuf && threadIdx.x == 0)
-    a.fs.tbuf[3ll * gridDim.x + blockIdx.x] = wall_clock64();
-  soft_pairs_tile<float, true, true>(a, pb, b, tl, -1, U.s, quad);
+  soft_pairs_tile<float, true>(a, pb, b, tl, -1, U.s);
 }
 
 // The fp64 DIB-R forward in one launch: the pair raster (fp64 test, fp64-culled candidates, the
@@ -1466,16 +1116,14 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_bwd(SoftArgs<T> a, SoftPai
   const int H = fs.H, W = fs.W, K = a.K;
   const float M = fs.M;
   const int novf = pb.counters[2];
-  const bool st = pb.counters[3] == 1;  // entries are 4 tile + quadrant (kd_dibr_fwd_st)
   for (int i = blk; i < novf; i += nblk) {
-    const int64_t ent = pb.ovf[i];
-    const int64_t tile = st ? ent >> 2 : ent;
+    const int64_t tile = pb.ovf[i];
     const int b = (int)(tile / pb.ntiles), tl = (int)(tile - (int64_t)b * pb.ntiles);
     int64_t lo, hi;
     view_range(fs, b, lo, hi);
-    const TileGeom t = st ? tile_geom_st(H, W, tl, (int)(ent & 3)) : tile_geom(H, W, tl);
+    const TileGeom t = tile_geom(H, W, tl);
     const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-    const bool unc = t.inimg && (!st || threadIdx.x < kWave) && a.face_idx[p] < 0;
+    const bool unc = t.inimg && a.face_idx[p] < 0;
     const bool wave_unc = __ballot(unc) != 0ull;
     const double sp =
         unc ? -(double)a.sigmainv * (double)soft_grad_at<T>(a, b, p) * (1.0 - (double)a.soft_in[p])
@@ -1572,7 +1220,8 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   a.fs.tbuf = debug_tile_buffer();
   // one launch for the whole soft mask (the autograd path: no close-face lists)
   const bool fused =
-      reduce && a.soft && !a.prob && !a.last && a.K <= kFuseSlots && !(a.fs.dbg & 4096);
+      reduce && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
+      !(test_forms() & KD_FORM_SOFT_SPLIT);
   if (fused) {
     ProfScope prof(K_SOFT_PAIRS, stream);
     // 6 workgroups per CU (the 16 KB record-index table); 4 and 8 measured no faster
@@ -1610,7 +1259,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
           return set_error(KD_ERR_LAUNCH, "soft lists: %s", hipGetErrorString(ea));
       }
       if (ablate(debug_flags(), (1 << 16) | (1 << 23)))  // diagnostics: the skipped index stores
-        hipMemsetAsync(a.cidx, 0xFF, sizeof(int64_t) * fs.B * fs.H * fs.W * a.K, stream);  // -1
+        (void)hipMemsetAsync(a.cidx, 0xFF, sizeof(int64_t) * fs.B * fs.H * fs.W * a.K, stream);  // -1
       hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), dyn, stream, a, pb);
     } else
       hipLaunchKernelGGL(kd_soft_reduce<T>, dim3(8192), dim3(kBlock), 0, stream, a, pb);
@@ -1624,7 +1273,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
 
 bool dibr_fwd_fusable(const RasterFwdArgs<double> &ra, const SoftArgs<double> &a) {
   return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
-         !(debug_flags() & ((1 << 26) | 4096));
+         !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT));
 }
 
 int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
@@ -1645,35 +1294,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
 
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) {
   return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
-         !(debug_flags() & ((1 << 26) | 4096));
-}
-
-// Helper workgroups for kd_dibr_fwd_help (0: the plain tile kernel).  Needs the fixed pool
-// layout (a job's records start at tile * 256 K), the per-launch help region zeroed by the
-// binning (kHelpClear) and an occupancy that leaves the tiles slots beside the helpers: the
-// helpers are at most half of the chip's resident workgroups of this kernel, so tiles -- which
-// never wait -- always find slots, and every helper's exit condition is reached.
-// Opt-in (debug flag 256; 512: the helped kernel without helper workgroups, returned as -1):
-// measured slower than the plain tile kernel at every view count (C3, same box: 1 view forward
-// 82.6 us against 67.5, 2 views 123 against 72, 8 views 210 against 157; without helper
-// workgroups 72.4 / 161.5 -- the owners' claims alone cost ~5 us), see DESIGN.md section 4.
-static int help_workgroups(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a,
-                           const SoftPairBuf<float> &pb) {
-  if (!(a.fs.dbg & (256 | 512)) || a.fs.tbuf || !pb.fixed || a.K > kFuseSlots ||
-      a.bb.n_clear < kHelpClear || (a.fs.dbg & (1 << 28)) || pb.ntiles * ra.fs.B >= (1 << 30))
-    return 0;
-  static int slots = -1;  // resident kd_dibr_fwd_help workgroups of the device (first call)
-  if (slots < 0) {
-    int dev = 0, ncu = 0, per = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kd_dibr_fwd_help, kBlock, 0) !=
-            hipSuccess)
-      ncu = per = 0;
-    slots = ncu * per;
-  }
-  if (a.fs.dbg & 512) return -1;  // A/B: the helped tile kernel without helper workgroups
-  return std::min(kHelpers, slots / 2);
+         !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT));
 }
 
 int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
@@ -1681,43 +1302,14 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   ra.fs.dbg = a.fs.dbg = debug_flags();
   ra.fs.tbuf = nullptr;
   a.fs.tbuf = debug_tile_buffer();
-  if (dibr_small_batch(ra.fs.B, ra.fs.H, ra.fs.W, 4) && ra.bb.nchunk > 0) {  // small batch
-    ProfScope prof(K_DIBR_FWD, stream);
-    const int64_t n = (int64_t)pb.ntiles * ra.fs.B;
-    const int64_t nwg = 4 * ((n + 7) / 8 * 8);
-    if (KD_DIAG && a.fs.tbuf)
-      hipLaunchKernelGGL(kd_dibr_fwd_st<KD_DIAG != 0>, dim3((unsigned)nwg), dim3(kBlock), 0,
-                         stream, ra, a, pb);
-    else
-      hipLaunchKernelGGL(kd_dibr_fwd_st<false>, dim3((unsigned)nwg), dim3(kBlock), 0, stream, ra,
-                         a, pb);
-  } else if (const int nh = help_workgroups(ra, a, pb)) {
-    ProfScope prof(K_DIBR_FWD, stream);
-    const int64_t ntot = pb.ntiles * ra.fs.B;
-    hipLaunchKernelGGL(kd_dibr_fwd_help, dim3((unsigned)(ntot + std::max(nh, 0))), dim3(kBlock),
-                       0, stream, ra, a, pb);
-  } else {
+  {
     ProfScope prof(K_DIBR_FWD, stream);
     const dim3 grid((unsigned)pb.ntiles, ra.fs.B);
-    const bool bal = (a.fs.dbg & (1 << 28)) != 0;  // measured slower: diagnostics only
-    if constexpr (KD_DIAG) {
-      if (a.fs.tbuf) {
-        if (bal)
-          hipLaunchKernelGGL((kd_dibr_fwd_tiles<true, true>), grid, dim3(kBlock), 0, stream, ra,
-                             a, pb);
-        else
-          hipLaunchKernelGGL((kd_dibr_fwd_tiles<true, false>), grid, dim3(kBlock), 0, stream, ra,
-                             a, pb);
-        goto launched;
-      }
-    }
-    if (bal)
-      hipLaunchKernelGGL((kd_dibr_fwd_tiles<false, true>), grid, dim3(kBlock), 0, stream, ra, a,
+    if (KD_DIAG && a.fs.tbuf)
+      hipLaunchKernelGGL((kd_dibr_fwd_tiles<KD_DIAG != 0>), grid, dim3(kBlock), 0, stream, ra, a,
                          pb);
     else
-      hipLaunchKernelGGL((kd_dibr_fwd_tiles<false, false>), grid, dim3(kBlock), 0, stream, ra, a,
-                         pb);
-  launched:;
+      hipLaunchKernelGGL((kd_dibr_fwd_tiles<false>), grid, dim3(kBlock), 0, stream, ra, a, pb);
   }
   if (pool_may_overflow(a.K)) ovf_fwd_launch<float, true>(a, pb, stream);
   const hipError_t e = hipGetLastError();

@@ -100,57 +100,6 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
 }
 __device__ __forceinline__ TileGeom tile_geom(int H, int W) { return tile_geom(H, W, blockIdx.x); }
 
-// Small-batch mode (kd_dibr_fwd_st): a workgroup covers only the 8x8 quadrant `quad` of fine
-// tile `tile`, with all four waves on its 64 pixels (lane l: pixel (l & 7, l >> 3) of the
-// quadrant, the pixel thread quad * 64 + l of the 16x16 tile frame owns there).  The tile and
-// sub-tile filter boxes are the quadrant.
-__device__ __forceinline__ TileGeom tile_geom_st(int H, int W, int tile, int quad) {
-  const int ntx = (W + kTile - 1) / kTile;
-  const int tx = tile % ntx, ty = tile / ntx;
-  const int lane = threadIdx.x & 63;
-  TileGeom t;
-  t.WX0 = tx * kTile + (quad & 1) * 8;
-  t.WY0 = ty * kTile + (quad >> 1) * 8;
-  t.WX1 = min(t.WX0 + 7, W - 1);
-  t.WY1 = min(t.WY0 + 7, H - 1);
-  t.X0 = t.WX0;
-  t.Y0 = t.WY0;
-  t.X1 = t.WX1;
-  t.Y1 = t.WY1;
-  t.px = t.WX0 + (lane & 7);
-  t.py = t.WY0 + (lane >> 3);
-  t.inimg = t.px < W && t.py < H;
-  t.wave_live = t.WX0 < W && t.WY0 < H;
-  t.nbin = -1;
-  t.FX0 = t.X0;
-  t.FX1 = t.X1;
-  t.FY0 = t.Y0;
-  t.FY1 = t.Y1;
-  t.SX0 = t.WX0;
-  t.SX1 = t.WX1;
-  t.SY0 = t.WY0;
-  t.SY1 = t.WY1;
-  return t;
-}
-
-// (view, fine tile, quadrant) of a small-batch workgroup, from the bins' heaviest-first order:
-// workgroup d runs on XCD d % 8 (round-robin dealing); its k = d / 8-th slot there takes
-// order entry (k / 4) * 8 + d % 8, quadrant k % 4 -- the four quadrants of a tile (one coarse bin)
-// share an XCD's L2, and the order stays heaviest first.  false: past the last entry.
-__device__ __forceinline__ bool st_of_block(const BinBuffers &bb, int B, int H, int W, int &b,
-                                            int &tile, int &nbin, int &quad) {
-  const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-  const int d = blockIdx.x, k = d >> 3;
-  const int e = (k >> 2) * 8 + (d & 7);
-  quad = k & 3;
-  if (e >= B * ntiles) return false;
-  const int2 v = bb.order[e];
-  b = v.x / ntiles;
-  tile = v.x - b * ntiles;
-  nbin = v.y;
-  return true;
-}
-
 struct TileLists {
   int f[kCap];                   // local face index (ascending)
   Span span[kCap];

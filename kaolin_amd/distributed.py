@@ -75,9 +75,11 @@ class EarlyReduce:
     `params` (a parameter starts once it and every parameter before it are ready), so every rank
     issues the same collectives in the same order whatever order its hooks fire in; the
     collectives run on RCCL's stream while the rest of the backward runs on the compute stream.
-    ``wait()`` issues whatever is left -- a parameter this rank produced no gradient for (e.g. a
-    rank holding no views) contributes zeros -- and joins them.  The vertex gradient (the last
-    one produced) is reduced by the caller."""
+    ``flush()`` issues whatever is left -- a parameter this rank produced no gradient for (e.g. a
+    rank holding no views) contributes zeros -- and ``wait()`` joins them.  A caller that issues
+    collectives of its own after the backward (the vertex gradient's bucket) calls ``flush()``
+    first, so that every rank issues the shared reductions before its own, in the same order,
+    whichever hooks fired on it."""
 
     def __init__(self, params, group=None):
         self.group = group
@@ -104,11 +106,15 @@ class EarlyReduce:
             self._issue(self.next)
             self.next += 1
 
-    def wait(self):
+    def flush(self):
+        """Issue every parameter not issued yet (zeros for a gradient this rank never produced)."""
         if self.handles:
             while self.next < len(self.params):
                 self._issue(self.next)
                 self.next += 1
+
+    def wait(self):
+        self.flush()
         for w in self.works:
             w.wait()
         self.works = []
@@ -121,16 +127,23 @@ class EarlyReduce:
 
 class GradBucket:
     """The step's exchange: the shared parameters' gradients summed over the ranks as ONE flat
-    all-reduce.  The flat buffer is allocated once; ``pack()`` copies the gradients into it (on
-    the current stream: inside a captured HIP graph these copies are graph nodes), ``reduce()``
-    runs the collective (RCCL over xGMI with backend "nccl") and ``unpack()`` copies the sums
-    back.  A single contiguous gradient is reduced in place (no copies).  Parameters without a
-    gradient on this rank contribute zeros, so every rank issues the same collective."""
+    all-reduce per dtype (one in the DIB-R step: vertices and features share a dtype; a mixed
+    set keeps each gradient's precision instead of casting it into one buffer).  The flat
+    buffers are allocated once; ``pack()`` copies the gradients into them (on the current
+    stream: inside a captured HIP graph these copies are graph nodes) and ``reduce()`` runs the
+    collectives (RCCL over xGMI with backend "nccl", in the fixed order of the parameters' first
+    dtype occurrence) and copies the sums back.  A single contiguous gradient of its dtype is
+    reduced in place (no copies).  Parameters without a gradient on this rank contribute zeros,
+    so every rank issues the same collectives."""
 
     def __init__(self, params, group=None):
         self.params = list(params)
         self.group = group
-        self.flat = None
+        self.flat = {}  # dtype -> flat buffer
+        groups = {}
+        for i, p in enumerate(self.params):
+            groups.setdefault(p.dtype, []).append(i)
+        self.groups = list(groups.items())  # [(dtype, [param indices])], first-occurrence order
 
     def _grads(self):
         for p in self.params:
@@ -138,32 +151,42 @@ class GradBucket:
                 p.grad = torch.zeros_like(p)
         return [p.grad for p in self.params]
 
+    @staticmethod
+    def _in_place(gs):
+        return len(gs) == 1 and gs[0].is_contiguous()
+
     def pack(self):
         if not self.params or not _distributed(self.group):
             return
-        gs = self._grads()
-        if len(gs) == 1 and gs[0].is_contiguous():
-            return
-        n = sum(g.numel() for g in gs)
-        if self.flat is None or self.flat.numel() != n or self.flat.device != gs[0].device:
-            self.flat = torch.empty(n, device=gs[0].device, dtype=gs[0].dtype)
-        off = 0
-        for g in gs:
-            self.flat[off:off + g.numel()].copy_(g.reshape(-1))
-            off += g.numel()
+        grads = self._grads()
+        for dt, idx in self.groups:
+            gs = [grads[i] for i in idx]
+            if self._in_place(gs):
+                continue
+            n = sum(g.numel() for g in gs)
+            flat = self.flat.get(dt)
+            if flat is None or flat.numel() != n or flat.device != gs[0].device:
+                flat = self.flat[dt] = torch.empty(n, device=gs[0].device, dtype=dt)
+            off = 0
+            for g in gs:
+                flat[off:off + g.numel()].copy_(g.reshape(-1))
+                off += g.numel()
 
     def reduce(self):
         if not self.params or not _distributed(self.group):
             return
-        gs = self._grads()
-        if len(gs) == 1 and gs[0].is_contiguous():
-            dist.all_reduce(gs[0], op=dist.ReduceOp.SUM, group=self.group)
-            return
-        dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
-        off = 0
-        for g in gs:
-            g.copy_(self.flat[off:off + g.numel()].view_as(g))
-            off += g.numel()
+        grads = self._grads()
+        for dt, idx in self.groups:
+            gs = [grads[i] for i in idx]
+            if self._in_place(gs):
+                dist.all_reduce(gs[0], op=dist.ReduceOp.SUM, group=self.group)
+                continue
+            flat = self.flat[dt]
+            dist.all_reduce(flat, op=dist.ReduceOp.SUM, group=self.group)
+            off = 0
+            for g in gs:
+                g.copy_(flat[off:off + g.numel()].view_as(g))
+                off += g.numel()
 
     def __call__(self):
         self.pack()
@@ -231,6 +254,7 @@ def dibr_step(vertices, faces, camera_proj, camera_transform, face_features, hei
                                          face_features, height, width, grad_interp, grad_soft,
                                          sigmainv, boxlen, knum, prepare, render)
         late = [vertices] + [p for p in shared if not early.handles]
+        early.flush()  # the shared reductions first on every rank, whichever hooks fired
         GradBucket(late, group)()
         early.wait()
     finally:
@@ -250,7 +274,8 @@ class GraphedStep:
     the zeroed-on-the-side gradient buffers) inside the graph: tests/test_gpu_graphed_step.py
     compares replays with eager steps."""
 
-    def __init__(self, params, fn, params_to_reduce=None, group=None, warmup=3):
+    def __init__(self, params, fn, params_to_reduce=None, group=None, warmup=3,
+                 capture_hook=None):
         self.params = list(params)  # every parameter whose .grad the step writes
         self.reduce = self.params if params_to_reduce is None else list(params_to_reduce)
         self.fn = fn
@@ -266,15 +291,30 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(s)
         self._clear()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            self.out = fn()
-            self.bucket.pack()
+        if capture_hook:  # e.g. the library's per-launch HIP events, captured as graph nodes
+            capture_hook(True)
+        try:
+            with torch.cuda.graph(self.graph):
+                self.out = fn()
+                self.bucket.pack()
+        finally:
+            if capture_hook:
+                capture_hook(False)
 
     def _clear(self):
         for p in self.params:
             p.grad = None
 
-    def __call__(self):
+    def replay(self):
+        """The GPU part of the step (one graph launch)."""
         self.graph.replay()
+        return self.out
+
+    def exchange(self):
+        """The step's all-reduce (eager RCCL), after the replay."""
         self.bucket.reduce()
+
+    def __call__(self):
+        self.replay()
+        self.exchange()
         return self.out

@@ -68,3 +68,15 @@ def test_prepare_vertices_ranges_partition():
     empty = np.zeros(4, np.int64)
     out = np.empty(5, np.int32)
     assert _lib.load().kd_prepare_vertices_ranges(empty.ctypes.data, 3, 256, out.ctypes.data) == 0
+
+
+def test_production_library_reads_no_debug_flags():
+    """The production library selects no kernel from debug flags (diagnostic build only); the
+    launch-form test hook accepts only its KD_FORM_* bits."""
+    lib = _lib.load()
+    assert lib.kd_debug_set(0) == _lib.KD_OK
+    assert lib.kd_debug_set(256) != _lib.KD_OK
+    assert b'diagnostic' in lib.kd_last_error()
+    assert lib.kd_set_test_forms(8) != _lib.KD_OK
+    _lib.set_test_forms(_lib.FORM_SPLIT_FWD | _lib.FORM_SPLIT_BWD | _lib.FORM_SOFT_SPLIT)
+    _lib.set_test_forms(0)

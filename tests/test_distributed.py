@@ -233,3 +233,131 @@ def test_early_reduce_fixed_order_world2():
     for _, g0, g1 in res:
         np.testing.assert_array_equal(g0, 2 * np.arange(4.) + 10)
         np.testing.assert_array_equal(g1, 2 * np.arange(7.) - 3)
+
+
+# --------------------------------------------------------------------------------------------
+# dibr_step's collective order when one rank produces no shared gradient
+# --------------------------------------------------------------------------------------------
+def _no_shared_grad_worker(rank, world, port, q):
+    """dibr_step with a shared feature table that only rank 0's render uses: rank 1's hook never
+    fires, so its EarlyReduce issues the table's all-reduce (zeros) only at flush().  Both ranks
+    must issue [table, vertices] in that order (different sizes: a mismatch fails under gloo or
+    mixes up the sums).  The local gradients are computed first, with no process group."""
+    import types
+    verts, faces, face_uvs = workloads.uv_sphere(6, 5, seed=0)
+    F = faces.shape[0]
+    cam = workloads.orbit_cameras(2, 0.3, first_view=2 * rank, total_views=4)
+    proj = workloads.generate_perspective_projection(math.pi / 4)
+    g_feat, g_soft = workloads.view_grads(2 * rank, 2, 4, 5, 3)
+
+    def render(height, width, fvz, fvi, feats, nz, sigmainv, boxlen, knum):
+        base = (fvi * fvi).sum() + (feats.sum() if rank == 0 else 0.)
+        B = fvi.shape[0]
+        return (base * torch.ones(B, height, width, 3), base * torch.ones(B, height, width),
+                torch.zeros(B, height, width, dtype=torch.long))
+
+    def run():
+        v = verts.clone().requires_grad_(True)
+        table = torch.ones(1, F, 3, 3).requires_grad_(True)
+        distributed.dibr_step(v, faces, proj, cam, table, 4, 5, g_feat, g_soft, shared=(table,),
+                              prepare=_prepare, render=render)
+        return types.SimpleNamespace(v=v.grad.detach().clone(),
+                                     t=None if table.grad is None else table.grad.detach().clone())
+
+    try:
+        local = run()
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                          WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+        distributed.init_from_env('gloo')
+        red = run()
+        q.put((rank, local.v.numpy(), None if local.t is None else local.t.numpy(),
+               red.v.numpy(), red.t.numpy()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, 'error', repr(e), None, None))
+
+
+def test_dibr_step_rank_without_shared_grad_world2():
+    res = _run_world(_no_shared_grad_worker)
+    (_, v0, t0, rv0, rt0), (_, v1, t1, rv1, rt1) = res
+    assert t0 is not None and t1 is None  # only rank 0 produced a table gradient
+    for rv, rt in ((rv0, rt0), (rv1, rt1)):
+        np.testing.assert_allclose(rv, v0 + v1, rtol=1e-6)
+        np.testing.assert_allclose(rt, t0, rtol=1e-6)
+
+
+# --------------------------------------------------------------------------------------------
+# GradBucket keeps each gradient's dtype
+# --------------------------------------------------------------------------------------------
+def _mixed_dtype_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        distributed.init_from_env('gloo')
+        a = torch.zeros(4, requires_grad=True)
+        b = torch.zeros(3, dtype=torch.float64, requires_grad=True)
+        c = torch.zeros(2, requires_grad=True)
+        a.grad = torch.full((4,), 1. + rank)
+        b.grad = torch.full((3,), 1. + 1e-12 * (rank + 1), dtype=torch.float64)
+        c.grad = torch.full((2,), 3. * rank)
+        bucket = distributed.GradBucket([a, b, c])
+        bucket.pack()
+        bucket.reduce()
+        q.put((rank, a.grad.numpy().copy(), b.grad.numpy().copy(), c.grad.numpy().copy(),
+               str(b.grad.dtype)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, 'error', repr(e), None, None))
+
+
+def test_grad_bucket_mixed_dtypes_world2():
+    for _, ga, gb, gc, dt in _run_world(_mixed_dtype_worker):
+        assert dt == 'torch.float64'
+        np.testing.assert_array_equal(ga, np.full(4, 3.))
+        np.testing.assert_allclose(gb, np.full(3, 2. + 3e-12), rtol=1e-15)  # not through fp32
+        assert np.all(gb - 2. > 2e-12)
+        np.testing.assert_array_equal(gc, np.full(2, 3.))
+
+
+# --------------------------------------------------------------------------------------------
+# bench.py's workload through the product's sharded step (test doubles for the GPU stages)
+# --------------------------------------------------------------------------------------------
+def _bench_args():
+    import types
+    return types.SimpleNamespace(dtype='f32', config='c1', sigmainv=7000., boxlen=0.02,
+                                 knum=30, iou=None)
+
+
+def _bench_rank_step(first, n, total):
+    import bench
+    wl = bench.Workload(_bench_args(), torch.device('cpu'), first, n, total)
+    distributed.dibr_step(wl.vertices, wl.faces, wl.proj, wl.cam, wl.feats, wl.H, wl.W,
+                          wl.g_feat, wl.g_soft, prepare=_prepare, render=_render, **wl.kw)
+    return wl.vertices.grad.detach().clone().numpy()
+
+
+def _bench_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        r, wsz, _ = distributed.init_from_env('gloo')
+        first, n = distributed.shard_views(3, r, wsz)
+        q.put((r, _bench_rank_step(first, n, 3)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:
+        q.put((rank, 'error', repr(e)))
+
+
+def test_bench_workload_sharded_world2():
+    """bench.Workload (C1 shapes, 3 views over 2 ranks: uneven shards) through dibr_step: the
+    all-reduced vertex gradient equals the single-process one over all views."""
+    import oracle
+    oracle.lib()
+    res = _run_world(_bench_worker)
+    ref = _bench_rank_step(0, 3, 3)
+    assert np.abs(ref).sum() > 0
+    for _, g in res:
+        np.testing.assert_allclose(g, ref, rtol=1e-4, atol=1e-5)

@@ -245,34 +245,23 @@ def test_reference_op_form_raw_vs_oracle(dt, knum, boxes):
 
 
 # --------------------------------------------------------------------------------------------
-# the per-pixel waves, the cell-major forward (debug flag 1024) and the pooled one (2048)
+# the forward on shapes the sphere rows do not reach: pixel grids with NaN pixels, dense soups
 # --------------------------------------------------------------------------------------------
-def _both_kernels(px, rr, fvz, fvi, feat, knum, raw_boxes=None):
-    """The per-pixel (default), cell-major (flag 1024) and pooled (flag 2048) forwards: identical."""
-    from kaolin_amd import _C, _lib
+def _forward(px, rr, fvz, fvi, feat, knum, raw_boxes=None):
+    """The forward through the API (raw_boxes None) or the raw op."""
+    from kaolin_amd import _C
     from kaolin_amd.render.mesh import deftet_sparse_render
-    out = []
-    for flags in (0, 1024, 2048):
-        _lib.load().kd_debug_set(flags)
-        try:
-            if raw_boxes is None:
-                interp, fidx = deftet_sparse_render(T(px), T(rr), T(fvz), T(fvi), T(feat), knum)
-                out.append((N(interp), N(fidx)))
-            else:
-                r = _C.render.mesh.deftet_sparse_render_forward_cuda(
-                    T(fvz), T(fvi), T(raw_boxes), T(px), T(rr), knum, 1e-8)
-                out.append(tuple(N(t) for t in r))
-        finally:
-            _lib.load().kd_debug_set(0)
-    for other in out[1:]:
-        for a, b in zip(out[0], other):
-            np.testing.assert_array_equal(a, b)
-    return out[0]
+    if raw_boxes is None:
+        interp, fidx = deftet_sparse_render(T(px), T(rr), T(fvz), T(fvi), T(feat), knum)
+        return N(interp), N(fidx)
+    r = _C.render.mesh.deftet_sparse_render_forward_cuda(
+        T(fvz), T(fvi), T(raw_boxes), T(px), T(rr), knum, 1e-8)
+    return tuple(N(t) for t in r)
 
 
 @pytest.mark.parametrize('dt', [np.float32, np.float64])
 @pytest.mark.parametrize('knum', [1, 8, 30, 32])
-def test_pooled_matches_wave_kernel_sphere_grid(dt, knum):
+def test_forward_sphere_grid(dt, knum):
     """A pixel grid over a rendered sphere (the bench row's shape: neighbouring pixels share
     cells), a ragged last workgroup (P not a multiple of 64), pixels off the grid's [-1, 1]
     range and NaN pixels."""
@@ -289,7 +278,7 @@ def test_pooled_matches_wave_kernel_sphere_grid(dt, knum):
     px[0, 5] = np.nan
     px[0, 77, 1] = np.nan
     rr = np.broadcast_to(np.array([-1e9, 0.], dt), (1, H * W, 2)).copy()
-    interp, fidx = _both_kernels(px, rr, fvz, fvi, feat, knum)
+    interp, fidx = _forward(px, rr, fvz, fvi, feat, knum)
     assert (fidx >= 0).any()
     oi, of, _ = f3.deftet_forward(px, rr, fvz, fvi, feat, knum)
     np.testing.assert_array_equal(fidx, of)
@@ -298,54 +287,16 @@ def test_pooled_matches_wave_kernel_sphere_grid(dt, knum):
 
 @pytest.mark.parametrize('dt', [np.float32, np.float64])
 @pytest.mark.parametrize('size', [0.15, 0.6, 2.0])
-def test_pooled_overflow_falls_back(dt, size):
-    """Soups from a few candidates per pixel (all pooled) to hundreds (the 1024-candidate pool
-    overflows, those pixels take the per-pixel path inside the same launch), sorted and raw."""
+def test_forward_dense_soups(dt, size):
+    """Soups from a few candidates per pixel to hundreds, sorted and raw."""
     px, rr, fvz, fvi, feat = soup(2, 2000, 333, dt, 11, size=size, nan_faces=3)
     knum = 24
-    interp, fidx = _both_kernels(px, rr, fvz, fvi, feat, knum)
+    interp, fidx = _forward(px, rr, fvz, fvi, feat, knum)
     oi, of, _ = f3.deftet_forward(px, rr, fvz, fvi, feat, knum)
     np.testing.assert_array_equal(fidx, of)
     np.testing.assert_array_equal(interp, oi)
     bbox = np.concatenate([fvi.min(2), fvi.max(2)], -1)
-    raw = _both_kernels(px, rr, fvz, fvi, feat, knum, raw_boxes=bbox)
+    raw = _forward(px, rr, fvz, fvi, feat, knum, raw_boxes=bbox)
     ofi, od, oa0, oa1 = f3.deftet_forward_raw(px, rr, fvz, fvi, bbox, knum)
     for a, b in zip(raw, (ofi, od, oa0, oa1)):
         np.testing.assert_array_equal(a, b)
-
-
-@pytest.mark.parametrize('dt', [np.float32, np.float64])
-def test_small_workspace_takes_the_per_pixel_kernel(dt):
-    from kaolin_amd import _lib as _l
-    _l.load().kd_debug_set(1024)  # ask for the cell-major kernel: the small workspace refuses it
-    try:
-        _small_workspace(dt)
-    finally:
-        _l.load().kd_debug_set(0)
-
-
-def _small_workspace(dt):
-    """A caller sizing the workspace with kd_deftet_workspace_size (no pixel count) gets the
-    per-pixel kernel and the same results as the cell-major one."""
-    from kaolin_amd import _lib
-    from kaolin_amd.render.mesh import deftet_sparse_render
-    px, rr, fvz, fvi, feat = soup(1, 1500, 500, dt, 5, size=0.5)
-    knum = 12
-    interp0, fidx0 = deftet_sparse_render(T(px), T(rr), T(fvz), T(fvi), T(feat), knum)
-    lib = _lib.load()
-    dp = 1 if dt == np.float64 else 0
-    small = int(lib.kd_deftet_workspace_size(1, 1500, dp))
-    assert small < int(lib.kd_deftet_workspace_size_p(1, 500, 1500, dp))
-    ws = torch.empty((small,), dtype=torch.uint8, device=DEV)
-    tdt = torch.float32 if dt == np.float32 else torch.float64
-    interp = torch.empty((1, 500, knum, 3), device=DEV, dtype=tdt)
-    fidx = torch.empty((1, 500, knum), device=DEV, dtype=torch.long)
-    wts = torch.empty((1, 500, knum, 3), device=DEV, dtype=tdt)
-    ins = [T(a) for a in (px, rr, fvz, fvi, feat)]
-    p = lambda t: t.data_ptr()  # noqa: E731
-    sfx = 'f64' if dp else 'f32'
-    _lib.call(f'kd_deftet_sparse_render_forward_{sfx}', 1, 500, 1500, knum, 3,
-              *(p(t) for t in ins), 1e-8, p(interp), p(fidx), p(wts), p(ws), small,
-              torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
-    assert torch.equal(fidx, fidx0) and torch.equal(interp, interp0)

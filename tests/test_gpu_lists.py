@@ -64,7 +64,7 @@ def test_lists_vs_oracle(dname, knum):
 def test_op_backward_on_lists_with_holes(dname, knum):
     """The op backward reads given lists and stops at a row's first -1, whatever follows it
     (dibr_soft_mask_cuda.cu:273-276): rows with a -1 punched into slot 3 must drop their later
-    entries -- in the coalesced form and in the lane-per-pixel form (debug flag 1 << 29)."""
+    entries."""
     from kaolin_amd import _C, _lib
     dt = TORCH_DTYPES[dname]
     fvi, face_idx = _view(100, 51, 256, 2, dt, elevation=0.7)
@@ -81,12 +81,7 @@ def test_op_backward_on_lists_with_holes(dname, knum):
     ref = oracle.soft_mask_backward(N(gs), N(soft), N(face_idx), N(prob), N(holes), N(ctype),
                                     N(sfvi), sig, M)
     tol = 1e-4 if dname == 'f32' else 1e-9
-    for flags in (0, 1 << 29):
-        _lib.load().kd_debug_set(flags)
-        try:
-            gop = _C.render.mesh.dibr_soft_mask_backward_cuda(gs, soft, face_idx, prob, holes,
-                                                              ctype, sfvi, sig, M)
-            torch.cuda.synchronize()
-        finally:
-            _lib.load().kd_debug_set(0)
-        np.testing.assert_allclose(N(gop), ref, rtol=tol, atol=tol * 0.1 * np.abs(ref).max())
+    gop = _C.render.mesh.dibr_soft_mask_backward_cuda(gs, soft, face_idx, prob, holes, ctype,
+                                                      sfvi, sig, M)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(N(gop), ref, rtol=tol, atol=tol * 0.1 * np.abs(ref).max())

@@ -696,7 +696,7 @@ def test_dibr_rasterization_fused_matches_composition(dname):
 @pytest.mark.parametrize('D', [3, 5])
 def test_dibr_fused_launches_match_split_launches(D):
     """dibr_rasterization's one-launch forward (kd_dibr_fwd_tiles) and backward (kd_dibr_bwd)
-    against the same tile bodies as separate launches (debug flags 1<<26, 1<<24) on a 50k-face
+    against the same tile bodies as separate launches (kd_set_test_forms) on a 50k-face
     mesh: identical forward outputs, gradients to summation-order tolerance.  (D = 5 keeps the
     fused forward and the split backward.)"""
     import math
@@ -714,11 +714,10 @@ def test_dibr_fused_launches_match_split_launches(D):
     feats = torch.rand((B, F, 3, D), generator=gen).to(DEV)
     g1 = torch.rand((B, h, w, D), generator=gen).to(DEV)
     g2 = torch.rand((B, h, w), generator=gen).to(DEV)
-    lib = _lib.load()
     out = []
     try:
-        for flags in (0, (1 << 24) | (1 << 26)):
-            lib.kd_debug_set(flags)
+        for forms in (0, _lib.FORM_SPLIT_FWD | _lib.FORM_SPLIT_BWD):
+            _lib.set_test_forms(forms)
             fa = fvi.detach().clone().requires_grad_(True)
             ft = feats.clone().requires_grad_(True)
             i, s, f = dibr_rasterization(h, w, fvc[..., 2], fa, ft, nrm[..., 2])
@@ -726,7 +725,7 @@ def test_dibr_fused_launches_match_split_launches(D):
             torch.cuda.synchronize()
             out.append((i, s, f, fa.grad, ft.grad))
     finally:
-        lib.kd_debug_set(0)
+        _lib.set_test_forms(0)
     (i0, s0, f0, ga0, gf0), (i1, s1, f1, ga1, gf1) = out
     assert (s0 < 1).any() and (f0 >= 0).any()
     assert torch.equal(f0, f1) and torch.equal(i0, i1) and torch.equal(s0, s1)
