@@ -254,41 +254,20 @@ def _median_over_ranks(xs, dev, world):
     return m
 
 
-def kernel_map(wl, steps, use_graph, lists):
-    """Per-kernel durations from the library's HIP events on the launch stream: recorded while a
-    second copy of the step's graph is captured (the events are graph nodes) and read after each
-    of `steps` replays -- the launches the timed region runs, in the same back-to-back order.
-    Without a graph (or if the capture with events fails): eager launches of the step.
+def kernel_map(wl, steps, lists):
+    """Per-kernel durations from the library's HIP events on the launch stream, over `steps`
+    eager launches of the step (events cannot be recorded inside the captured graph on this
+    stack: the capture leaves the context unusable).  The graph replays' own per-kernel
+    durations are in the committed rocprofv3 kernel traces (tools/trace_steps.py).
     Returns ({name: (total ms, launches)}, source, face_idx)."""
-    if use_graph:
-        try:
-            _lib.profile_collect()
-            gs = distributed.GraphedStep(wl.params, wl.forward_backward, params_to_reduce=[],
-                                         capture_hook=_lib.profile_enable)
-            tot = {}
-            for _ in range(steps):
-                face_idx = gs.replay()
-                torch.cuda.synchronize()
-                for k, (ms, c) in _lib.profile_collect(keep=True).items():
-                    a, n = tot.get(k, (0.0, 0))
-                    tot[k] = (a + ms, n + c)
-            _lib.profile_collect()
-            del gs
-            if tot:
-                return tot, 'hip graph replays (library events captured as graph nodes)', face_idx
-        except Exception as e:  # noqa: BLE001 -- fall back to eager launches
-            _lib.profile_enable(False)
-            _lib.profile_collect()
-            torch.cuda.synchronize()
-            print(f'[bench] graph event capture failed ({type(e).__name__}: {e}); eager map',
-                  file=sys.stderr)
     with dibr.close_lists(lists):
         _lib.profile_enable(True)
         for _ in range(steps):
             face_idx = wl.eager_step()
         torch.cuda.synchronize()
         _lib.profile_enable(False)
-    return _lib.profile_collect(), 'eager launches', face_idx
+    return _lib.profile_collect(), 'eager launches (HIP events around each library launch)', \
+        face_idx
 
 
 def load_pmc(path, config, dtype, lists, views):
@@ -358,7 +337,6 @@ def main():
     with dibr.close_lists(args.lists):
         wl = Workload(args, dev, first, n, total)
         step, launch = make_step(wl, use_graph)
-        graphed = isinstance(step, distributed.GraphedStep)
         elapsed, evt = timed(step, args.steps, args.warmup, dev, world)
     ms_per_step = elapsed * 1e3 / args.steps
     step_median = _median_over_ranks(evt['step_ms'], dev, world)
@@ -379,8 +357,8 @@ def main():
                 'global_batch': B_global * world}
         del step2, wl2
 
-    # ---- per-kernel durations: HIP events on the launch stream, over graph replays ---------
-    prof, prof_src, face_idx = kernel_map(wl, args.steps, graphed, args.lists)
+    # ---- per-kernel durations: HIP events recorded on the launch stream, eager pass ---------
+    prof, prof_src, face_idx = kernel_map(wl, args.steps, args.lists)
     covered = int((face_idx >= 0).sum().item())
 
     fvz, fvi, nz = wl.inputs()

@@ -53,9 +53,6 @@ int kd_version(void);
  * kd_profile_kernel_name(id) names them.  Not for use under stream capture. */
 void kd_profile_enable(int on);
 int kd_profile_collect(double *total_ms, int64_t *launches, int n);
-/* The same; keep != 0 leaves the recorded events in place (events recorded while a HIP graph
- * was captured are graph nodes: read them again after every replay, then once with keep = 0). */
-int kd_profile_collect_keep(double *total_ms, int64_t *launches, int n, int keep);
 const char *kd_profile_kernel_name(int id);
 
 /* Diagnostics only: ablation switches read by the kernels of the diagnostic build

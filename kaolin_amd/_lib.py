@@ -119,8 +119,6 @@ def load():
             lib.kd_profile_enable.restype = None
             lib.kd_profile_collect.argtypes = [c_p, c_p, c_int]
             lib.kd_profile_collect.restype = c_int
-            lib.kd_profile_collect_keep.argtypes = [c_p, c_p, c_int, c_int]
-            lib.kd_profile_collect_keep.restype = c_int
             lib.kd_profile_kernel_name.argtypes = [c_int]
             lib.kd_profile_kernel_name.restype = ctypes.c_char_p
             lib.kd_debug_set.argtypes = [c_int]
@@ -204,15 +202,13 @@ def profile_enable(on=True):
     load().kd_profile_enable(1 if on else 0)
 
 
-def profile_collect(keep=False):
-    """{kernel name: (total ms, launches)} for the launches recorded since the last collect
-    (keep: leave the events for another read -- those of a captured graph, after each replay)."""
+def profile_collect():
+    """{kernel name: (total ms, launches)} for the launches recorded since the last collect."""
     lib = load()
     n = 32
     ms = (ctypes.c_double * n)()
     cnt = (ctypes.c_int64 * n)()
-    k = lib.kd_profile_collect_keep(ctypes.cast(ms, c_p), ctypes.cast(cnt, c_p), n,
-                                    1 if keep else 0)
+    k = lib.kd_profile_collect(ctypes.cast(ms, c_p), ctypes.cast(cnt, c_p), n)
     return {lib.kd_profile_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(k) if cnt[i]}
 
 

@@ -109,14 +109,11 @@ int kd_debug_buffer(void *device_ptr) {
   return KD_OK;
 }
 
-int kd_profile_collect_keep(double *total_ms, int64_t *launches, int n, int keep) {
+int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
   std::vector<kd::Rec> recs;
   {
     std::lock_guard<std::mutex> lk(kd::g_prof_mu);
-    if (keep)
-      recs = kd::g_recs;
-    else
-      recs.swap(kd::g_recs);
+    recs.swap(kd::g_recs);
   }
   for (auto &r : recs) {
     float ms = 0.f;
@@ -125,16 +122,10 @@ int kd_profile_collect_keep(double *total_ms, int64_t *launches, int n, int keep
       if (total_ms) total_ms[r.id] += ms;
       if (launches) launches[r.id] += 1;
     }
-    if (!keep) {
-      (void)hipEventDestroy(r.start);
-      (void)hipEventDestroy(r.stop);
-    }
+    (void)hipEventDestroy(r.start);
+    (void)hipEventDestroy(r.stop);
   }
   return kd::K_NUM_KERNELS;
-}
-
-int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
-  return kd_profile_collect_keep(total_ms, launches, n, 0);
 }
 
 const char *kd_profile_kernel_name(int id) {

@@ -105,9 +105,12 @@ struct RasterPairsLDS {
 // Tile tl of view b (nbin: faces of its coarse bin, or -1).  Each thread owns pixel
 // (t.px, t.py) of tile_geom(H, W, tl) and writes its outputs; wave w tests its own sub-tile's
 // 64-face chunks.
-template <typename T>
+// CLK (diagnostics, kd_dibr_fwd_tiles<true>): the wall clock at the end of the walk and tests
+// (before the epilogue) into clk[slot].
+template <typename T, bool CLK = false>
 __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int b, int tl,
-                                                  int nbin, RasterPairsLDS<T> &S) {
+                                                  int nbin, RasterPairsLDS<T> &S,
+                                                  long long *clk = nullptr) {
   constexpr bool kF64 = sizeof(T) == 8;
   TileLists &L = S.L;
   auto &s_geo = S.geo;
@@ -151,39 +154,82 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
       s_cull[1][k] = a.bb.cull[2 * fi + 1];
     }
   };
+  // CLK: per-wave cycle counts of the phases (wave 0's are written out): [0] pass A row
+  // intervals + transpose + scan, [1] pair placement, [2] pass B, [4] chunks, [5] candidate
+  // pairs, [7] batches
+  long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto now_clk = [&]() -> long long {
+    return CLK ? (long long)__builtin_readcyclecounter() : 0ll;
+  };
   // B: the reference's per-pixel test (rasterization_cuda.cu:131-162) over the current batch
   auto test_batch = [&](int total) {
+    const long long tb0 = now_clk();
+    struct Acc {
+      long long &c, t0;
+      bool on;
+      __device__ ~Acc() {
+        if (on) c += (long long)__builtin_readcyclecounter() - t0;
+      }
+    } acc{cyc[2], tb0, CLK};
     if (ablate(fs.dbg, 16)) return;
     wave_lds_sync();
+    // branch-free (all three quotients, every load issued up front, selects), so the LDS reads
+    // and the three division chains interleave: one wave per SIMD (small batches) would
+    // otherwise wait out each dependent step
+    struct PairIn {
+      int q, f;
+      T g[9];
+      bool valid;
+    };
+    auto pair_load = [&](int e, PairIn &P) {
+      P.valid = e < total;
+      const int pr = s_pair[w][P.valid ? e : 0];  // pair: (pixel << 8) | entry
+      P.q = (pr >> 8) & 63;
+      const int k = L.sub[w][pr & 255];
+#pragma unroll
+      for (int i = 0; i < 9; ++i) P.g[i] = s_geo[i][k];
+      P.f = L.f[k];
+    };
+    auto pair_key = [&](const PairIn &P, unsigned long long &key, bool &nan_hit, T &zout) {
+      const float x0 = sx * (float)(2 * (t.WX0 + (P.q & 7)) + 1 - W);
+      const float y0 = sy * (float)(H - 2 * (t.WY0 + (P.q >> 3)) - 1);
+      const T a_edge_x = P.g[0] - (T)x0, a_edge_y = P.g[1] - (T)y0;
+      const T b_edge_x = P.g[2] - (T)x0, b_edge_y = P.g[3] - (T)y0;
+      const T c_edge_x = P.g[4] - (T)x0, c_edge_y = P.g[5] - (T)y0;
+      const T w0 = b_edge_x * c_edge_y - b_edge_y * c_edge_x;
+      const T w1 = c_edge_x * a_edge_y - c_edge_y * a_edge_x;
+      const T w2 = a_edge_x * b_edge_y - a_edge_y * b_edge_x;
+      T norm = w0 + w1 + w2;
+      norm = (T)((double)norm + copysign((double)a.eps, (double)norm));
+      // rasterization_cuda.cu:131-162 (raster_face_test's sequence, without its branches)
+      const T q0 = w0 / norm, q1 = w1 / norm, q2 = w2 / norm;
+      const bool in = P.valid && !(q0 < (T)0. || q1 < (T)0. || q2 < (T)0.);
+      const T z0 = q0 * P.g[6] + q1 * P.g[7] + q2 * P.g[8];
+      nan_hit = in && isnan(z0);
+      const bool ok = in && !isnan(z0) && z0 != (T)-INFINITY;
+      float zk;  // fp64: the depth rounded down to fp32 in the key, the exact one in zx
+      if constexpr (kF64)
+        zk = __double2float_rd((double)z0);
+      else
+        zk = (float)z0;
+      const unsigned long long packed = ((unsigned long long)ordered_f32(zk) << 32) |
+                                        (unsigned long long)(0xffffffffu - (uint32_t)P.f);
+      key = packed & (0ull - (unsigned long long)ok);
+      zout = z0;
+    };
     for (int e0 = 0; e0 < total; e0 += kWave) {
-      const int e = e0 + lane;
-      if (e < total) {
-        const int pr = s_pair[w][e];  // pair: (pixel << 8) | entry
-        const int q = (pr >> 8) & 63, k = L.sub[w][pr & 255];
-        const int ox = t.WX0, oy = t.WY0;
-        const int krow = kw;
-        const float x0 = sx * (float)(2 * (ox + (q & 7)) + 1 - W);
-        const float y0 = sy * (float)(H - 2 * (oy + (q >> 3)) - 1);
-        T w0, w1, w2, z0;
-        if (raster_face_test<T, false>((T)x0, (T)y0, s_geo[0][k], s_geo[1][k], s_geo[2][k],
-                                       s_geo[3][k], s_geo[4][k], s_geo[5][k], s_geo[6][k],
-                                       s_geo[7][k], s_geo[8][k], a.eps, w0, w1, w2, z0)) {
-          if (isnan(z0)) {
-            atomicOr(&s_nan[krow], 1ull << q);
-          } else if (z0 != (T)-INFINITY) {
-            // fp64: the depth rounded down to fp32 in the key, the exact one in zx
-            float zk;
-            if constexpr (kF64)
-              zk = __double2float_rd((double)z0);
-            else
-              zk = (float)z0;
-            const unsigned long long key =
-                ((unsigned long long)ordered_f32(zk) << 32) |
-                (unsigned long long)(0xffffffffu - (uint32_t)L.f[k]);
-            atomicMax(&s_key[krow][q], key);
-            if constexpr (kF64) atomicMax(&S.zx[krow][q], ordered_f64((double)z0));
-          }
-        }
+      PairIn pa;
+      pair_load(e0 + lane, pa);
+      unsigned long long ka;
+      bool na;
+      T za;
+      pair_key(pa, ka, na, za);
+      if (ka) {
+        atomicMax(&s_key[kw][pa.q], ka);
+        if constexpr (kF64) atomicMax(&S.zx[kw][pa.q], ordered_f64((double)za));
+      }
+      if (__ballot(na)) {  // (rare) a NaN depth: the pixel replays the reference loop
+        if (na) atomicOr(&s_nan[kw], 1ull << pa.q);
       }
     }
     wave_lds_sync();
@@ -192,9 +238,12 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     if (ablate(fs.dbg, 1)) return;
     if (nsub == 0) return;
     int total = 0;
+    if (CLK) cyc[7] += 1;
 #pragma unroll 1
     for (int c = 0; c < 4; ++c) {
       if (c * kWave >= nsub) break;
+      long long tc0 = now_clk();
+      if (CLK) cyc[4] += 1;
       const int ls = w;
       const int ns = nsub;
       const int ox = t.WX0, oy = t.WY0;
@@ -235,24 +284,61 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
       uint64_t m = wave_transpose64(fm);
       const int cnt = __popcll(m);
       const int incl = wave_incl_scan(cnt);
-      int end_tot = total + __builtin_amdgcn_readlane(incl, 63);
-      int pos = total + incl - cnt;
+      const int ctot = __builtin_amdgcn_readlane(incl, 63);
+      if (CLK) {
+        const long long t1 = now_clk();
+        cyc[0] += t1 - tc0;
+        tc0 = t1;
+        cyc[5] += ctot;
+      }
+      // pairs placed rank-major: step r writes every pixel lane's r-th candidate, packed by
+      // the lanes still holding one (ballot + mbcnt), so every window of kRasterPairCap pairs
+      // is filled by all lanes at once -- pixel-major runs let only the few lanes whose runs
+      // cover a window work on it (the poles: ~2000 pairs per wave and chunk).  Pass B does
+      // not depend on the order (the key maximum).
+      (void)ctot;
+      int pos = total;
       const int qbits = (lane << 8) | (c << 6);
       while (true) {
-        while (m && pos < kRasterPairCap) {
-          s_pair[w][pos++] = (unsigned short)(qbits | (int)__builtin_ctzll(m));
-          m &= m - 1ull;
+        const bool act = m != 0ull;
+        const uint64_t am = __ballot(act);
+        if (!am) break;
+        const int n = __popcll(am);
+        const int slot = pos + mbcnt(am);
+        const unsigned short pr = (unsigned short)(qbits | (act ? (int)__builtin_ctzll(m) : 0));
+        const bool now = act && slot < kRasterPairCap;
+        if (now) s_pair[w][slot] = pr;
+        if (pos + n > kRasterPairCap) {  // the window filled within this step
+          if (CLK) {
+            const long long t1 = now_clk();
+            cyc[1] += t1 - tc0;
+            tc0 = t1;
+          }
+          test_batch(kRasterPairCap);
+          if (CLK) tc0 = now_clk();
+          if (act && !now) s_pair[w][slot - kRasterPairCap] = pr;
+          pos += n - kRasterPairCap;
+        } else {
+          pos += n;
         }
-        if (end_tot <= kRasterPairCap) break;
-        test_batch(kRasterPairCap);  // the batch is exactly full
-        pos -= kRasterPairCap;
-        end_tot -= kRasterPairCap;
+        m &= m - 1ull;
       }
-      total = end_tot;
+      if (CLK) {
+        const long long t1 = now_clk();
+        cyc[1] += t1 - tc0;
+        tc0 = t1;
+      }
+      total = pos;
     }
     if (total) test_batch(total);
   };
   tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
+  if (CLK && KD_DIAG && clk && threadIdx.x == 0) {
+    const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
+    clk[slot] = wall_clock64();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) clk[(1 + i) * nb + slot] = cyc[i];  // wave 0's phase counts
+  }
 
   if (!t.inimg || ablate(fs.dbg, 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;

@@ -250,20 +250,40 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
   s_pm[lane] = pm;
   s_off[lane] = (unsigned short)(incl - cnt);
   wave_lds_sync();
-  // pixel lanes: write own records, slots ascending with the face index
+  // pixel lanes: write own records, slots ascending with the face index; four selected faces
+  // per step, their LDS reads (entry -> face, the face's offset and pixel mask) issued together
+  // (one wave per SIMD at small batches: a dependent LDS chain per face is exposed latency)
   const uint64_t below = (1ull << lane) - 1ull;
   int slot = my_kid;
-  for (uint64_t m = sel; m; m &= m - 1ull) {
-    const int jj = __builtin_ctzll(m);
-    const int kk = L.sub[ls][c * kWave + jj];
-    SoftPairRec r;
-    r.row = (int32_t)(lo + L.f[kk]);
-    r.slot = (uint16_t)slot++;
-    r.q = (uint8_t)tile_q;
-    r.type = 0;
-    const int ri = base + s_off[jj] + __popcll(s_pm[jj] & below);
-    rec[ri] = r;
-    if (s_ridx) s_ridx[r.slot][ridx_q] = (unsigned short)ri;  // (slot, pixel) -> record
+  for (uint64_t m = sel; m;) {
+    constexpr int U = 4;
+    int jj[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      jj[u] = m ? (int)__builtin_ctzll(m) : -1;
+      m &= m - 1ull;  // (0 stays 0)
+    }
+    int kk[U], off[U];
+    uint64_t pmu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = jj[u] < 0 ? 0 : jj[u];
+      kk[u] = L.sub[ls][c * kWave + j];
+      off[u] = s_off[j];
+      pmu[u] = s_pm[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (jj[u] < 0) break;
+      SoftPairRec r;
+      r.row = (int32_t)(lo + L.f[kk[u]]);
+      r.slot = (uint16_t)slot++;
+      r.q = (uint8_t)tile_q;
+      r.type = 0;
+      const int ri = base + off[u] + __popcll(pmu[u] & below);
+      rec[ri] = r;
+      if (s_ridx) s_ridx[r.slot][ridx_q] = (unsigned short)ri;  // (slot, pixel) -> record
+    }
   }
   my_kid = slot;
   wave_lds_sync();
@@ -698,7 +718,8 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
     const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
     a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
   }
-  raster_pairs_tile<float>(ra, b, tl, nbin, U.r);
+  raster_pairs_tile<float, DIAG>(
+      ra, b, tl, nbin, U.r, DIAG && a.fs.tbuf ? a.fs.tbuf + 7ll * gridDim.x * gridDim.y : nullptr);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =

@@ -256,21 +256,59 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
   return x;
 }
 
-// 64x64 bit-matrix transpose across a wave: lane l bit j -> lane j bit l (block swaps).
-__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
+// x of lane (lane ^ SH), for the whole wave without the LDS crossbar (ds_bpermute): gfx950's
+// permlane swaps for 32 / 16, DPP for 8 / 4 / 2 / 1.  Both candidates are materialised before the
+// select (empty asm), so the cross-lane reads run with every lane active (a DPP or permlane read
+// issued under a partial EXEC would see `old` for the inactive source lanes).
+template <int SH>
+__device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
   const int lane = threadIdx.x & 63;
-  const uint64_t masks[6] = {0x00000000ffffffffull, 0x0000ffff0000ffffull,
-                             0x00ff00ff00ff00ffull, 0x0f0f0f0f0f0f0f0full,
-                             0x3333333333333333ull, 0x5555555555555555ull};
-#pragma unroll
-  for (int st = 0; st < 6; ++st) {
-    const int sh = 32 >> st;
-    const uint64_t mlo = masks[st];
-    const uint32_t ylo = (uint32_t)__shfl_xor((int)(uint32_t)x, sh);
-    const uint32_t yhi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), sh);
-    const uint64_t y = ((uint64_t)yhi << 32) | ylo;
-    x = (lane & sh) ? ((x & ~mlo) | ((y & ~mlo) >> sh)) : ((x & mlo) | ((y & mlo) << sh));
+  uint32_t a, b;
+  bool hi;
+  if constexpr (SH == 32) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    a = r[1];  // lanes 0..31: the upper half's values
+    b = r[0];  // lanes 32..63: the lower half's values
+    hi = lane >= 32;
+  } else if constexpr (SH == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    a = r[1];  // even rows: the odd rows' values
+    b = r[0];  // odd rows: the even rows' values
+    hi = (lane & 16) != 0;
+  } else if constexpr (SH == 8) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xf, 0xf, false);  // row_ror:8
+  } else if constexpr (SH == 4) {
+    a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xf, 0xf, false);  // row_shl:4
+    b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    hi = (lane & 4) != 0;
+  } else if constexpr (SH == 2) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, false);  // [2,3,0,1]
+  } else {
+    static_assert(SH == 1, "lane_xor: SH in {1, 2, 4, 8, 16, 32}");
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, false);  // [1,0,3,2]
   }
+  asm volatile("" : "+v"(a), "+v"(b));
+  return hi ? b : a;
+}
+
+template <int SH>
+__device__ __forceinline__ uint64_t transpose_step(uint64_t x, uint64_t mlo) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t ylo = lane_xor<SH>((uint32_t)x);
+  const uint32_t yhi = lane_xor<SH>((uint32_t)(x >> 32));
+  const uint64_t y = ((uint64_t)yhi << 32) | ylo;
+  return (lane & SH) ? ((x & ~mlo) | ((y & ~mlo) >> SH)) : ((x & mlo) | ((y & mlo) << SH));
+}
+
+// 64x64 bit-matrix transpose across a wave: lane l bit j -> lane j bit l (block swaps).
+// Every lane of the wave must be active.
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
+  x = transpose_step<32>(x, 0x00000000ffffffffull);
+  x = transpose_step<16>(x, 0x0000ffff0000ffffull);
+  x = transpose_step<8>(x, 0x00ff00ff00ff00ffull);
+  x = transpose_step<4>(x, 0x0f0f0f0f0f0f0f0full);
+  x = transpose_step<2>(x, 0x3333333333333333ull);
+  x = transpose_step<1>(x, 0x5555555555555555ull);
   return x;
 }
 

@@ -274,8 +274,7 @@ class GraphedStep:
     the zeroed-on-the-side gradient buffers) inside the graph: tests/test_gpu_graphed_step.py
     compares replays with eager steps."""
 
-    def __init__(self, params, fn, params_to_reduce=None, group=None, warmup=3,
-                 capture_hook=None):
+    def __init__(self, params, fn, params_to_reduce=None, group=None, warmup=3):
         self.params = list(params)  # every parameter whose .grad the step writes
         self.reduce = self.params if params_to_reduce is None else list(params_to_reduce)
         self.fn = fn
@@ -291,15 +290,9 @@ class GraphedStep:
         torch.cuda.current_stream().wait_stream(s)
         self._clear()
         self.graph = torch.cuda.CUDAGraph()
-        if capture_hook:  # e.g. the library's per-launch HIP events, captured as graph nodes
-            capture_hook(True)
-        try:
-            with torch.cuda.graph(self.graph):
-                self.out = fn()
-                self.bucket.pack()
-        finally:
-            if capture_hook:
-                capture_hook(False)
+        with torch.cuda.graph(self.graph):
+            self.out = fn()
+            self.bucket.pack()
 
     def _clear(self):
         for p in self.params:

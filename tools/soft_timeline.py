@@ -22,7 +22,7 @@ v = workloads.sphere_views(n_lon, n_lat, H, W, B, dev, elevation=elev)
 fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['normals_z']
 ntx, nty = (W + 15) // 16, (H + 15) // 16
 n = B * ntx * nty
-buf = torch.zeros(7 * n, dtype=torch.int64, device=dev)
+buf = torch.zeros(16 * n, dtype=torch.int64, device=dev)
 extra = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
 lib = _lib.load()
 lib.kd_debug_buffer(buf.data_ptr())
@@ -34,7 +34,7 @@ dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
 lib.kd_debug_set(0)
 lib.kd_debug_buffer(None)
-t = buf.view(7, n).cpu().numpy()
+t = buf.view(16, n).cpu().numpy()
 dur = t[1] / 100.0          # us (100 MHz wall clock)
 start = (t[2] - t[2].min()) / 100.0
 end = start + dur
@@ -77,15 +77,23 @@ if t[5].any():  # soft phase split: pass A (walk + records), pair math, product 
     rend = t[3]
     pa = np.where(t[5] > 0, (t[5] - rend) / 100.0, 0)
     pm = np.where((t[6] > 0) & (t[5] > 0), (t[6] - t[5]) / 100.0, 0)
-    print('slowest tiles: slot | raster us | soft: passA pairmath rest | soft_nbin unc | '
-          'raster_nbin | view tx ty')
+    # raster split: walk + tests (start -> t[7]) and the epilogue (t[7] -> t[3])
+    rw = np.where(t[7] > 0, (t[7] - t[2]) / 100.0, 0)
+    print('slowest tiles: slot | raster us (walk+tests epilogue) | soft: passA pairmath rest | '
+          'soft_nbin unc | raster_nbin | view tx ty')
     for i in np.argsort(end)[::-1][:15]:
         tv = int(tile[i]) // (ntx * nty)
         tt = int(tile[i]) % (ntx * nty)
-        print(f'  {i:5d} | {rdur[i]:6.1f} | {pa[i]:6.1f} {pm[i]:6.1f} '
+        print(f'  {i:5d} | {rdur[i]:6.1f} ({rw[i]:5.1f} {rdur[i] - rw[i]:5.1f}) | {pa[i]:6.1f} {pm[i]:6.1f} '
               f'{dur[i] - rdur[i] - pa[i] - pm[i]:6.1f} | {t[4][i]:5d} {u_slot[i]:4d} | '
               f'{nbin[i]:5d} | {tv} {tt % ntx} {tt // ntx}')
     print(f'sums (ms): passA {pa.sum() / 1e3:.2f} pairmath {pm.sum() / 1e3:.2f}')
+    # raster pass A / B split of wave 0 (core clock cycles; diag CLK counters)
+    print('raster wave 0 (kcycles): rows+transpose place passB dense | chunks pairs dense batches')
+    for i in np.argsort(rdur)[::-1][:8]:
+        c = t[8:16, i]
+        print(f'  slot {i:5d} raster {rdur[i]:5.1f} us: {c[0] / 1e3:7.1f} {c[1] / 1e3:7.1f} '
+              f'{c[2] / 1e3:7.1f} {c[3] / 1e3:7.1f} | {c[4]:4d} {c[5]:6d} {c[6]:4d} {c[7]:3d}')
 late = np.argsort(end)[::-1][:10]
 print('latest ending (slot, start, dur):', [(int(i), round(float(start[i]), 1),
                                             round(float(dur[i]), 1)) for i in late])
