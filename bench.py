@@ -311,6 +311,8 @@ def main():
                          '(the training loop\'s), fused into the renderer or as the composition')
     ap.add_argument('--no-weak', action='store_true', help='skip the N > 1 weak-scaling phase')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--tile-split', type=int, default=0, choices=[0, 1, 2, 4],
+                    help='workgroups per tile of the fused forward (kd_set_tile_split; 0: auto)')
     ap.add_argument('--pmc', default=None,
                     help='PMC traffic summary (default profiles/r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
@@ -324,6 +326,7 @@ def main():
     dev = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(dev)
     _lib.load()
+    _lib.set_tile_split(args.tile_split)
     soup = args.config in SOUP_CONFIGS
     B_global = SOUP_CONFIGS[args.config][3] if soup else CONFIGS[args.config][4]
     weak_main = args.views_per_gpu is not None

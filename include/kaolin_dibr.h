@@ -74,6 +74,13 @@ int kd_debug_buffer(void *device_ptr);
 #define KD_FORM_SOFT_SPLIT 4
 int kd_set_test_forms(int forms);
 
+/* Workgroups per 16x16 tile of dibr_rasterization's fp32 forward (a test and tuning hook; 0 by
+ * default = chosen from the batch's tile count against the device's workgroup slots).  With 2 or
+ * 4, each tile is rendered by that many workgroups (half / quarter tiles, several waves per 8x8
+ * sub-tile), so that a small batch's heavy tiles spread over more CUs; results are identical.
+ * Used only when the soft mask's record pool is the fixed one (knum <= 32, no pool limit). */
+int kd_set_tile_split(int split);
+
 /* Pool limits (a test and tuning hook; both 1 by default).  The workspaces hold two bounded
  * pools whose layout depends only on the call's sizes: the coarse bins (16 entries per face row)
  * and the soft mask's (pixel, close face) records (min(knum, 12) per pixel plus block slack).

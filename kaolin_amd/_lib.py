@@ -129,6 +129,8 @@ def load():
             lib.kd_set_pool_limits.restype = c_int
             lib.kd_set_test_forms.argtypes = [c_int]
             lib.kd_set_test_forms.restype = c_int
+            lib.kd_set_tile_split.argtypes = [c_int]
+            lib.kd_set_tile_split.restype = c_int
             lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
             lib.kd_prepare_vertices_ranges.restype = c_i64
             # diagnostic build only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
@@ -183,6 +185,13 @@ def set_test_forms(forms=0):
     """Run dibr_rasterization through the separate launches its one-launch kernels fuse
     (kd_set_test_forms, a test hook); 0 restores the default."""
     if load().kd_set_test_forms(int(forms)) != KD_OK:
+        raise RuntimeError(load().kd_last_error().decode(errors='replace'))
+
+
+def set_tile_split(split=0):
+    """Workgroups per tile of the fused fp32 forward (kd_set_tile_split, a test and tuning hook):
+    1, 2 or 4; 0 restores the automatic choice."""
+    if load().kd_set_tile_split(int(split)) != KD_OK:
         raise RuntimeError(load().kd_last_error().decode(errors='replace'))
 
 

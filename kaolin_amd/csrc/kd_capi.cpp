@@ -19,6 +19,8 @@ int debug_flags() { return g_debug.load(); }
 #endif
 std::atomic<int> g_forms{0};
 int test_forms() { return g_forms.load(); }
+std::atomic<int> g_split{0};
+int tile_split() { return g_split.load(); }
 std::atomic<long long *> g_tbuf{nullptr};
 std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
 float pool_limit_bins() { return g_lim_bins.load(); }
@@ -92,6 +94,13 @@ int kd_set_test_forms(int forms) {
   if (forms & ~(KD_FORM_SPLIT_FWD | KD_FORM_SPLIT_BWD | KD_FORM_SOFT_SPLIT))
     return kd::set_error(KD_ERR_INVALID_ARGUMENT, "unknown launch form bits 0x%x", forms);
   kd::g_forms.store(forms);
+  return KD_OK;
+}
+
+int kd_set_tile_split(int split) {
+  if (split != 0 && split != 1 && split != 2 && split != 4)
+    return kd::set_error(KD_ERR_INVALID_ARGUMENT, "tile split must be 0, 1, 2 or 4 (got %d)", split);
+  kd::g_split.store(split);
   return KD_OK;
 }
 

@@ -46,6 +46,8 @@ constexpr int debug_flags() { return 0; }
 // kd_set_test_forms (KD_FORM_* of kaolin_dibr.h): run dibr_rasterization through the separate
 // launches its one-launch kernels fuse (a test hook of both builds)
 int test_forms();
+// kd_set_tile_split: workgroups per tile of the fused fp32 forward (0: chosen by the batch size)
+int tile_split();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
 
 // Per-workgroup duration (wall clock, 100 MHz ticks) for diagnostics: written by thread 0 when

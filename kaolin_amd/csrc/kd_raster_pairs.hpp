@@ -107,10 +107,15 @@ struct RasterPairsLDS {
 // 64-face chunks.
 // CLK (diagnostics, kd_dibr_fwd_tiles<true>): the wall clock at the end of the walk and tests
 // (before the epilogue) into clk[slot].
-template <typename T, bool CLK = false>
+// SPLIT > 1 (kd_tile.hpp tile_geom_part): the workgroup is part `part` of the tile; the waves of
+// one sub-tile take its face chunks in turn (chunk c by role c % SPLIT) and post into the
+// sub-tile's key row, whose maximum does not depend on the order; role 0 writes the outputs.
+// uncm (nullptr: none): receives per sub-tile the mask of its uncovered in-image pixels.
+template <typename T, bool CLK = false, int SPLIT = 1>
 __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int b, int tl,
                                                   int nbin, RasterPairsLDS<T> &S,
-                                                  long long *clk = nullptr) {
+                                                  long long *clk = nullptr, int part = 0,
+                                                  uint64_t *uncm = nullptr) {
   constexpr bool kF64 = sizeof(T) == 8;
   TileLists &L = S.L;
   auto &s_geo = S.geo;
@@ -124,14 +129,15 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
-  TileGeom t = tile_geom(H, W, tl);
+  TileGeom t = SPLIT == 1 ? tile_geom(H, W, tl) : tile_geom_part<SPLIT>(H, W, tl, part);
   t.nbin = nbin;
-  const int kw = w;  // LDS key row of this wave's pixels
+  const int kw = t.sub;  // LDS key row of this wave's pixels
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
   {  // (the walk's first barrier orders these before any pass B)
     s_key[kw][lane] = 0ull;
     if (kF64) S.zx[kF64 ? kw : 0][lane] = 0ull;
     if (lane == 0) s_nan[kw] = 0ull;
+    if (uncm && lane == 0 && t.role == 0) uncm[t.sub] = 0ull;
   }
   // this wave's row centres relative to its first row
   const float ysub = px_cy(M, H, t.WY0);
@@ -240,7 +246,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     int total = 0;
     if (CLK) cyc[7] += 1;
 #pragma unroll 1
-    for (int c = 0; c < 4; ++c) {
+    for (int c = t.role; c < 4; c += SPLIT) {
       if (c * kWave >= nsub) break;
       long long tc0 = now_clk();
       if (CLK) cyc[4] += 1;
@@ -340,7 +346,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     for (int i = 0; i < 8; ++i) clk[(1 + i) * nb + slot] = cyc[i];  // wave 0's phase counts
   }
 
-  if (!t.inimg || ablate(fs.dbg, 8192)) return;
+  if (t.role != 0 || !t.inimg || ablate(fs.dbg, 8192)) return;
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
   const T x0 = (T)px_cx(M, W, t.px), y0 = (T)px_cy(M, H, t.py);
   int best = -1;
@@ -385,6 +391,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     }
   }
   a.face_idx[p] = best;
+  if (uncm && best < 0) atomicOr(&uncm[t.sub], 1ull << lane);
   T *wo = a.weights + p * 3;
   T *io = a.interp + p * a.D;
   if (best >= 0) {

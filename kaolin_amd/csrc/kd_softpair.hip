@@ -436,6 +436,7 @@ struct SoftPairsLDS {
   int nrec, ibase, box[4];
   double iou[8];  // iou_tile_terms
   int wbox[4][4];   // per wave: the box of its pixels that can still take a face (walk filter)
+  unsigned char gcnt[2][4][kWave];  // split tiles: per wave, each pixel's hits of its chunk
 };
 
 // Tile tl of view b (nbin: faces of its soft coarse bin, or -1).  Each thread owns pixel
@@ -467,9 +468,18 @@ __device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const Soft
   }
 }
 
-template <typename T, bool FUSED>
+// SPLIT > 1 (FUSED, fixed pool only; kd_tile.hpp tile_geom_part): the workgroup is part `part`
+// of the tile, with its own room of the tile's records (the part's pixels x K) and its own work
+// items; records keep the tile frame's pixel index q.  Pass A takes a sub-tile's chunks in groups
+// of SPLIT, chunk g * SPLIT + r by role r: each role counts its pixels' hits, and after one barrier
+// every role knows the hits of the roles before it, so a pixel's slots stay in face order (its
+// first K).  Role 0 forms the product and writes the pixel outputs.  uncm (nullptr: read
+// face_idx): per sub-tile, the mask of uncovered in-image pixels (the fused raster phase's).
+template <typename T, bool FUSED, int SPLIT = 1>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
-                                                int b, int tl, int nbin, SoftPairsLDS<FUSED> &S) {
+                                                int b, int tl, int nbin, SoftPairsLDS<FUSED> &S,
+                                                int part = 0, const uint64_t *uncm = nullptr) {
+  static_assert(SPLIT == 1 || FUSED, "split tiles: the fused soft mask only");
   TileLists &L = S.L;
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W, K = a.K;
@@ -477,14 +487,16 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
   const int nview = (int)(hi - lo);
-  TileGeom t = tile_geom(H, W, tl);
+  TileGeom t = SPLIT == 1 ? tile_geom(H, W, tl) : tile_geom_part<SPLIT>(H, W, tl, part);
   t.nbin = nbin;
+  const int tile_q = t.sub * kWave + lane;  // the pixel's index in the 16x16 tile frame
   if (KD_DIAG && fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, bin) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
   const int64_t p = ((int64_t)b * H + t.py) * W + t.px;
-  const bool unc = t.inimg && a.face_idx[p] < 0;
+  const bool unc = t.inimg && (uncm ? ((uncm[t.sub] >> lane) & 1ull) != 0ull : a.face_idx[p] < 0);
   const bool wave_unc = __ballot(unc) != 0ull;
+  const bool owner = t.role == 0;  // this lane writes the pixel's outputs
   const int64_t tile = (int64_t)b * pb.ntiles + tl;
   int my_kid = 0;
 
@@ -526,7 +538,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     // latency overlaps the walk's first loads (records are written after a barrier of
     // tile_rounds)
     if (pb.fixed) {
-      if (tid == 0) S.base = tile * kBlock * K;
+      if (tid == 0) S.base = tile * kBlock * K + (int64_t)part * (kBlock / SPLIT) * K;
     } else if (tid == 0) {
       const BinGeom &g = a.bb.g;
       const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
@@ -544,10 +556,39 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     t.FY1 = s_box[3];
     auto stage = [&](int, int64_t) {};  // pass A needs the spans only
     auto round = [&](int nsub, int) {
-      if (wave_unc && !ablate(fs.dbg, 1024)) {
-        for (int c = 0; c * kWave < nsub; ++c)
-          soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], &S.nrec,
-                             pb.rec + S.base, FUSED ? S.ridx : nullptr);
+      if constexpr (SPLIT == 1) {
+        if (wave_unc && !ablate(fs.dbg, 1024)) {
+          for (int c = 0; c * kWave < nsub; ++c)
+            soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], &S.nrec,
+                               pb.rec + S.base, FUSED ? S.ridx : nullptr);
+        }
+      } else {
+        // groups of SPLIT chunks (a workgroup-uniform count: every wave meets the barriers)
+        const int nmax = max(max(L.nsub[0], L.nsub[1]), max(L.nsub[2], L.nsub[3]));
+        constexpr int NS = 4 / SPLIT;
+        for (int g = 0; g * SPLIT * kWave < nmax; ++g) {
+          const int c = g * SPLIT + t.role;
+          const bool mine = wave_unc && c * kWave < nsub;  // (wave-uniform)
+          uint64_t hits = mine ? chunk_hits(L, w, nsub, c, t.WX0, t.WY0) : 0ull;
+          hits = (unc && my_kid < K) ? hits : 0ull;
+          const int cnt = __popcll(hits);
+          S.gcnt[g & 1][w][lane] = (unsigned char)cnt;
+          __syncthreads();
+          int before = 0, all = 0;
+#pragma unroll
+          for (int r = 0; r < SPLIT; ++r) {
+            const int x = S.gcnt[g & 1][r * NS + w % NS][lane];
+            before += r < t.role ? x : 0;
+            all += x;
+          }
+          int slot = my_kid + before;
+          const int take = min(cnt, max(K - slot, 0));
+          const uint64_t sel = take < cnt ? lowest_bits(hits, take) : hits;
+          if (mine)
+            soft_chunk_write(L, w, sel, c, lo, slot, S.pm[w], S.off[w], &S.nrec, pb.rec + S.base,
+                             S.ridx, tile_q, tile_q);
+          my_kid = min(K, my_kid + all);
+        }
       }
     };
     // once every uncovered pixel holds K close faces, later faces cannot enter; a tile without
@@ -616,7 +657,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     }
   }
   T sval = unc ? (T)0.0 : (T)1.0;  // this pixel's soft value (FUSED: the product below)
-  if (t.inimg) {
+  if (t.inimg && owner) {
     if (!FUSED) pb.npix[p] = my_kid;  // the split pipeline's reduce
     if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
     else if (a.soft && my_kid == 0) a.soft[p] = (T)0.0;
@@ -645,7 +686,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   if constexpr (FUSED) {
     zero_side_job(a);
     if (n == 0) {
-      iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
+      iou_tile_terms<T>(a, b, tl, p, t.inimg && owner, sval, S.iou);
       return;
     }
     // pair math over this tile's records (record order: coalesced reads; diag 32: none)
@@ -657,9 +698,9 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       fs.tbuf[6ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
           wall_clock64();
     // soft = 1 - prod(1 - p) in slot order (dibr_soft_mask_cuda.cu:174-181, double-promoted)
-    if (unc && my_kid > 0) {
+    if (unc && owner && my_kid > 0) {
       constexpr int U8 = 8;
-      const int rq = tid;  // the pixel's column of the record table
+      const int rq = tile_q;  // the pixel's column of the record table
       T prod = (T)1.0;
       for (int s0 = 0; s0 < my_kid; s0 += U8) {
         T pv[U8];
@@ -672,7 +713,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       sval = (T)(1.0 - (double)prod);
       a.soft[p] = sval;
     }
-    iou_tile_terms<T>(a, b, tl, p, t.inimg, sval, S.iou);
+    iou_tile_terms<T>(a, b, tl, p, t.inimg && owner, sval, S.iou);
   }
 }
 
@@ -701,15 +742,21 @@ union DibrTileLDS {
 // DIAG (debug flag 64 with a debug buffer): per dispatch slot the tile, its bin counts, start,
 // duration and raster-phase end (tools/soft_timeline.py).  A separate instantiation: the clock's
 // live registers alone make the kernel spill.
-template <bool DIAG>
+//
+// SPLIT (1, 2, 4; kd_tile.hpp tile_geom_part): each tile as SPLIT workgroups over a (tiles *
+// SPLIT, views) grid, for batches too small to fill the chip with whole tiles: a heavy tile's
+// raster chunks, pass A chunks and pair math spread over SPLIT CUs.  The raster phase hands the
+// soft phase its uncovered pixels through `uncm` (the soft phase's waves need not own them).
+template <bool DIAG, int SPLIT>
 __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
                                                               SoftArgs<float> a,
                                                               SoftPairBuf<float> pb) {
   __shared__ DibrTileLDS<float> U;
+  __shared__ uint64_t uncm[4];
   TileClock clk(DIAG ? a.fs.tbuf : nullptr, 1);
   if (DIAG) clk.start_to(2);
-  int b, tl, nbin;
-  tile_of_block(ra.bb, ra.fs.H, ra.fs.W, b, tl, nbin, ra.fs.dbg);
+  int b, tl, nbin, part;
+  tile_of_block_split<SPLIT>(ra.bb, ra.fs.H, ra.fs.W, b, tl, part, nbin, ra.fs.dbg);
   if (DIAG && a.fs.tbuf && threadIdx.x == 0) {
     const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
     a.fs.tbuf[slot] = ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
@@ -718,13 +765,14 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
     const int ct = (ty * kTile / g.ct) * g.nctx + (tx * kTile / g.ct);
     a.fs.tbuf[4 * nb + slot] = a.bb.totals[(int64_t)b * g.nct() + ct];
   }
-  raster_pairs_tile<float, DIAG>(
-      ra, b, tl, nbin, U.r, DIAG && a.fs.tbuf ? a.fs.tbuf + 7ll * gridDim.x * gridDim.y : nullptr);
+  raster_pairs_tile<float, DIAG, SPLIT>(
+      ra, b, tl, nbin, U.r, DIAG && a.fs.tbuf ? a.fs.tbuf + 7ll * gridDim.x * gridDim.y : nullptr,
+      part, uncm);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
-  soft_pairs_tile<float, true>(a, pb, b, tl, -1, U.s);
+  soft_pairs_tile<float, true, SPLIT>(a, pb, b, tl, -1, U.s, part, uncm);
 }
 
 // The fp64 DIB-R forward in one launch: the pair raster (fp64 test, fp64-culled candidates, the
@@ -1313,6 +1361,28 @@ int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
   return KD_OK;
 }
 
+// Workgroups per tile of the fused fp32 forward (kd_dibr_fwd_tiles SPLIT): the tile split hook
+// (kd_set_tile_split) when set, else by the batch's tile count against the chip's workgroup
+// slots.  Split tiles need the fixed record pool (every part owns its pixels' K records).
+static int fwd_tile_split(int64_t tiles, bool fixed_pool) {
+  if (!fixed_pool) return 1;
+  const int forced = tile_split();
+  if (forced > 0) return forced;
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  // measured at C3 (bench.py --tile-split, same box): 1 view (1024 tiles) 0.1177 / 0.1076 /
+  // 0.1170 ms per step at 1 / 2 / 4 workgroups per tile; 2 views (2048) 0.1388 / 0.1463 / 0.1624;
+  // 8 views 0.310 / 0.352.  A part repeats the tile's raster walk (~10 us of dependent loads at
+  // one wave per SIMD), so splitting pays only while the whole tiles fit one round of slots.
+  const int64_t slots = (int64_t)cus * 6;  // kd_dibr_fwd_tiles: 6 workgroups per CU
+  return tiles <= slots ? 2 : 1;
+}
+
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) {
   return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
          !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT));
@@ -1325,12 +1395,25 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
-    const dim3 grid((unsigned)pb.ntiles, ra.fs.B);
-    if (KD_DIAG && a.fs.tbuf)
-      hipLaunchKernelGGL((kd_dibr_fwd_tiles<KD_DIAG != 0>), grid, dim3(kBlock), 0, stream, ra, a,
-                         pb);
+    const int split = fwd_tile_split((int64_t)ra.fs.B * pb.ntiles, pb.fixed && !pool_may_overflow(a.K));
+    const dim3 grid((unsigned)pb.ntiles * split, ra.fs.B);
+    const bool diag = KD_DIAG && a.fs.tbuf;
+#define KD_FWD_TILES(S)                                                                         \
+  do {                                                                                        \
+    if (diag)                                                                                 \
+      hipLaunchKernelGGL((kd_dibr_fwd_tiles<KD_DIAG != 0, S>), grid, dim3(kBlock), 0, stream, \
+                         ra, a, pb);                                                          \
+    else                                                                                      \
+      hipLaunchKernelGGL((kd_dibr_fwd_tiles<false, S>), grid, dim3(kBlock), 0, stream, ra, a,  \
+                         pb);                                                                 \
+  } while (0)
+    if (split == 4)
+      KD_FWD_TILES(4);
+    else if (split == 2)
+      KD_FWD_TILES(2);
     else
-      hipLaunchKernelGGL((kd_dibr_fwd_tiles<false>), grid, dim3(kBlock), 0, stream, ra, a, pb);
+      KD_FWD_TILES(1);
+#undef KD_FWD_TILES
   }
   if (pool_may_overflow(a.K)) ovf_fwd_launch<float, true>(a, pb, stream);
   const hipError_t e = hipGetLastError();

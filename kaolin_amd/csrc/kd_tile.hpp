@@ -34,6 +34,8 @@ struct TileGeom {
   // the wave has none)
   int FX0, FX1, FY0, FY1;      // tile filter
   int SX0, SX1, SY0, SY1;      // this wave's sub-list filter
+  int sub;                     // this wave's 8x8 sub-tile in the 16x16 tile frame (0..3)
+  int role;                    // split tiles: which of the sub-tile's waves this is (0 owns pixels)
 };
 
 // (view, fine tile) of dispatch slot d of n tile slots: the bins' heaviest-first order
@@ -96,9 +98,85 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
   t.SX1 = t.WX1;
   t.SY0 = t.WY0;
   t.SY1 = t.WY1;
+  t.sub = w;
+  t.role = 0;
   return t;
 }
 __device__ __forceinline__ TileGeom tile_geom(int H, int W) { return tile_geom(H, W, blockIdx.x); }
+
+// Split tiles (few views: more workgroups than tiles fill the chip).  Part `part` of SPLIT (1, 2
+// or 4) of a 16x16 tile is a 256-thread workgroup over 4 / SPLIT of its 8x8 sub-tiles (SPLIT 2:
+// the upper or lower 16x8 half; SPLIT 4: one sub-tile), with SPLIT waves per sub-tile: wave w
+// takes sub-tile part * (4 / SPLIT) + w % (4 / SPLIT) in role w / (4 / SPLIT).  Every wave of a
+// sub-tile maps its lanes to the sub-tile's pixels; role 0 owns them (writes the outputs), the
+// other roles share the sub-tile's face chunks.  The workgroup's filter box is its part.
+template <int SPLIT>
+__device__ __forceinline__ TileGeom tile_geom_part(int H, int W, int tile, int part) {
+  static_assert(SPLIT == 1 || SPLIT == 2 || SPLIT == 4, "SPLIT in {1, 2, 4}");
+  constexpr int NS = 4 / SPLIT;  // sub-tiles per part
+  const int ntx = (W + kTile - 1) / kTile;
+  const int tx = tile % ntx, ty = tile / ntx;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int s = part * NS + w % NS;
+  TileGeom t;
+  // the part's pixel rect: the union of its sub-tiles (s0 .. s0 + NS - 1)
+  const int s0 = part * NS;
+  t.X0 = tx * kTile + (NS == 1 ? (s0 & 1) * 8 : 0);
+  t.Y0 = ty * kTile + (s0 >> 1) * 8;
+  t.X1 = min(t.X0 + (NS == 1 ? 7 : kTile - 1), W - 1);
+  t.Y1 = min(t.Y0 + (NS == 4 ? kTile - 1 : 7), H - 1);
+  t.WX0 = tx * kTile + (s & 1) * 8;
+  t.WY0 = ty * kTile + (s >> 1) * 8;
+  t.WX1 = min(t.WX0 + 7, W - 1);
+  t.WY1 = min(t.WY0 + 7, H - 1);
+  t.px = t.WX0 + (lane & 7);
+  t.py = t.WY0 + (lane >> 3);
+  t.inimg = t.px < W && t.py < H;
+  t.wave_live = t.WX0 < W && t.WY0 < H;
+  t.nbin = -1;
+  t.FX0 = t.X0;
+  t.FX1 = t.X1;
+  t.FY0 = t.Y0;
+  t.FY1 = t.Y1;
+  t.SX0 = t.WX0;
+  t.SX1 = t.WX1;
+  t.SY0 = t.WY0;
+  t.SY1 = t.WY1;
+  t.sub = s;
+  t.role = w / NS;
+  return t;
+}
+
+// (view, fine tile, part) of this workgroup of a (tiles * SPLIT, views) grid: dispatch slot d
+// is part d % SPLIT of tile slot d / SPLIT (heaviest-first order when the bins were built), after
+// the XCD-aware regrouping of tile_of_slot applied to the parts' slots (the parts of a tile and
+// their coarse-bin siblings share an XCD's L2).
+template <int SPLIT>
+__device__ __forceinline__ void tile_of_block_split(const BinBuffers &bb, int H, int W, int &b,
+                                                    int &tile, int &part, int &nbin,
+                                                    int dbg = 0) {
+  if (SPLIT == 1) {
+    part = 0;
+    tile_of_block(bb, H, W, b, tile, nbin, dbg);
+    return;
+  }
+  const int n = gridDim.x * gridDim.y;
+  int d = blockIdx.y * gridDim.x + blockIdx.x;
+  if ((d | 31) < n && !ablate(dbg, (1 << 17))) d = (d & ~31) | ((d & 7) << 2) | ((d >> 3) & 3);
+  part = d % SPLIT;
+  const int ts = d / SPLIT;
+  const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+  if (bb.order && bb.nchunk > 0) {
+    const int2 v = bb.order[ts];
+    b = v.x / ntiles;
+    tile = v.x - b * ntiles;
+    nbin = v.y;
+  } else {
+    b = ts / ntiles;
+    tile = ts - b * ntiles;
+    nbin = -1;
+  }
+}
 
 struct TileLists {
   int f[kCap];                   // local face index (ascending)

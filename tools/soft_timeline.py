@@ -1,6 +1,7 @@
 """Dispatch-slot timeline of the forward tile kernel (kd_dibr_fwd_tiles, or kd_soft_pairs with
 debug flag 1<<26; kd_debug_set flag 64): when do the heavy tiles start and end, and (fused) how
-long is each tile's raster phase?  python tools/soft_timeline.py [config] [extra debug flags]"""
+long is each tile's raster phase?
+python tools/soft_timeline.py [config] [extra debug flags] [tile split 1|2|4, default 1]"""
 import os
 os.environ.setdefault('KAOLIN_AMD_DIAG', '1')  # the diagnostic build (ablation flags)
 import sys
@@ -21,10 +22,12 @@ dev = torch.device('cuda')
 v = workloads.sphere_views(n_lon, n_lat, H, W, B, dev, elevation=elev)
 fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['normals_z']
 ntx, nty = (W + 15) // 16, (H + 15) // 16
-n = B * ntx * nty
+split = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+n = B * ntx * nty * split  # dispatch slots (parts of tiles)
 buf = torch.zeros(16 * n, dtype=torch.int64, device=dev)
 extra = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
 lib = _lib.load()
+_lib.set_tile_split(split)
 lib.kd_debug_buffer(buf.data_ptr())
 for _ in range(3):
     dibr_rasterization(H, W, fvz, fvi, feats, nz)
