@@ -150,6 +150,7 @@ class Workload:
         g_feat, g_soft = workloads.view_grads(first, n, H, W, self.D, dtype=dt)
         self.g_feat, self.g_soft = g_feat.to(dev), g_soft.to(dev)
         self.iou = args.iou
+        self.vertex_bwd = args.vertex_bwd
         self.gt = None
         if self.iou and not self.soup:  # a target silhouette: a disc in the middle of each view
             yy, xx = torch.meshgrid(torch.arange(H, dtype=dt), torch.arange(W, dtype=dt),
@@ -167,7 +168,8 @@ class Workload:
             return face_idx
         return distributed.dibr_forward_backward(
             self.vertices, self.faces, self.proj, self.cam, self.feats, self.H, self.W,
-            self.g_feat, self.g_soft, gt_mask=self.gt, iou=self.iou or 'fused', **self.kw)
+            self.g_feat, self.g_soft, gt_mask=self.gt, iou=self.iou or 'fused',
+            fused_vertices=self.vertex_bwd == 'fused', **self.kw)
 
     def clear(self):
         for p in self.params:
@@ -311,6 +313,9 @@ def main():
                          '(the training loop\'s), fused into the renderer or as the composition')
     ap.add_argument('--no-weak', action='store_true', help='skip the N > 1 weak-scaling phase')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--vertex-bwd', default='gather', choices=['gather', 'fused'],
+                    help='face -> vertex gradient: prepare_vertices\' gather kernel after the DIB-R '
+                         'backward, or fused into it (dibr_rasterization_from_vertices)')
     ap.add_argument('--tile-split', type=int, default=0, choices=[0, 1, 2, 4],
                     help='workgroups per tile of the fused forward (kd_set_tile_split; 0: auto)')
     ap.add_argument('--pmc', default=None,
@@ -480,6 +485,10 @@ def main():
                                   (' + RCCL vertex-grad all-reduce'
                                    if world > 1 and not soup else ''),
                    'launch': launch,
+                   'vertex_grad': ('fused into the DIB-R backward (dibr_rasterization_from_vertices)'
+                                   if args.vertex_bwd == 'fused' else
+                                   'prepare_vertices backward (gather kernel)'),
+                   'tile_split': args.tile_split or 'auto',
                    'close_lists': 'materialised' if args.lists else 'not materialised',
                    'soft_mask_grad': (f'mask_iou(soft, gt) ({args.iou})' if args.iou
                                       else 'fixed seeded grad_soft'),

@@ -219,12 +219,14 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   }
   // chunk-bit membership mask per coarse tile: bit t set <=> face (chunk * chunk size + t) touches
   // it; each thread holds faces tid (and tid + 256).
-  constexpr int kWords = PER * kBlock / 32, kPerT = PER;
-  extern __shared__ uint32_t s_mask[];  // [nct][kWords]
+  // (rows padded to an odd stride: lanes reading one word of different tiles' masks hit
+  // different banks)
+  constexpr int kWords = PER * kBlock / 32, kStride = kWords + 1, kPerT = PER;
+  extern __shared__ uint32_t s_mask[];  // [nct][kStride]
   __shared__ int s_bbase[kMaxCtiles], s_offs[kMaxCtiles], s_scan[kBlock / kWave];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
-  for (int k = tid; k < nct * kWords; k += kBlock) s_mask[k] = 0u;
+  for (int k = tid; k < nct * kStride; k += kBlock) s_mask[k] = 0u;
   {  // this chunk's exclusive offsets in every tile's bin (strided reads, once)
     const int *offs = bb.counts + (int64_t)b * nct * bb.nchunk + chunk;
     for (int c = tid; c < nct; c += kBlock) s_offs[c] = offs[(int64_t)c * bb.nchunk];
@@ -274,7 +276,7 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
     const int word = t >> 5;
     for (int cy = sp[u].y0 >> bb.g.sh; cy <= sp[u].y1 >> bb.g.sh; ++cy)
       for (int cx = sp[u].x0 >> bb.g.sh; cx <= sp[u].x1 >> bb.g.sh; ++cx)
-        atomicOr(&s_mask[(cy * bb.g.nctx + cx) * kWords + word], bit);
+        atomicOr(&s_mask[(cy * bb.g.nctx + cx) * kStride + word], bit);
   }
   __syncthreads();
   const int *offs = s_offs;  // (staged above: counts are tile-major)
@@ -292,7 +294,7 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
         const int c = cy * bb.g.nctx + cx;
         const int bc = bbase[c];
         if (bc < 0) continue;  // overflowed: its tiles walk all faces of the view
-        const uint32_t *m = s_mask + c * kWords;
+        const uint32_t *m = s_mask + c * kStride;
         int rank = __popc(m[word] & (bit - 1u));
         for (int k = 0; k < word; ++k) rank += __popc(m[k]);
         bins[bc + offs[c] + rank] = local;
@@ -434,7 +436,7 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
   {  // + one column of workgroups for the tile order (kd_bin_scatter, tile_order)
     // chunk-bit masks per coarse tile: up to 64 KB of dynamic LDS at 1024 coarse tiles (a
     // gfx950 workgroup may hold up to 160 KB; past 64 KB it has to be asked for)
-    const size_t dyn = sizeof(uint32_t) * (bb.chunk / 32) * (size_t)bb.g.nct();
+    const size_t dyn = sizeof(uint32_t) * (bb.chunk / 32 + 1) * (size_t)bb.g.nct();
     const void *fn = two ? (const void *)kd_bin_scatter<T, 2> : (const void *)kd_bin_scatter<T, 1>;
     if (dyn > 48 * 1024) {
       const hipError_t ea =

@@ -352,14 +352,26 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   int best = -1;
   T bw0 = (T)0, bw1 = (T)0, bw2 = (T)0;
   bool replay = (s_nan[kw] >> lane) & 1ull;
+  // the winner's features (D <= kFr) are loaded with its corners: one round trip, not two
+  constexpr int kFr = 4;
+  const bool fr_ok = a.D <= kFr;
+  T fr[3][kFr];
   if (!replay && s_key[kw][lane] != 0ull) {
     best = (int)(0xffffffffu - (uint32_t)(s_key[kw][lane] & 0xffffffffull));
     T v[6];
     load_corners(fs, lo + best, v);
     const T *zz = a.fvz + (lo + best) * a.fvz_fs;
+    const T za = zz[0], zb = zz[a.fvz_cs], zc = zz[2 * a.fvz_cs];
+    if (fr_ok) {
+      const T *r = a.feat + (lo + best) * 3 * a.D;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int d = 0; d < kFr; ++d) fr[i][d] = d < a.D ? r[i * a.D + d] : (T)0;
+    }
     T z0;
-    raster_face_test<T>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], zz[0], zz[a.fvz_cs],
-                        zz[2 * a.fvz_cs], a.eps, bw0, bw1, bw2, z0);
+    raster_face_test<T>(x0, y0, v[0], v[1], v[2], v[3], v[4], v[5], za, zb, zc, a.eps, bw0, bw1,
+                        bw2, z0);
     // fp64: the key's face is the winner only if its depth is the exact maximum
     if constexpr (kF64) replay = ordered_f64((double)z0) != S.zx[kw][lane];
   }
@@ -398,9 +410,15 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     wo[0] = bw0;
     wo[1] = bw1;
     wo[2] = bw2;
-    const T *r = a.feat + (lo + best) * 3 * a.D;
-    for (int d = 0; d < a.D; ++d)
-      io[d] = bw0 * r[d] + bw1 * r[a.D + d] + bw2 * r[2 * a.D + d];
+    if (fr_ok && !replay) {
+#pragma unroll
+      for (int d = 0; d < kFr; ++d)
+        if (d < a.D) io[d] = bw0 * fr[0][d] + bw1 * fr[1][d] + bw2 * fr[2][d];
+    } else {
+      const T *r = a.feat + (lo + best) * 3 * a.D;
+      for (int d = 0; d < a.D; ++d)
+        io[d] = bw0 * r[d] + bw1 * r[a.D + d] + bw2 * r[2 * a.D + d];
+    }
   } else {
     wo[0] = (T)0;
     wo[1] = (T)0;

@@ -187,6 +187,10 @@ struct SoftPairRec {
   uint8_t q;      // pixel of the tile (tile_geom thread index)
   uint8_t type;   // distance type 0..5 (set by the pair math, while the line is in L2)
 };
+// (soft_chunk_write stores a record as one 64-bit word: row | slot << 32 | q << 48 | type << 56)
+static_assert(sizeof(SoftPairRec) == 8 && offsetof(SoftPairRec, slot) == 4 &&
+                  offsetof(SoftPairRec, q) == 6 && offsetof(SoftPairRec, type) == 7,
+              "SoftPairRec layout");
 
 template <typename T>
 struct SoftCoef {
@@ -254,6 +258,8 @@ bool dibr_fwd_fusable(const RasterFwdArgs<double> &ra, const SoftArgs<double> &a
 int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a, SoftPairBuf<double> &pb,
                           hipStream_t stream);
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a);
+// workgroups per tile (1, 2, 4) the fused fp32 forward will use for B views
+int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B);
 int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
                           hipStream_t stream);
 // The soft-mask backward and the raster backward (kd_raster_bwd.hpp, D <= 3) in one launch.

@@ -233,7 +233,7 @@ __device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, i
 // record's q); ridx_q: its column of the (slot, pixel) record table.
 __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uint64_t sel, int c,
                                                  int64_t lo, int &my_kid, uint64_t *s_pm,
-                                                 unsigned short *s_off, int *s_nrec,
+                                                 int *s_off, int *s_row, int *s_nrec,
                                                  SoftPairRec *rec,
                                                  unsigned short (*s_ridx)[kBlock], int tile_q,
                                                  int ridx_q) {
@@ -246,14 +246,19 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
   if (tot == 0) return;
   int base = 0;
   if (lane == 0) base = atomicAdd(s_nrec, tot);
+  // the face lane's row (its entry of the chunk), staged with its mask and first record so that
+  // a pixel lane needs one LDS round trip per selected face
+  const int row = cnt ? (int)(lo + L.f[L.sub[ls][c * kWave + lane]]) : 0;
   base = __builtin_amdgcn_readfirstlane(base);
   s_pm[lane] = pm;
-  s_off[lane] = (unsigned short)(incl - cnt);
+  s_off[lane] = base + incl - cnt;
+  s_row[lane] = row;
   wave_lds_sync();
-  // pixel lanes: write own records, slots ascending with the face index; four selected faces
-  // per step, their LDS reads (entry -> face, the face's offset and pixel mask) issued together
-  // (one wave per SIMD at small batches: a dependent LDS chain per face is exposed latency)
+  // pixel lanes: write own records, slots ascending with the face index, four selected faces per
+  // step with every LDS read issued before the first store; a record is one 8-byte store
   const uint64_t below = (1ull << lane) - 1ull;
+  unsigned long long *rec8 = reinterpret_cast<unsigned long long *>(rec);
+  const unsigned long long qbits = (unsigned long long)(uint8_t)tile_q << 48;
   int slot = my_kid;
   for (uint64_t m = sel; m;) {
     constexpr int U = 4;
@@ -263,27 +268,26 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
       jj[u] = m ? (int)__builtin_ctzll(m) : -1;
       m &= m - 1ull;  // (0 stays 0)
     }
-    int kk[U], off[U];
+    int off[U], rw[U];
     uint64_t pmu[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = jj[u] < 0 ? 0 : jj[u];
-      kk[u] = L.sub[ls][c * kWave + j];
       off[u] = s_off[j];
+      rw[u] = s_row[j];
       pmu[u] = s_pm[j];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if (jj[u] < 0) break;
-      SoftPairRec r;
-      r.row = (int32_t)(lo + L.f[kk[u]]);
-      r.slot = (uint16_t)slot++;
-      r.q = (uint8_t)tile_q;
-      r.type = 0;
-      const int ri = base + off[u] + __popcll(pmu[u] & below);
-      rec[ri] = r;
-      if (s_ridx) s_ridx[r.slot][ridx_q] = (unsigned short)ri;  // (slot, pixel) -> record
+      if (jj[u] >= 0) {
+        const int ri = off[u] + __popcll(pmu[u] & below);
+        // SoftPairRec {row, slot, q, type = 0} as one little-endian 64-bit word
+        rec8[ri] = (unsigned long long)(uint32_t)rw[u] |
+                   ((unsigned long long)(uint16_t)(slot + u) << 32) | qbits;
+        if (s_ridx) s_ridx[slot + u][ridx_q] = (unsigned short)ri;  // (slot, pixel) -> record
+      }
     }
+    slot += (jj[0] >= 0) + (jj[1] >= 0) + (jj[2] >= 0) + (jj[3] >= 0);
   }
   my_kid = slot;
   wave_lds_sync();
@@ -291,14 +295,13 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
 
 __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
                                                    int K, const TileGeom &t, int64_t lo,
-                                                   int &my_kid, uint64_t *s_pm,
-                                                   unsigned short *s_off, int *s_nrec,
-                                                   SoftPairRec *rec,
+                                                   int &my_kid, uint64_t *s_pm, int *s_off,
+                                                   int *s_row, int *s_nrec, SoftPairRec *rec,
                                                    unsigned short (*s_ridx)[kBlock] = nullptr) {
   const int tile_q = threadIdx.x;
   const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
-  soft_chunk_write(L, threadIdx.x >> 6, sel, c, lo, my_kid, s_pm, s_off, s_nrec, rec, s_ridx,
-                   tile_q, tile_q);
+  soft_chunk_write(L, threadIdx.x >> 6, sel, c, lo, my_kid, s_pm, s_off, s_row, s_nrec, rec,
+                   s_ridx, tile_q, tile_q);
 }
 
 // The streaming form of one chunk (a tile without records): the pixel lane visits the same
@@ -431,7 +434,8 @@ struct SoftPairsLDS {
   unsigned short ridx[FUSED ? kFuseSlots : 1][kBlock];
   TileLists L;
   uint64_t pm[4][kWave];
-  unsigned short off[4][kWave];
+  int off[4][kWave];   // soft_chunk_write: a chunk face's first record
+  int row[4][kWave];   // ... and its face row
   int64_t base;
   int nrec, ibase, box[4];
   double iou[8];  // iou_tile_terms
@@ -475,10 +479,14 @@ __device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const Soft
 // every role knows the hits of the roles before it, so a pixel's slots stay in face order (its
 // first K).  Role 0 forms the product and writes the pixel outputs.  uncm (nullptr: read
 // face_idx): per sub-tile, the mask of uncovered in-image pixels (the fused raster phase's).
-template <typename T, bool FUSED, int SPLIT = 1>
+// CLK (diagnostics, kd_dibr_fwd_tiles<true>): wave 0's pass-A cycle counts into clk[(i) * slots
+// + slot]: [0] round (hits, selection, record writes) [1] record writes [2] done() [3] batches
+// [4] chunks [5] faces through the filter [6] records of the workgroup [7] pass A
+template <typename T, bool FUSED, int SPLIT = 1, bool CLK = false>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                 int b, int tl, int nbin, SoftPairsLDS<FUSED> &S,
-                                                int part = 0, const uint64_t *uncm = nullptr) {
+                                                int part = 0, const uint64_t *uncm = nullptr,
+                                                long long *clk = nullptr) {
   static_assert(SPLIT == 1 || FUSED, "split tiles: the fused soft mask only");
   TileLists &L = S.L;
   const FaceSet<T> &fs = a.fs;
@@ -555,13 +563,35 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     t.FY0 = s_box[2];
     t.FY1 = s_box[3];
     auto stage = [&](int, int64_t) {};  // pass A needs the spans only
-    auto round = [&](int nsub, int) {
+    long long cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto now_clk = [&]() -> long long {
+      return CLK ? (long long)__builtin_readcyclecounter() : 0ll;
+    };
+    const long long pa0 = now_clk();
+    auto round = [&](int nsub, int ncnt) {
+      const long long r0 = now_clk();
+      if (CLK) {
+        cyc[3] += 1;
+        cyc[5] += ncnt;
+      }
       if constexpr (SPLIT == 1) {
         if (wave_unc && !ablate(fs.dbg, 1024)) {
-          for (int c = 0; c * kWave < nsub; ++c)
-            soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], &S.nrec,
-                               pb.rec + S.base, FUSED ? S.ridx : nullptr);
+          for (int c = 0; c * kWave < nsub; ++c) {
+            if constexpr (CLK) {
+              cyc[4] += 1;
+              const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
+              const long long w0 = now_clk();
+              soft_chunk_write(L, w, sel, c, lo, my_kid, S.pm[w], S.off[w], S.row[w], &S.nrec,
+                               pb.rec + S.base, FUSED ? S.ridx : nullptr, tid, tid);
+              cyc[1] += now_clk() - w0;
+            } else {
+              soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], S.row[w],
+                                 &S.nrec,
+                                 pb.rec + S.base, FUSED ? S.ridx : nullptr);
+            }
+          }
         }
+        if (CLK) cyc[0] += now_clk() - r0;
       } else {
         // groups of SPLIT chunks (a workgroup-uniform count: every wave meets the barriers)
         const int nmax = max(max(L.nsub[0], L.nsub[1]), max(L.nsub[2], L.nsub[3]));
@@ -584,11 +614,17 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
           int slot = my_kid + before;
           const int take = min(cnt, max(K - slot, 0));
           const uint64_t sel = take < cnt ? lowest_bits(hits, take) : hits;
+          const long long w0 = now_clk();
           if (mine)
-            soft_chunk_write(L, w, sel, c, lo, slot, S.pm[w], S.off[w], &S.nrec, pb.rec + S.base,
-                             S.ridx, tile_q, tile_q);
+            soft_chunk_write(L, w, sel, c, lo, slot, S.pm[w], S.off[w], S.row[w], &S.nrec,
+                             pb.rec + S.base, S.ridx, tile_q, tile_q);
+          if (CLK) {
+            cyc[1] += now_clk() - w0;
+            cyc[4] += mine ? 1 : 0;
+          }
           my_kid = min(K, my_kid + all);
         }
+        if (CLK) cyc[0] += now_clk() - r0;
       }
     };
     // once every uncovered pixel holds K close faces, later faces cannot enter; a tile without
@@ -597,6 +633,14 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     // enlarged span reaches none of them cannot enter any list, so the next batches' tile list
     // and sub-lists hold only faces that can (exact, like the first filter)
     auto done = [&]() {
+      const long long d0 = now_clk();
+      struct Acc {
+        long long &c, t0;
+        bool on;
+        __device__ ~Acc() {
+          if (on) c += (long long)__builtin_readcyclecounter() - t0;
+        }
+      } acc{cyc[2], d0, CLK};
       const bool open = unc && my_kid < K;
       const uint64_t om = __ballot(open);
       int bx0 = 1 << 30, bx1 = -1, by0 = 1 << 30, by1 = -1;
@@ -644,6 +688,14 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     tile_rounds(L, a.bb, nview, b, lo, t, stage, round_checked, fs.dbg, done);
     __syncthreads();
     ovf = S.base == -2;
+    if (CLK && KD_DIAG && clk && tid == 0) {
+      const int64_t nb = (int64_t)gridDim.x * gridDim.y,
+                    slot = (int64_t)blockIdx.y * gridDim.x + blockIdx.x;
+      cyc[6] = S.nrec;
+      cyc[7] = now_clk() - pa0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) clk[i * nb + slot] = cyc[i];
+    }
     if (KD_DIAG && fs.tbuf && tid == 0 && FUSED)  // diagnostics: end of pass A
       fs.tbuf[5ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
           wall_clock64();
@@ -772,7 +824,9 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
-  soft_pairs_tile<float, true, SPLIT>(a, pb, b, tl, -1, U.s, part, uncm);
+  soft_pairs_tile<float, true, SPLIT, DIAG>(
+      a, pb, b, tl, -1, U.s, part, uncm,
+      DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr);
 }
 
 // The fp64 DIB-R forward in one launch: the pair raster (fp64 test, fp64-culled candidates, the
@@ -1364,7 +1418,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
 // Workgroups per tile of the fused fp32 forward (kd_dibr_fwd_tiles SPLIT): the tile split hook
 // (kd_set_tile_split) when set, else by the batch's tile count against the chip's workgroup
 // slots.  Split tiles need the fixed record pool (every part owns its pixels' K records).
-static int fwd_tile_split(int64_t tiles, bool fixed_pool) {
+int fwd_tile_split(int64_t tiles, bool fixed_pool) {
   if (!fixed_pool) return 1;
   const int forced = tile_split();
   if (forced > 0) return forced;
@@ -1383,6 +1437,10 @@ static int fwd_tile_split(int64_t tiles, bool fixed_pool) {
   return tiles <= slots ? 2 : 1;
 }
 
+int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B) {
+  return fwd_tile_split((int64_t)B * pb.ntiles, pb.fixed && !pool_may_overflow(K));
+}
+
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) {
   return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
          !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT));
@@ -1395,7 +1453,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
-    const int split = fwd_tile_split((int64_t)ra.fs.B * pb.ntiles, pb.fixed && !pool_may_overflow(a.K));
+    const int split = dibr_fwd_split(pb, a.K, ra.fs.B);
     const dim3 grid((unsigned)pb.ntiles * split, ra.fs.B);
     const bool diag = KD_DIAG && a.fs.tbuf;
 #define KD_FWD_TILES(S)                                                                         \

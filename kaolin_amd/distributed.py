@@ -195,7 +195,8 @@ class GradBucket:
 
 def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_features, height,
                           width, grad_interp, grad_soft, sigmainv=7000., boxlen=0.02, knum=30,
-                          prepare=None, render=None, gt_mask=None, iou='fused'):
+                          prepare=None, render=None, gt_mask=None, iou='fused',
+                          fused_vertices=False):
     """The GPU part of one DIB-R training step on this rank's views: project the
     shared mesh to the rank's cameras (``prepare_vertices``, utils.py:128-175), render
     (``dibr_rasterization``, dibr.py:119-209, valid faces = normals z >= 0) and back-propagate
@@ -210,8 +211,19 @@ def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_f
     mask_iou(soft_mask, gt_mask) (metrics/render.py:18-40, ian_dibr.py:264-265) instead of
     grad_soft: fused into the renderer (iou='fused', dibr_rasterization_with_mask_iou) or as the
     composition dibr_rasterization + mask_iou (iou='compose').
+    fused_vertices: ``dibr_rasterization_from_vertices`` (the face -> vertex step inside the DIB-R
+    backward kernel) instead of prepare_vertices + dibr_rasterization (HIP kernels, no gt_mask).
     Returns face_idx (B_rank, H, W)."""
     B = camera_transform.shape[0]
+    if fused_vertices and gt_mask is None and prepare is None and render is None:
+        from .render.mesh import dibr_rasterization_from_vertices
+        feats = face_features if face_features.shape[0] == B else \
+            face_features.expand(B, *face_features.shape[1:])
+        interp, soft, face_idx = dibr_rasterization_from_vertices(
+            height, width, vertices.unsqueeze(0), faces, camera_proj, camera_transform, feats,
+            sigmainv, boxlen, knum)
+        torch.autograd.backward([interp, soft], [grad_interp, grad_soft])
+        return face_idx
     if prepare is None or render is None:
         from .render.mesh import dibr_rasterization, prepare_vertices
         prepare = prepare or prepare_vertices

@@ -188,11 +188,14 @@ class DibrRenderHip(Function):
     SURVEY.md §8 f1): the corner gradients of the raster and the soft mask go straight to the
     vertex gradient, with no (B, F, 3, 2) gradient and no separate scatter kernel.
 
-    Measured at C3 (same box): the fused backward takes 144-150 us against 69 + 19 us for the
-    DIB-R backward plus kd_prepare_bwd -- the vertex atomics (3 per corner, every vertex shared
-    by ~6 faces and every view) serialise where the per-face grad_fvi atomics did not.  The
-    training step (kaolin_amd.distributed) therefore keeps the two-kernel path; this node stays
-    as the f1 entry point, parity-tested (tests/test_gpu_vertices.py)."""
+    Measured at C3 (same box, bench.py --vertex-bwd fused, profiles/r04/ab_vtx*.txt): the fused
+    backward takes 156 us against 68.6 + 18.5 us for the DIB-R backward plus kd_prepare_bwd at 8
+    views (step 0.369 vs 0.302 ms), and 31 against 18.7 + 10.7 us at 1 view -- the vertex
+    atomics (3 per corner, every vertex shared by ~6 faces and every view) serialise where the
+    per-face grad_fvi atomics did not; per-(tile, vertex) LDS sums before the projection (round
+    4) did not change that.  The training step (kaolin_amd.distributed) therefore keeps the
+    two-kernel path; this node stays as the f1 entry point, parity-tested
+    (tests/test_gpu_vertices.py)."""
 
     @staticmethod
     def forward(ctx, vertices, faces, camera_proj, camera_transform, face_features, height,

@@ -1,7 +1,7 @@
 """Same-box A/B of whole trees: python tools/ab_dirs.py DIR_A DIR_B [reps] [bench args...]
 
 Runs DIR/bench.py (--no-cpu-baseline) alternately from each tree `reps` times and prints the best
-ms/step and per-kernel averages of each (box-to-box spread is a few %, so compare on one box)."""
+median step time (ms_per_step_median) and per-kernel averages of each (box-to-box spread is a few %, so compare on one box)."""
 import json
 import os
 import subprocess
@@ -21,10 +21,10 @@ for r in range(reps):
             print(f'{d}: rc={p.returncode}\n{p.stderr[-2000:]}')
             sys.exit(1)
         out = json.loads(lines[-1])
-        res[d].append(out['ms_per_step'])
+        res[d].append(out.get('ms_per_step_median') or out['ms_per_step'])
         for k, v in out['kernels'].items():
             kern[d].setdefault(k, []).append(v['avg_us'])
-        print(f'rep {r} {os.path.basename(d)}: {out["ms_per_step"]:.4f} ms', flush=True)
+        print(f'rep {r} {os.path.basename(d)}: {res[d][-1]:.4f} ms (median step)', flush=True)
 for d in dirs:
     print(f'{os.path.basename(d)}: ms/step {sorted(res[d])}  best {min(res[d]):.4f}')
 names = list(kern[dirs[0]]) + [k for k in kern[dirs[1]] if k not in kern[dirs[0]]]

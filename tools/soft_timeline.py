@@ -24,7 +24,7 @@ fvz, fvi, feats, nz = v['fvz'], v['fvi'].requires_grad_(True), v['feats'], v['no
 ntx, nty = (W + 15) // 16, (H + 15) // 16
 split = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 n = B * ntx * nty * split  # dispatch slots (parts of tiles)
-buf = torch.zeros(16 * n, dtype=torch.int64, device=dev)
+buf = torch.zeros(24 * n, dtype=torch.int64, device=dev)
 extra = int(sys.argv[2], 0) if len(sys.argv) > 2 else 0
 lib = _lib.load()
 _lib.set_tile_split(split)
@@ -37,7 +37,7 @@ dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
 lib.kd_debug_set(0)
 lib.kd_debug_buffer(None)
-t = buf.view(16, n).cpu().numpy()
+t = buf.view(24, n).cpu().numpy()
 dur = t[1] / 100.0          # us (100 MHz wall clock)
 start = (t[2] - t[2].min()) / 100.0
 end = start + dur
@@ -97,6 +97,12 @@ if t[5].any():  # soft phase split: pass A (walk + records), pair math, product 
         c = t[8:16, i]
         print(f'  slot {i:5d} raster {rdur[i]:5.1f} us: {c[0] / 1e3:7.1f} {c[1] / 1e3:7.1f} '
               f'{c[2] / 1e3:7.1f} {c[3] / 1e3:7.1f} | {c[4]:4d} {c[5]:6d} {c[6]:4d} {c[7]:3d}')
+    # soft pass A of wave 0 (core clock cycles; diag CLK counters)
+    print('soft pass A wave 0 (kcycles): passA round write done | batches chunks faces records')
+    for i in np.argsort(pa)[::-1][:10]:
+        c = t[16:24, i]
+        print(f'  slot {i:5d} passA {pa[i]:5.1f} us: {c[7] / 1e3:7.1f} {c[0] / 1e3:7.1f} '
+              f'{c[1] / 1e3:7.1f} {c[2] / 1e3:7.1f} | {c[3]:3d} {c[4]:4d} {c[5]:5d} {c[6]:5d}')
 late = np.argsort(end)[::-1][:10]
 print('latest ending (slot, start, dur):', [(int(i), round(float(start[i]), 1),
                                             round(float(dur[i]), 1)) for i in late])
