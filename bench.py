@@ -316,6 +316,8 @@ def main():
     ap.add_argument('--vertex-bwd', default='gather', choices=['gather', 'fused'],
                     help='face -> vertex gradient: prepare_vertices\' gather kernel after the DIB-R '
                          'backward, or fused into it (dibr_rasterization_from_vertices)')
+    ap.add_argument('--coarse-tile', type=int, default=0, choices=[0, 16, 32],
+                    help='coarse bin edge of the DIB-R binning (kd_set_coarse_tile; 0: auto)')
     ap.add_argument('--tile-split', type=int, default=0, choices=[0, 1, 2, 4],
                     help='workgroups per tile of the fused forward (kd_set_tile_split; 0: auto)')
     ap.add_argument('--pmc', default=None,
@@ -332,6 +334,7 @@ def main():
     torch.cuda.set_device(dev)
     _lib.load()
     _lib.set_tile_split(args.tile_split)
+    _lib.set_coarse_tile(args.coarse_tile)
     soup = args.config in SOUP_CONFIGS
     B_global = SOUP_CONFIGS[args.config][3] if soup else CONFIGS[args.config][4]
     weak_main = args.views_per_gpu is not None
@@ -489,6 +492,7 @@ def main():
                                    if args.vertex_bwd == 'fused' else
                                    'prepare_vertices backward (gather kernel)'),
                    'tile_split': args.tile_split or 'auto',
+                   'coarse_tile': args.coarse_tile or 'auto',
                    'close_lists': 'materialised' if args.lists else 'not materialised',
                    'soft_mask_grad': (f'mask_iou(soft, gt) ({args.iou})' if args.iou
                                       else 'fixed seeded grad_soft'),

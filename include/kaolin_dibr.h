@@ -81,6 +81,12 @@ int kd_set_test_forms(int forms);
  * Used only when the soft mask's record pool is the fixed one (knum <= 32, no pool limit). */
 int kd_set_tile_split(int split);
 
+/* Coarse bin edge of dibr_rasterization in pixels (a test and tuning hook; 0 by default = 32;
+ * larger images grow it to at most 32 bins per side).  Results never depend on it.  It fixes the workspace layout of a call:
+ * hold it constant between a forward and its backward (kd_dibr_workspace_size covers every
+ * choice). */
+int kd_set_coarse_tile(int px);
+
 /* Pool limits (a test and tuning hook; both 1 by default).  The workspaces hold two bounded
  * pools whose layout depends only on the call's sizes: the coarse bins (16 entries per face row)
  * and the soft mask's (pixel, close face) records (min(knum, 12) per pixel plus block slack).

@@ -131,6 +131,8 @@ def load():
             lib.kd_set_test_forms.restype = c_int
             lib.kd_set_tile_split.argtypes = [c_int]
             lib.kd_set_tile_split.restype = c_int
+            lib.kd_set_coarse_tile.argtypes = [c_int]
+            lib.kd_set_coarse_tile.restype = c_int
             lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
             lib.kd_prepare_vertices_ranges.restype = c_i64
             # diagnostic build only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
@@ -192,6 +194,13 @@ def set_tile_split(split=0):
     """Workgroups per tile of the fused fp32 forward (kd_set_tile_split, a test and tuning hook):
     1, 2 or 4; 0 restores the automatic choice."""
     if load().kd_set_tile_split(int(split)) != KD_OK:
+        raise RuntimeError(load().kd_last_error().decode(errors='replace'))
+
+
+def set_coarse_tile(px=0):
+    """dibr_rasterization's coarse bin edge (kd_set_coarse_tile, a test and tuning hook): 16 or
+    32 pixels; 0 restores the default (32).  Hold it between a forward and its backward."""
+    if load().kd_set_coarse_tile(int(px)) != KD_OK:
         raise RuntimeError(load().kd_last_error().decode(errors='replace'))
 
 

@@ -21,6 +21,18 @@ std::atomic<int> g_forms{0};
 int test_forms() { return g_forms.load(); }
 std::atomic<int> g_split{0};
 int tile_split() { return g_split.load(); }
+std::atomic<int> g_ct{0};
+int coarse_tile_hook() { return g_ct.load(); }
+int device_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
 std::atomic<long long *> g_tbuf{nullptr};
 std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
 float pool_limit_bins() { return g_lim_bins.load(); }
@@ -101,6 +113,13 @@ int kd_set_tile_split(int split) {
   if (split != 0 && split != 1 && split != 2 && split != 4)
     return kd::set_error(KD_ERR_INVALID_ARGUMENT, "tile split must be 0, 1, 2 or 4 (got %d)", split);
   kd::g_split.store(split);
+  return KD_OK;
+}
+
+int kd_set_coarse_tile(int px) {
+  if (px != 0 && px != 16 && px != 32)
+    return kd::set_error(KD_ERR_INVALID_ARGUMENT, "coarse tile must be 0, 16 or 32 (got %d)", px);
+  kd::g_ct.store(px);
   return KD_OK;
 }
 

@@ -48,6 +48,10 @@ constexpr int debug_flags() { return 0; }
 int test_forms();
 // kd_set_tile_split: workgroups per tile of the fused fp32 forward (0: chosen by the batch size)
 int tile_split();
+// kd_set_coarse_tile: dibr_rasterization's coarse bin edge (0: chosen by the batch size)
+int coarse_tile_hook();
+// compute units of the current device (cached on first use; 256 when unknown)
+int device_cus();
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
 
 // Per-workgroup duration (wall clock, 100 MHz ticks) for diagnostics: written by thread 0 when

@@ -21,9 +21,23 @@
 
 namespace kd {
 
+// Coarse bin edge (kd_binning bin_geom ct0) of a call: the test / tuning hook's, else 32 px.
+// Measured at C3 (bench.py --coarse-tile, same box; profiles/r04/ab_ct*.txt): with 16-px bins
+// (each fine tile walks only its own faces) the fused forward at 1 view drops from 55.1 to
+// 48.9 us, but the scatter's per-chunk membership masks grow with the bin count (10.3 -> 18.4
+// us; 21.6 -> 60.5 us at 8 views) and the count's LDS atomics with the bins a face touches:
+// 1 view 0.1098 -> 0.1161 ms, 2 views 0.1382 -> 0.1553, 8 views 0.3017 -> 0.3590.  A function
+// of the hook only, so forward and backward agree (the pair buffers lead the workspace anyway).
+static int dibr_ct0(int, int, int) {
+  const int hook = coarse_tile_hook();
+  return hook > 0 ? hook : kCoarseTile0;
+}
+
 size_t dibr_workspace_bytes(int B, int H, int W, int64_t F, int K, int esize) {
+  // sized for the smallest coarse tile (the most bins): covers every dibr_ct0 choice
   const int64_t N = (int64_t)B * F;
-  return bin_workspace_bytes(B, H, W, N, F) + soft_pair_workspace_bytes(B, H, W, N, F, K, esize);
+  return bin_workspace_bytes(B, H, W, N, F, kTile) +
+         soft_pair_workspace_bytes(B, H, W, N, F, K, esize, kTile);
 }
 
 template <typename T>
@@ -33,14 +47,17 @@ struct DibrBuffers {
   SoftPairBuf<T> pb;   // soft-mask records
 };
 
+// The pair buffers first: their place does not depend on the coarse tile (dibr_ct0), so a
+// backward finds its forward's records whatever it would choose.
 template <typename T>
 static DibrBuffers<T> dibr_carve(void *ws, int B, int H, int W, int64_t F, int K) {
   const int64_t N = (int64_t)B * F;
+  const int ct0 = dibr_ct0(B, H, W);
   DibrBuffers<T> d;
   size_t off = 0;
-  d.rbb = bin_carve(ws, off, B, H, W, N, F);
-  d.sbb = bin_carve(ws, off, B, H, W, N, F);  // soft_pair_workspace_bytes starts with these
   d.pb = soft_pair_carve<T>(ws, off, B, H, W, K);
+  d.rbb = bin_carve(ws, off, B, H, W, N, F, ct0);
+  d.sbb = bin_carve(ws, off, B, H, W, N, F, ct0);
   return d;
 }
 

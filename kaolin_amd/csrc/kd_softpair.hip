@@ -1422,13 +1422,7 @@ int fwd_tile_split(int64_t tiles, bool fixed_pool) {
   if (!fixed_pool) return 1;
   const int forced = tile_split();
   if (forced > 0) return forced;
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 256;
-    return n > 0 ? n : 256;
-  }();
+  const int cus = device_cus();
   // measured at C3 (bench.py --tile-split, same box): 1 view (1024 tiles) 0.1177 / 0.1076 /
   // 0.1170 ms per step at 1 / 2 / 4 workgroups per tile; 2 views (2048) 0.1388 / 0.1463 / 0.1624;
   // 8 views 0.310 / 0.352.  A part repeats the tile's raster walk (~10 us of dependent loads at

@@ -1,4 +1,5 @@
-"""GPU: split tiles of the fused fp32 DIB-R forward (kd_dibr_fwd_tiles SPLIT, kd_set_tile_split).
+"""GPU: split tiles of the fused fp32 DIB-R forward (kd_dibr_fwd_tiles SPLIT, kd_set_tile_split)
+and the 16-px coarse bins of small batches (kd_set_coarse_tile).
 
 With 2 or 4 workgroups per 16x16 tile (half / quarter tiles, several waves per 8x8 sub-tile
 sharing its face chunks), the forward must produce exactly what the one-workgroup tile produces:
@@ -30,6 +31,7 @@ def _restore_split():
     yield
     from kaolin_amd import _lib
     _lib.set_tile_split(0)
+    _lib.set_coarse_tile(0)
 
 
 def _with_split(split, fn):
@@ -143,3 +145,65 @@ def test_split_hook_rejects_bad_values():
     from kaolin_amd import _lib
     with pytest.raises(RuntimeError):
         _lib.set_tile_split(3)
+
+
+def _with_ct(px, fn):
+    from kaolin_amd import _lib
+    _lib.set_coarse_tile(px)
+    try:
+        return fn()
+    finally:
+        _lib.set_coarse_tile(0)
+
+
+@pytest.mark.parametrize('views', [1, 8])
+def test_coarse_tile_16_matches_32_c3(views):
+    """16-px coarse bins (each fine tile's own bin) against the 32-px bins: the walks keep the
+    same faces in the same order, so every output is bit-identical"""
+    from kaolin_amd import workloads
+    h = w = 512
+    v = workloads.sphere_views(250, 101, h, w, views, DEV)
+    a = _with_ct(32, lambda: _fwd_bwd(h, w, v))
+    b = _with_ct(16, lambda: _fwd_bwd(h, w, v))
+    _same(b, a)
+
+
+@pytest.mark.parametrize('hw', [(136, 200), (520, 72)])
+def test_coarse_tile_16_ragged_vs_oracle(hw):
+    """16-px bins on sides that are not multiples of 16 (and one side past 32 bins: 32-px bins)"""
+    from kaolin_amd import workloads
+    h, w = hw
+    v = workloads.sphere_views(60, 31, h, w, 2, DEV)
+    out = _with_ct(16, lambda: _fwd_bwd(h, w, v))
+    for b in range(2):
+        _check_view(h, w, b, out)
+
+
+def test_coarse_tile_changed_between_forward_and_backward():
+    """the backward finds its forward's records whatever coarse tile it would choose (the pair
+    buffers lead the workspace)"""
+    from kaolin_amd import _lib, workloads
+    from kaolin_amd.render.mesh import dibr_rasterization
+    h = w = 256
+    v = workloads.sphere_views(100, 51, h, w, 2, DEV)
+    ref = _with_ct(16, lambda: _fwd_bwd(h, w, v))
+    fvi = v['fvi'].detach().clone().requires_grad_(True)
+    feats = v['feats'].contiguous().clone().requires_grad_(True)
+    _lib.set_coarse_tile(16)
+    try:
+        interp, soft, face_idx = dibr_rasterization(h, w, v['fvz'], fvi, feats, v['normals_z'])
+        _lib.set_coarse_tile(32)
+        torch.autograd.backward([interp, soft], [ref[7], ref[8]])
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_coarse_tile(0)
+    assert torch.equal(face_idx, ref[6]) and torch.equal(soft, ref[5])
+    for x, y in ((fvi.grad, ref[1].grad), (feats.grad, ref[2].grad)):
+        r = N(y)
+        np.testing.assert_allclose(N(x), r, rtol=1e-4, atol=1e-5 * np.abs(r).max())
+
+
+def test_coarse_tile_hook_rejects_bad_values():
+    from kaolin_amd import _lib
+    with pytest.raises(RuntimeError):
+        _lib.set_coarse_tile(8)
