@@ -321,7 +321,7 @@ def main():
     ap.add_argument('--tile-split', type=int, default=0, choices=[0, 1, 2, 4],
                     help='workgroups per tile of the fused forward (kd_set_tile_split; 0: auto)')
     ap.add_argument('--pmc', default=None,
-                    help='PMC traffic summary (default profiles/r03 or r02/pmc_traffic_<config>.json)')
+                    help='PMC traffic summary (default profiles/r04, r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
 
     # KD_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (ranks share cuda:0;
@@ -390,7 +390,7 @@ def main():
             del ws
     fused = 'kd_soft_pair_math' not in prof  # the one-launch soft mask (kd_softpair.hip)
     pmc, pmc_src = {}, None
-    for rnd in ([args.pmc] if args.pmc else ['r03', 'r02']):  # the newest committed summary
+    for rnd in ([args.pmc] if args.pmc else ['r04', 'r03', 'r02']):  # the newest committed summary
         pmc_path = rnd if args.pmc else os.path.join(ROOT, 'profiles', rnd,
                                                        f'pmc_traffic_{args.config}.json')
         pmc, pmc_src = load_pmc(pmc_path, args.config, args.dtype, args.lists, n)
