@@ -209,19 +209,26 @@ def make_step(wl, use_graph):
 
 def timed(step, steps, warmup, dev, world):
     """W untimed steps, then exactly K steps between barrier + synchronize on both sides; the
-    wall time is the max over ranks.  Each timed step is also bracketed by HIP events on the
-    current stream (the replay, and for a GraphedStep at N > 1 the all-reduce after it), so the
-    line carries the median step and the all-reduce's own time.  Returns (elapsed s, {'step_ms':
-    [...], 'allreduce_ms': [...] or None})."""
+    wall time is the max over ranks (nothing else is enqueued in that region).  Then K more steps,
+    each bracketed by HIP events on the current stream (the replay, and for a GraphedStep at N > 1
+    the all-reduce after it), for the median step and the all-reduce's own time.  Returns
+    (elapsed s, {'step_ms': [...], 'allreduce_ms': [...] or None})."""
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # the per-step event pass (not part of the timed region)
     split = isinstance(step, distributed.GraphedStep) and world > 1
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-    t0 = time.perf_counter()
     for e in ev:
         e[0].record()
         if split:
@@ -232,9 +239,6 @@ def timed(step, steps, warmup, dev, world):
             step()
         e[2].record()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
     step_ms = [e[0].elapsed_time(e[2]) for e in ev]
     ar_ms = [e[1].elapsed_time(e[2]) for e in ev] if split else None
     if world > 1:
@@ -472,9 +476,9 @@ def main():
         'ms_per_step_median': None if step_median is None else round(step_median, 4),
         'allreduce_us': None if ar_median is None else round(ar_median * 1e3, 2),
         'timing': 'value and ms_per_step: K steps between barrier + synchronize, wall clock, max '
-                  'over ranks; ms_per_step_median: median of the per-step HIP event times (max '
-                  'over ranks); allreduce_us: median per-step time of the RCCL all-reduce after '
-                  'the graph replay (N > 1)',
+                  'over ranks, nothing else enqueued; ms_per_step_median: median of the per-step '
+                  'HIP event times of K further steps (max over ranks); allreduce_us: median '
+                  'per-step time of the RCCL all-reduce after the graph replay (N > 1)',
         'higher_is_better': True, 'scaling': 'weak' if weak_main else 'strong',
         'vs_baseline': None, 'dtype': args.dtype,
         'data': 'synthetic (seeded ' + ('triangle soup' if soup else 'uv-sphere, orbit cameras')
