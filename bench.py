@@ -150,7 +150,9 @@ class Workload:
         g_feat, g_soft = workloads.view_grads(first, n, H, W, self.D, dtype=dt)
         self.g_feat, self.g_soft = g_feat.to(dev), g_soft.to(dev)
         self.iou = args.iou
-        self.vertex_bwd = args.vertex_bwd
+        self.vertex_path = args.vertex_path
+        if args.vertex_path != 'compose':
+            dibr.FUSED_VERTEX_BACKWARD = args.vertex_path == 'node-vtx'
         self.gt = None
         if self.iou and not self.soup:  # a target silhouette: a disc in the middle of each view
             yy, xx = torch.meshgrid(torch.arange(H, dtype=dt), torch.arange(W, dtype=dt),
@@ -169,7 +171,7 @@ class Workload:
         return distributed.dibr_forward_backward(
             self.vertices, self.faces, self.proj, self.cam, self.feats, self.H, self.W,
             self.g_feat, self.g_soft, gt_mask=self.gt, iou=self.iou or 'fused',
-            fused_vertices=self.vertex_bwd == 'fused', **self.kw)
+            fused_vertices=self.vertex_path != 'compose', **self.kw)
 
     def clear(self):
         for p in self.params:
@@ -317,9 +319,11 @@ def main():
                          '(the training loop\'s), fused into the renderer or as the composition')
     ap.add_argument('--no-weak', action='store_true', help='skip the N > 1 weak-scaling phase')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--vertex-bwd', default='gather', choices=['gather', 'fused'],
-                    help='face -> vertex gradient: prepare_vertices\' gather kernel after the DIB-R '
-                         'backward, or fused into it (dibr_rasterization_from_vertices)')
+    ap.add_argument('--vertex-path', default='node', choices=['compose', 'node', 'node-vtx'],
+                    help='prepare_vertices + dibr_rasterization as two nodes (compose), or as '
+                         'dibr_rasterization_from_vertices (node: the projection inside the '
+                         'binning launch, gather backward; node-vtx: its face -> vertex step '
+                         'inside the DIB-R backward kernel)')
     ap.add_argument('--coarse-tile', type=int, default=0, choices=[0, 16, 32],
                     help='coarse bin edge of the DIB-R binning (kd_set_coarse_tile; 0: auto)')
     ap.add_argument('--tile-split', type=int, default=0, choices=[0, 1, 2, 4],
@@ -492,9 +496,12 @@ def main():
                                   (' + RCCL vertex-grad all-reduce'
                                    if world > 1 and not soup else ''),
                    'launch': launch,
-                   'vertex_grad': ('fused into the DIB-R backward (dibr_rasterization_from_vertices)'
-                                   if args.vertex_bwd == 'fused' else
-                                   'prepare_vertices backward (gather kernel)'),
+                   'vertex_path': {'compose': 'prepare_vertices + dibr_rasterization',
+                                   'node': 'dibr_rasterization_from_vertices (projection in the '
+                                           'binning launch; gather backward)',
+                                   'node-vtx': 'dibr_rasterization_from_vertices (face -> vertex '
+                                               'step in the DIB-R backward kernel)'}[
+                                       args.vertex_path],
                    'tile_split': args.tile_split or 'auto',
                    'coarse_tile': args.coarse_tile or 'auto',
                    'close_lists': 'materialised' if args.lists else 'not materialised',

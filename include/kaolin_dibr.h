@@ -276,6 +276,32 @@ int kd_dibr_rasterization_forward_f64(int batch, int height, int width, int64_t 
                                       int64_t *face_idx, double *weights, double *soft,
                                       int want_grad, double *grad_fvi_zero, double *grad_feat_zero,
                                       void *workspace, size_t workspace_bytes, void *stream);
+/* The same forward from the vertices (prepare_vertices, camera transform form,
+ * kaolin/render/mesh/utils.py:128-175, followed by dibr_rasterization of its outputs, the DIB-R
+ * training step of examples/tutorial/ian_dibr.py): vertices (vertex_batch, V, 3) with
+ * vertex_batch 1 or batch, faces (F, 3) int64, camera_proj (3), camera_transform (batch, 4, 3).
+ * Writes prepare_vertices' outputs fvc (batch, F, 3, 3), fvi (batch, F, 3, 2) and normals
+ * (batch, F, 3) -- the projection runs inside the binning launch, which writes them -- and
+ * renders with face_vertices_z = fvc[..., 2], face_vertices_image = fvi, face_normals_z =
+ * normals[..., 2]; every output equals kd_prepare_vertices_forward followed by
+ * kd_dibr_rasterization_forward.  Its backward: kd_dibr_rasterization_backward_* for grad_fvi,
+ * then kd_prepare_vertices_backward_*; or kd_dibr_rasterization_backward_vertices_*. */
+int kd_dibr_rasterization_forward_vertices_f32(
+    int batch, int height, int width, int vertex_batch, int64_t num_vertices, int64_t num_faces,
+    int feat_dim, const float *vertices, const int64_t *faces, const float *camera_proj,
+    const float *camera_transform, const float *feat, double multiplier, float eps,
+    float sigmainv, double boxlen, int knum, float *fvc, float *fvi, float *normals,
+    float *interp, int64_t *face_idx, float *weights, float *soft, int want_grad,
+    float *grad_fvi_zero, float *grad_feat_zero, void *workspace, size_t workspace_bytes,
+    void *stream);
+int kd_dibr_rasterization_forward_vertices_f64(
+    int batch, int height, int width, int vertex_batch, int64_t num_vertices, int64_t num_faces,
+    int feat_dim, const double *vertices, const int64_t *faces, const double *camera_proj,
+    const double *camera_transform, const double *feat, double multiplier, float eps,
+    float sigmainv, double boxlen, int knum, double *fvc, double *fvi, double *normals,
+    double *interp, int64_t *face_idx, double *weights, double *soft, int want_grad,
+    double *grad_fvi_zero, double *grad_feat_zero, void *workspace, size_t workspace_bytes,
+    void *stream);
 int kd_dibr_rasterization_backward_f32(int batch, int height, int width, int64_t num_faces,
                                        int feat_dim, const float *grad_interp,
                                        const float *grad_soft, const int64_t *face_idx,

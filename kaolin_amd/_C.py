@@ -470,6 +470,56 @@ def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertic
     return interp, face_idx, weights, soft, ws
 
 
+def dibr_rasterization_forward_vertices(height, width, vertices, faces, camera_proj,
+                                        camera_transform, face_features, sigmainv, boxlen, knum,
+                                        multiplier, eps, want_grad=True, grad_buffers=None):
+    """prepare_vertices (camera transform form) + the fused DIB-R forward with the projection
+    inside the binning launch (kd_dibr_rasterization_forward_vertices).  Returns (fvc, fvi,
+    normals, interp, face_idx, weights, soft, workspace); grad_buffers as in
+    dibr_rasterization_forward_fused."""
+    fn = 'dibr_rasterization_from_vertices'
+    dev = _check_same_gpu(fn, vertices=vertices, faces=faces, camera_proj=camera_proj,
+                          camera_transform=camera_transform, face_features=face_features)
+    Bv, V = vertices.shape[:2]
+    B, F = camera_transform.shape[0], faces.shape[0]
+    D = face_features.shape[-1]
+    _check_size(fn, 'vertices', vertices, (Bv, V, 3))
+    _check_size(fn, 'faces', faces, (F, 3))
+    _check_size(fn, 'camera_transform', camera_transform, (B, 4, 3))
+    _check_size(fn, 'face_features', face_features, (B, F, 3, D))
+    if Bv not in (1, B):
+        raise RuntimeError(f'{fn}: vertices batch {Bv} must be 1 or the camera batch {B}')
+    if faces.dtype != torch.int64:
+        raise RuntimeError(f'{fn}: faces must be int64')
+    sfx = _sfx(vertices, fn)
+    _check_dtype(fn, vertices, camera_proj=camera_proj, camera_transform=camera_transform,
+                 face_features=face_features)
+    knum = int(knum)
+    if knum < 1:
+        raise RuntimeError(f'{fn}: knum must be >= 1, got {knum}')
+    vertices, faces = vertices.contiguous(), faces.contiguous()
+    camera_proj, camera_transform = camera_proj.contiguous(), camera_transform.contiguous()
+    feat = face_features.contiguous()
+    opts = dict(device=dev, dtype=vertices.dtype)
+    fvc = torch.empty((B, F, 3, 3), **opts)
+    fvi = torch.empty((B, F, 3, 2), **opts)
+    nrm = torch.empty((B, F, 3), **opts)
+    interp = torch.empty((B, height, width, D), **opts)
+    face_idx = torch.empty((B, height, width), device=dev, dtype=torch.long)
+    weights = torch.empty((B, height, width, 3), **opts)
+    soft = torch.empty((B, height, width), **opts)
+    nb = int(_lib.load().kd_dibr_workspace_size(B, height, width, F, knum,
+                                                1 if vertices.dtype == torch.float64 else 0))
+    ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
+    _lib.call(f'kd_dibr_rasterization_forward_vertices_{sfx}', B, height, width, Bv, V, F, D,
+              _ptr(vertices), _ptr(faces), _ptr(camera_proj), _ptr(camera_transform), _ptr(feat),
+              float(multiplier), float(eps), float(sigmainv), float(boxlen), knum, _ptr(fvc),
+              _ptr(fvi), _ptr(nrm), _ptr(interp), _ptr(face_idx), _ptr(weights), _ptr(soft),
+              1 if want_grad else 0, _ptr(grad_buffers[0]) if grad_buffers else None,
+              _ptr(grad_buffers[1]) if grad_buffers else None, _ptr(ws), nb, _stream(dev))
+    return fvc, fvi, nrm, interp, face_idx, weights, soft, ws
+
+
 def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights, soft,
                                       face_vertices_image, face_features, eps, multiplier,
                                       boxlen, sigmainv, knum, workspace, need_feat=True,
@@ -791,6 +841,7 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     dibr_soft_mask_forward_fused=dibr_soft_mask_forward_fused,
     dibr_soft_mask_backward_binned=dibr_soft_mask_backward_binned,
     dibr_rasterization_forward_fused=dibr_rasterization_forward_fused,
+    dibr_rasterization_forward_vertices=dibr_rasterization_forward_vertices,
     dibr_rasterization_backward_fused=dibr_rasterization_backward_fused,
     dibr_rasterization_backward_vertices=dibr_rasterization_backward_vertices,
     prepare_vertices_forward=prepare_vertices_forward,

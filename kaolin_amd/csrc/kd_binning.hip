@@ -1,6 +1,7 @@
 // kd_binning.hip -- see kd_binning.hpp for the algorithm.
 #include "kd_binning.hpp"
 #include "kd_cull.hpp"
+#include "kd_prep.hpp"
 #include "kd_tile.hpp"
 
 #include "kd_capi.hpp"
@@ -72,16 +73,19 @@ struct BinJobs {
   FaceSet<T> fs[2];
   BinBuffers bb[2];
   SpanConsts k[2];  // make_span constants of each set (host-computed)
+  PrepOut<T> prep;  // prep.a.vertices set: the corners come from prepare_vertices (kd_bin_count PREP)
 };
 
 // One face of one set: its exact span (stored), the raster set's cull coefficients, and its
 // coarse tiles counted in LDS.  v: the face's scaled corners (loaded once for both sets).
+// nzv (PREP): the face's normal z just computed, used instead of reading fs.nz.
 template <typename T>
 __device__ __forceinline__ void bin_count_face(const FaceSet<T> &fs, const BinBuffers &bb,
                                                const SpanConsts &k, int64_t i, const T v[6],
-                                               int *s_cnt) {
+                                               int *s_cnt, const T *nzv = nullptr) {
   Span s;
-  const bool ok = (!fs.valid || fs.valid[i]) && (!fs.nz || fs.nz[i * fs.nz_stride] >= (T)0);
+  const bool ok = (!fs.valid || fs.valid[i]) &&
+                  (!fs.nz || (nzv ? *nzv : fs.nz[i * fs.nz_stride]) >= (T)0);
   if (ok) {
     T box[4];
     face_box(fs, i, v, box);
@@ -110,9 +114,18 @@ __device__ __forceinline__ void bin_count_face(const FaceSet<T> &fs, const BinBu
 // One workgroup per (chunk, view): the chunk's faces in the NS sets (NS = 2: the raster's and
 // the soft mask's boxes of the same corners, which are loaded once), their counts per coarse
 // tile written tile-major (counts[b][c][chunk]: the scan reads each tile's chunks contiguously).
-template <typename T, int PER, int NS>  // PER = chunk / 256 faces per thread
+//
+// PREP (dibr_rasterization from vertices, NS = 1): the corners come from prepare_vertices'
+// arithmetic (kd_prep.hpp) on the vertices, and the raster set's workgroups (blockIdx.z 0) also
+// write its outputs (fvc, fvi, normals; rows staged in LDS, coalesced) -- no kd_prepare_fwd
+// launch, no reading the corners back.
+template <typename T, int PER, int NS, bool PREP = false>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
+  static_assert(!PREP || NS == 1, "PREP: one face set per workgroup");
   __shared__ int s_cnt[NS][kMaxCtiles];
+  __shared__ __align__(16) T s_pc[PREP ? kBlock * 9 : 1];
+  __shared__ __align__(16) T s_pi[PREP ? kBlock * 6 : 1];
+  __shared__ __align__(16) T s_pn[PREP ? kBlock * 3 : 1];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int z0 = NS == 2 ? 0 : blockIdx.z;  // NS = 1: blockIdx.z selects the set
   const int nct = jobs.bb[z0].g.nct();
@@ -133,8 +146,27 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < PER; ++u) {
-    const int64_t i = lo + (int64_t)chunk * (PER * kBlock) + u * kBlock + tid;
-    if (i < hi) {
+    const int64_t i0 = lo + (int64_t)chunk * (PER * kBlock) + u * kBlock;
+    const int64_t i = i0 + tid;
+    if constexpr (PREP) {
+      const FaceSet<T> &fs = jobs.fs[z0];
+      if (i < hi) {
+        T c[3][3], fi[6], n[3], v[6];
+        prep_face<T>(jobs.prep.a, i, c, fi, n);
+#pragma unroll
+        for (int k = 0; k < 6; ++k) v[k] = fi[k] * fs.scale;  // load_corners' product
+        if (z0 == 0) prep_stage<T>(c, fi, n, s_pc, s_pi, s_pn);
+        bin_count_face<T>(fs, jobs.bb[z0], jobs.k[z0], i, v, s_cnt[0], &n[2]);
+      }
+      if (z0 == 0 && i0 < hi) {  // (workgroup-uniform)
+        const int rows = (int)min((int64_t)kBlock, hi - i0);
+        __syncthreads();
+        lds_to_global<T>(jobs.prep.fvc + i0 * 9, s_pc, rows * 9);
+        lds_to_global<T>(jobs.prep.fvi + i0 * 6, s_pi, rows * 6);
+        lds_to_global<T>(jobs.prep.nrm + i0 * 3, s_pn, rows * 3);
+        __syncthreads();
+      }
+    } else if (i < hi) {
       T v[6];
       load_corners(jobs.fs[z0], i, v);
 #pragma unroll
@@ -423,8 +455,13 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
         hipLaunchKernelGGL((kd_bin_count<T, 1, 2>), grid_s, dim3(kBlock), 0, stream, jobs);
       done = shared;
     }
+    const bool prep = jobs.prep.a.vertices != nullptr;
     if (done) {
-    } else if (two)
+    } else if (prep && two)
+      hipLaunchKernelGGL((kd_bin_count<T, 2, 1, true>), grid_c, dim3(kBlock), 0, stream, jobs);
+    else if (prep)
+      hipLaunchKernelGGL((kd_bin_count<T, 1, 1, true>), grid_c, dim3(kBlock), 0, stream, jobs);
+    else if (two)
       hipLaunchKernelGGL((kd_bin_count<T, 2, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
     else
       hipLaunchKernelGGL((kd_bin_count<T, 1, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
@@ -456,7 +493,7 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
 
 template <typename T>
 hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t stream) {
-  BinJobs<T> jobs;
+  BinJobs<T> jobs{};
   jobs.fs[0] = jobs.fs[1] = fs;
   jobs.bb[0] = jobs.bb[1] = bb;
   jobs.k[0] = jobs.k[1] = span_consts(fs.M, fs.H, fs.W);
@@ -465,12 +502,13 @@ hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t str
 
 template <typename T>
 hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSet<T> &fs1,
-                      const BinBuffers &bb1, hipStream_t stream) {
+                      const BinBuffers &bb1, hipStream_t stream, const PrepOut<T> *prep) {
   // both sets must describe the same views, faces and image (same chunking and tile grid)
   if (fs0.B != fs1.B || fs0.N != fs1.N || fs0.H != fs1.H || fs0.W != fs1.W ||
       bb0.nchunk != bb1.nchunk || bb0.g.nct() != bb1.g.nct())
     return hipErrorInvalidValue;
-  BinJobs<T> jobs;
+  BinJobs<T> jobs{};
+  if (prep) jobs.prep = *prep;
   jobs.fs[0] = fs0;
   jobs.fs[1] = fs1;
   jobs.bb[0] = bb0;
@@ -509,9 +547,11 @@ int zero_buffers(T *p0, int64_t n0, T *p1, int64_t n1, hipStream_t stream) {
 }
 
 template hipError_t bin_faces2<float>(const FaceSet<float> &, const BinBuffers &,
-                                      const FaceSet<float> &, const BinBuffers &, hipStream_t);
+                                      const FaceSet<float> &, const BinBuffers &, hipStream_t,
+                                      const PrepOut<float> *);
 template hipError_t bin_faces2<double>(const FaceSet<double> &, const BinBuffers &,
-                                       const FaceSet<double> &, const BinBuffers &, hipStream_t);
+                                       const FaceSet<double> &, const BinBuffers &, hipStream_t,
+                                       const PrepOut<double> *);
 template int zero_buffers<float>(float *, int64_t, float *, int64_t, hipStream_t);
 template int zero_buffers<double>(double *, int64_t, double *, int64_t, hipStream_t);
 template hipError_t bin_faces<float>(const FaceSet<float> &, const BinBuffers &, hipStream_t);

@@ -93,11 +93,16 @@ BinBuffers bin_carve(void *ws, size_t &offset, int B, int H, int W, int64_t N,
 
 template <typename T>
 hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t stream);
+template <typename T>
+struct PrepOut;  // kd_prep.hpp
 // Two face sets of the same views and image (e.g. the raster's and the soft mask's boxes) binned
-// by the same three launches (blockIdx.z selects the set).
+// by the same three launches (blockIdx.z selects the set).  prep (nullable): the corners are
+// computed from the vertices by prepare_vertices' arithmetic in the count launch, which also
+// writes its outputs (prep->fvc / fvi / nrm; fs*.fvi must point at prep->fvi).
 template <typename T>
 hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSet<T> &fs1,
-                      const BinBuffers &bb1, hipStream_t stream);
+                      const BinBuffers &bb1, hipStream_t stream,
+                      const PrepOut<T> *prep = nullptr);
 
 // Zeroes n0 elements at p0 and n1 at p1 (either may be null / 0) in one launch.
 template <typename T>

@@ -13,6 +13,7 @@
 // Results are exactly those of rasterize + dibr_soft_mask.
 #include "../../include/kaolin_dibr.h"
 #include "kd_raster.hpp"
+#include "kd_prep.hpp"
 #include "kd_raster_bwd.hpp"
 #include "kd_soft.hpp"
 
@@ -96,7 +97,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
                     double M, float eps, float sigmainv, double boxlen, int K, T *interp,
                     int64_t *face_idx, T *weights, T *soft, int want_grad, T *gz_fvi,
                     T *gz_feat, void *ws, size_t wsb, void *stream_,
-                    const IouIo<T> &iou = IouIo<T>{}) {
+                    const IouIo<T> &iou = IouIo<T>{}, const PrepOut<T> *prep = nullptr) {
   hipStream_t stream = (hipStream_t)stream_;
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
   KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
@@ -136,7 +137,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
     d.sbb.clear_b = (int *)iou.acc;
     d.sbb.n_clear_b = 4 * kIouParts * B;
   }
-  hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream);
+  hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream, prep);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> ra{rfs, d.rbb, fvz, fvz_fs, fvz_cs, feat, D, eps, interp, face_idx, weights};
   SoftArgs<T> sa{};
@@ -167,6 +168,39 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   }
   if (rc != KD_OK || !iou.gt) return rc;
   return iou_finish_launch<T>(B, kIouParts, iou.acc, iou.stats, iou.loss, stream);
+}
+
+// prepare_vertices (camera transform form) + dibr_rasterization's forward, the projection done
+// by the binning count (kd_bin_count PREP), which also writes prepare_vertices' outputs: the
+// DIB-R training step's forward without a kd_prepare_fwd launch and without reading the corners
+// back.
+template <typename T>
+int prep_vertices_forward(int B, int Bv, int64_t V, int64_t F, const T *vert, const int64_t *faces,
+                          const T *proj, const T *tf, T *fvc, T *fvi, T *nrm, void *stream);
+
+template <typename T>
+static int dibr_fwd_vertices(int B, int H, int W, int Bv, int64_t V, int64_t F, int D,
+                             const T *vert, const int64_t *faces, const T *proj, const T *tf,
+                             const T *feat, double M, float eps, float sigmainv, double boxlen,
+                             int K, T *fvc, T *fvi, T *nrm, T *interp, int64_t *face_idx,
+                             T *weights, T *soft, int want_grad, T *gz_fvi, T *gz_feat, void *ws,
+                             size_t wsb, void *stream) {
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0 && V >= 0, "negative size");
+  KD_CHECK_ARG(Bv == 1 || Bv == B, "vertex batch must be 1 or the view count");
+  KD_CHECK_ARG((int64_t)B * F == 0 || (vert && faces && proj && tf && fvc && fvi && nrm),
+               "from vertices: NULL input or output");
+  if ((int64_t)B * F == 0 || H == 0 || W == 0) {  // no binning: prepare_vertices alone
+    const int rc = prep_vertices_forward<T>(B, Bv, V, F, vert, faces, proj, tf, fvc, fvi, nrm,
+                                            stream);
+    if (rc != KD_OK) return rc;
+    return dibr_fwd<T>(B, H, W, F, D, fvc + 2, 9, 3, fvi, feat, nrm + 2, 3, M, eps, sigmainv,
+                       boxlen, K, interp, face_idx, weights, soft, want_grad, gz_fvi, gz_feat,
+                       ws, wsb, stream);
+  }
+  const PrepOut<T> prep{PrepArgs<T>{B, Bv, V, F, vert, faces, proj, tf}, fvc, fvi, nrm};
+  return dibr_fwd<T>(B, H, W, F, D, fvc + 2, 9, 3, fvi, feat, nrm + 2, 3, M, eps, sigmainv,
+                     boxlen, K, interp, face_idx, weights, soft, want_grad, gz_fvi, gz_feat, ws,
+                     wsb, stream, IouIo<T>{}, &prep);
 }
 
 template <typename T>
@@ -308,6 +342,30 @@ int kd_dibr_rasterization_forward_f32(int B, int H, int W, int64_t F, int D, con
                          normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
                          face_idx, weights, soft, want_grad, grad_fvi_zero, grad_feat_zero, ws,
                          wsb, stream);
+}
+int kd_dibr_rasterization_forward_vertices_f32(
+    int B, int H, int W, int vertex_batch, int64_t V, int64_t F, int D, const float *vertices,
+    const int64_t *faces, const float *camera_proj, const float *camera_transform,
+    const float *feat, double M, float eps, float sigmainv, double boxlen, int knum, float *fvc,
+    float *fvi, float *normals, float *interp, int64_t *face_idx, float *weights, float *soft,
+    int want_grad, float *grad_fvi_zero, float *grad_feat_zero, void *ws, size_t wsb,
+    void *stream) {
+  return dibr_fwd_vertices<float>(B, H, W, vertex_batch, V, F, D, vertices, faces, camera_proj,
+                                  camera_transform, feat, M, eps, sigmainv, boxlen, knum, fvc, fvi,
+                                  normals, interp, face_idx, weights, soft, want_grad,
+                                  grad_fvi_zero, grad_feat_zero, ws, wsb, stream);
+}
+int kd_dibr_rasterization_forward_vertices_f64(
+    int B, int H, int W, int vertex_batch, int64_t V, int64_t F, int D, const double *vertices,
+    const int64_t *faces, const double *camera_proj, const double *camera_transform,
+    const double *feat, double M, float eps, float sigmainv, double boxlen, int knum, double *fvc,
+    double *fvi, double *normals, double *interp, int64_t *face_idx, double *weights,
+    double *soft, int want_grad, double *grad_fvi_zero, double *grad_feat_zero, void *ws,
+    size_t wsb, void *stream) {
+  return dibr_fwd_vertices<double>(B, H, W, vertex_batch, V, F, D, vertices, faces, camera_proj,
+                                   camera_transform, feat, M, eps, sigmainv, boxlen, knum, fvc,
+                                   fvi, normals, interp, face_idx, weights, soft, want_grad,
+                                   grad_fvi_zero, grad_feat_zero, ws, wsb, stream);
 }
 int kd_dibr_rasterization_forward_f64(int B, int H, int W, int64_t F, int D, const double *fvz,
                                       int64_t fvz_face_stride, int64_t fvz_corner_stride,

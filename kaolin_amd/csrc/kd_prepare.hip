@@ -19,38 +19,10 @@
 #include "../../include/kaolin_dibr.h"
 #include "kd_capi.hpp"
 #include "kd_common.hpp"
+#include "kd_prep.hpp"
 #include "kd_tile.hpp"
 
 namespace kd {
-
-template <typename T>
-struct PrepArgs {
-  int B, Bv;        // views; vertex batches (1 = shared by all views, else B)
-  int64_t V, F;
-  const T *vertices;   // (Bv, V, 3)
-  const int64_t *faces;  // (F, 3)
-  const T *proj;       // (3)
-  const T *tf;         // (B, 4, 3)
-};
-
-template <typename T>
-__device__ __forceinline__ void cam_point(const T *tf, const T *p, T c[3]) {
-#pragma unroll
-  for (int j = 0; j < 3; ++j) c[j] = p[0] * tf[j] + p[1] * tf[3 + j] + p[2] * tf[6 + j] + tf[9 + j];
-}
-
-// Copies n elements of T from LDS to global memory with the workgroup, 16-byte vectors when
-// both sides allow (the rows of a workgroup are contiguous in every output).
-template <typename T>
-__device__ __forceinline__ void lds_to_global(T *dst, const T *src, int n) {
-  if ((((uintptr_t)dst | (uintptr_t)src) & 15) == 0 && (n * sizeof(T)) % 16 == 0) {
-    const int nv = n * (int)sizeof(T) / 16;
-    for (int k = threadIdx.x; k < nv; k += kBlock)
-      reinterpret_cast<float4 *>(dst)[k] = reinterpret_cast<const float4 *>(src)[k];
-  } else {
-    for (int k = threadIdx.x; k < n; k += kBlock) dst[k] = src[k];
-  }
-}
 
 // One thread per (view, face) row; the rows' outputs (9 + 6 + 3 values each) are assembled in
 // LDS and written by the workgroup as contiguous, coalesced runs.
@@ -64,36 +36,9 @@ __global__ __launch_bounds__(kBlock) void kd_prepare_fwd(PrepArgs<T> a, T *fvc, 
     const int64_t i = i0 + threadIdx.x;
     const int rows = (int)min((int64_t)kBlock, total - i0);
     if (i < total) {
-      const int b = (int)(i / a.F);
-      const int64_t f = i - (int64_t)b * a.F;
-      const T *vb = a.vertices + (a.Bv == 1 ? 0 : (int64_t)b * a.V * 3);
-      const T *tf = a.tf + (int64_t)b * 12;
-      T c[3][3];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const int64_t v = a.faces[f * 3 + k];
-        cam_point<T>(tf, vb + v * 3, c[k]);
-      }
-      T *oc = s_c + threadIdx.x * 9;
-      T *oi = s_i + threadIdx.x * 6;
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        oc[k * 3 + 0] = c[k][0];
-        oc[k * 3 + 1] = c[k][1];
-        oc[k * 3 + 2] = c[k][2];
-        const T pz = c[k][2] * a.proj[2];
-        oi[k * 2 + 0] = c[k][0] * a.proj[0] / pz;
-        oi[k * 2 + 1] = c[k][1] * a.proj[1] / pz;
-      }
-      const T e1[3] = {c[1][0] - c[0][0], c[1][1] - c[0][1], c[1][2] - c[0][2]};
-      const T e2[3] = {c[2][0] - c[0][0], c[2][1] - c[0][1], c[2][2] - c[0][2]};
-      const T n[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
-                      e1[0] * e2[1] - e1[1] * e2[0]};
-      const T len = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]) + (T)1e-10;
-      T *on = s_n + threadIdx.x * 3;
-      on[0] = n[0] / len;
-      on[1] = n[1] / len;
-      on[2] = n[2] / len;
+      T c[3][3], fi[6], n[3];
+      prep_face<T>(a, i, c, fi, n);
+      prep_stage<T>(c, fi, n, s_c, s_i, s_n);
     }
     __syncthreads();
     lds_to_global<T>(fvc + i0 * 9, s_c, rows * 9);
@@ -216,6 +161,21 @@ __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T 
     gv[s_vid[kBlock - 1 - sg] * 3 + q] = s_acc[sg][q];
   }
 }
+
+template <typename T>
+static int prep_fwd(int B, int Bv, int64_t V, int64_t F, const T *vert, const int64_t *faces,
+                    const T *proj, const T *tf, T *fvc, T *fvi, T *nrm, void *stream);
+template <typename T>
+int prep_vertices_forward(int B, int Bv, int64_t V, int64_t F, const T *vert, const int64_t *faces,
+                          const T *proj, const T *tf, T *fvc, T *fvi, T *nrm, void *stream) {
+  return prep_fwd<T>(B, Bv, V, F, vert, faces, proj, tf, fvc, fvi, nrm, stream);
+}
+template int prep_vertices_forward<float>(int, int, int64_t, int64_t, const float *,
+                                          const int64_t *, const float *, const float *, float *,
+                                          float *, float *, void *);
+template int prep_vertices_forward<double>(int, int, int64_t, int64_t, const double *,
+                                           const int64_t *, const double *, const double *,
+                                           double *, double *, double *, void *);
 
 template <typename T>
 static int prep_fwd(int B, int Bv, int64_t V, int64_t F, const T *vert, const int64_t *faces,

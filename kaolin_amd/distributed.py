@@ -196,7 +196,7 @@ class GradBucket:
 def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_features, height,
                           width, grad_interp, grad_soft, sigmainv=7000., boxlen=0.02, knum=30,
                           prepare=None, render=None, gt_mask=None, iou='fused',
-                          fused_vertices=False):
+                          fused_vertices=True):
     """The GPU part of one DIB-R training step on this rank's views: project the
     shared mesh to the rank's cameras (``prepare_vertices``, utils.py:128-175), render
     (``dibr_rasterization``, dibr.py:119-209, valid faces = normals z >= 0) and back-propagate
@@ -211,8 +211,10 @@ def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_f
     mask_iou(soft_mask, gt_mask) (metrics/render.py:18-40, ian_dibr.py:264-265) instead of
     grad_soft: fused into the renderer (iou='fused', dibr_rasterization_with_mask_iou) or as the
     composition dibr_rasterization + mask_iou (iou='compose').
-    fused_vertices: ``dibr_rasterization_from_vertices`` (the face -> vertex step inside the DIB-R
-    backward kernel) instead of prepare_vertices + dibr_rasterization (HIP kernels, no gt_mask).
+    fused_vertices (default; HIP kernels, no gt_mask): ``dibr_rasterization_from_vertices``, one
+    node whose forward projects the vertices inside the binning launch (no kd_prepare_fwd), instead
+    of prepare_vertices + dibr_rasterization.  C3, same box (profiles/r04/ab_vp*.txt): 0.2963 ->
+    0.2949 ms per step at 8 views, 0.1082 -> 0.1056 at 1 view.
     Returns face_idx (B_rank, H, W)."""
     B = camera_transform.shape[0]
     if fused_vertices and gt_mask is None and prepare is None and render is None:

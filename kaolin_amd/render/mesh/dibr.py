@@ -182,41 +182,49 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
     return interp, soft, face_idx
 
 
-class DibrRenderHip(Function):
-    """prepare_vertices + dibr_rasterization as one autograd node whose backward runs the
-    face -> vertex step inside the DIB-R backward kernel (kd_dibr_rasterization_backward_vertices,
-    SURVEY.md §8 f1): the corner gradients of the raster and the soft mask go straight to the
-    vertex gradient, with no (B, F, 3, 2) gradient and no separate scatter kernel.
+# The from-vertices node's backward: False = the DIB-R backward's grad_fvi then prepare_vertices'
+# gather kernel (the faster form, measured below); True = the face -> vertex step inside the
+# DIB-R backward kernel (kd_dibr_rasterization_backward_vertices).
+FUSED_VERTEX_BACKWARD = False
 
-    Measured at C3 (same box, bench.py --vertex-bwd fused, profiles/r04/ab_vtx*.txt): the fused
-    backward takes 156 us against 68.6 + 18.5 us for the DIB-R backward plus kd_prepare_bwd at 8
-    views (step 0.369 vs 0.302 ms), and 31 against 18.7 + 10.7 us at 1 view -- the vertex
-    atomics (3 per corner, every vertex shared by ~6 faces and every view) serialise where the
-    per-face grad_fvi atomics did not; per-(tile, vertex) LDS sums before the projection (round
-    4) did not change that.  The training step (kaolin_amd.distributed) therefore keeps the
-    two-kernel path; this node stays as the f1 entry point, parity-tested
-    (tests/test_gpu_vertices.py)."""
+
+class DibrRenderHip(Function):
+    """prepare_vertices + dibr_rasterization as one autograd node.
+
+    Forward: kd_dibr_rasterization_forward_vertices -- the projection runs inside the binning
+    launch, which also writes prepare_vertices' outputs, so no kd_prepare_fwd launch runs and the
+    corners are not read back.  Backward: the DIB-R backward's grad_fvi, then prepare_vertices'
+    gather kernel over the vertex -> corner CSR (kd_prepare_bwd); or, with
+    FUSED_VERTEX_BACKWARD, the face -> vertex step inside the DIB-R backward kernel
+    (kd_dibr_rasterization_backward_vertices), which measured slower at C3 (same box, bench.py
+    --vertex-bwd fused, profiles/r04/ab_vtx*.txt): 156 us against 68.6 + 18.5 us for the two
+    kernels at 8 views, 31 against 18.7 + 10.7 at 1 view -- the vertex atomics (3 per corner,
+    every vertex shared by ~6 faces and every view) serialise where the per-face grad_fvi
+    atomics did not (per-(tile, vertex) LDS sums before the projection did not change that)."""
 
     @staticmethod
     def forward(ctx, vertices, faces, camera_proj, camera_transform, face_features, height,
                 width, sigmainv, boxlen, knum, multiplier, eps):
-        vertices = vertices.contiguous()
-        camera_proj = camera_proj.contiguous()
-        camera_transform = camera_transform.contiguous()
-        face_features = face_features.contiguous()
-        fvc, fvi, nrm = _C.prepare_vertices_forward(vertices, faces, camera_proj,
-                                                    camera_transform)
+        need_v = vertices.requires_grad
         need_feat = face_features.requires_grad
-        want_grad = vertices.requires_grad or need_feat
-        gfeat_buf = torch.empty(face_features.shape, device=face_features.device,
-                                dtype=face_features.dtype) if want_grad and need_feat else None
-        interp, face_idx, weights, soft, ws = _C.render.mesh.dibr_rasterization_forward_fused(
-            height, width, fvc[..., 2], fvi, face_features, nrm[..., 2], sigmainv, boxlen, knum,
-            multiplier, eps, want_grad=want_grad,
-            grad_buffers=(None, gfeat_buf) if want_grad else None)
+        want_grad = need_v or need_feat
+        fused_vtx = FUSED_VERTEX_BACKWARD
+        B, F = camera_transform.shape[0], faces.shape[0]
+        opts = dict(device=vertices.device, dtype=vertices.dtype)
+        gfvi_buf = torch.empty((B, F, 3, 2), **opts) if want_grad and not fused_vtx else None
+        gfeat_buf = torch.empty(face_features.shape, **opts) if want_grad and need_feat else None
+        fvc, fvi, nrm, interp, face_idx, weights, soft, ws = \
+            _C.render.mesh.dibr_rasterization_forward_vertices(
+                height, width, vertices, faces, camera_proj, camera_transform, face_features,
+                sigmainv, boxlen, knum, multiplier, eps, want_grad=want_grad,
+                grad_buffers=(gfvi_buf, gfeat_buf) if want_grad else None)
         ctx.save_for_backward(face_idx, weights, soft, fvi, fvc, face_features, faces,
-                              camera_proj, camera_transform, ws if want_grad else None)
-        ctx.gfeat_buf = gfeat_buf
+                              camera_proj.contiguous(), camera_transform.contiguous(),
+                              ws if want_grad else None)
+        ctx.bufs = (gfvi_buf, gfeat_buf)
+        ctx.fused_vtx = fused_vtx
+        from .utils import _adjacency
+        ctx.adj = _adjacency(faces, vertices.shape[1]) if need_v and not fused_vtx else None
         ctx.params = (eps, multiplier, boxlen, sigmainv, knum)
         ctx.vshape = (vertices.shape[0], vertices.shape[1])
         ctx.mark_non_differentiable(face_idx)
@@ -231,15 +239,27 @@ class DibrRenderHip(Function):
         (face_idx, weights, soft, fvi, fvc, feat, faces, proj, tf,
          workspace) = ctx.saved_tensors
         eps, multiplier, boxlen, sigmainv, knum = ctx.params
-        # the forward zeroed one grad_feat buffer: the first backward fills it, a second one
-        # (retained graph) gets a fresh buffer zeroed by the backward itself
-        buf, ctx.gfeat_buf = ctx.gfeat_buf, None
-        gvert, gfeat = _C.render.mesh.dibr_rasterization_backward_vertices(
-            grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier, boxlen,
-            sigmainv, knum, workspace, faces, fvc, proj, tf, ctx.vshape[0], ctx.vshape[1],
-            need_feat=need_feat, grad_feat_buffer=buf)
-        return (gvert if need_v else None, None, None, None, gfeat, None, None, None, None,
-                None, None, None)
+        # the forward zeroed one set of gradient buffers: the first backward fills them, a second
+        # one (retained graph) gets fresh buffers zeroed by the backward itself
+        bufs, ctx.bufs = ctx.bufs, (None, None)
+        if ctx.fused_vtx:
+            gvert, gfeat = _C.render.mesh.dibr_rasterization_backward_vertices(
+                grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier,
+                boxlen, sigmainv, knum, workspace, faces, fvc, proj, tf, ctx.vshape[0],
+                ctx.vshape[1], need_feat=need_feat, grad_feat_buffer=bufs[1])
+        else:
+            gfvi, gfeat = _C.render.mesh.dibr_rasterization_backward_fused(
+                grad_interp, grad_soft, face_idx, weights, soft, fvi, feat, eps, multiplier,
+                boxlen, sigmainv, knum, workspace, need_feat=need_feat,
+                grad_buffers=bufs if bufs[0] is not None else None)
+            gvert = None
+            if need_v:
+                from .utils import _adjacency
+                adj = ctx.adj if ctx.adj is not None else _adjacency(faces, ctx.vshape[1])
+                gvert = _C.prepare_vertices_backward(faces, proj, tf, fvc, None, gfvi, None, adj,
+                                                     ctx.vshape[0], ctx.vshape[1])
+        return (gvert if need_v else None, None, None, None, gfeat if need_feat else None, None,
+                None, None, None, None, None, None)
 
 
 def dibr_rasterization_from_vertices(height, width, vertices, faces, camera_proj,
@@ -247,19 +267,20 @@ def dibr_rasterization_from_vertices(height, width, vertices, faces, camera_proj
                                      boxlen=0.02, knum=30, multiplier=None, eps=None):
     r"""``prepare_vertices`` (utils.py:128-175, camera_transform form) followed by
     ``dibr_rasterization`` of its outputs (the DIB-R training step, examples/tutorial/
-    ian_dibr.py), as one autograd node with the face -> vertex step fused into the backward
-    kernel.  vertices (1 or B, V, 3), faces (F, 3) int64, camera_proj (3, 1),
+    ian_dibr.py), as one autograd node (DibrRenderHip: the projection inside the binning launch;
+    SURVEY.md §8 f1).  vertices (1 or B, V, 3), faces (F, 3) int64, camera_proj (3, 1),
     camera_transform (B, 4, 3), face_features (B, F, 3, D) (or a list, concatenated).  Returns
     (interpolated_features, soft_mask, face_idx), the same values as
     ``dibr_rasterization(h, w, fvc[..., 2], fvi, face_features, normals[..., 2], ...)``; the
     gradients flow to vertices and face_features.  Falls back to that composition when it
-    cannot fuse (feature dim > 3, camera tensors requiring grad, close_lists mode)."""
+    cannot fuse (camera tensors requiring grad, close_lists mode, feature dim > 3 with
+    FUSED_VERTEX_BACKWARD)."""
     feats = torch.cat(face_features, dim=-1) \
         if isinstance(face_features, (list, tuple)) else face_features
     _multiplier = 1000. if multiplier is None else multiplier
     _eps = 1e-8 if eps is None else eps
-    if (feats.shape[-1] > 3 or camera_proj.requires_grad or camera_transform.requires_grad
-            or _lists_enabled()):
+    if ((FUSED_VERTEX_BACKWARD and feats.shape[-1] > 3) or camera_proj.requires_grad or
+            camera_transform.requires_grad or _lists_enabled()):
         from .utils import prepare_vertices
         fvc, fvi, nrm = prepare_vertices(vertices, faces, camera_proj,
                                          camera_transform=camera_transform)

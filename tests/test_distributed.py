@@ -327,7 +327,7 @@ def test_grad_bucket_mixed_dtypes_world2():
 def _bench_args():
     import types
     return types.SimpleNamespace(dtype='f32', config='c1', sigmainv=7000., boxlen=0.02,
-                                 knum=30, iou=None, vertex_bwd='gather')
+                                 knum=30, iou=None, vertex_path='compose')
 
 
 def _bench_rank_step(first, n, total):

@@ -1,4 +1,6 @@
-"""GPU: dibr_rasterization_from_vertices -- prepare_vertices + dibr_rasterization with the
+"""GPU: dibr_rasterization_from_vertices -- prepare_vertices + dibr_rasterization as one node
+whose forward projects the vertices inside the binning launch (kd_dibr_rasterization_forward_
+vertices) and whose backward is either the DIB-R backward + prepare_vertices' gather kernel or the
 face -> vertex step fused into the DIB-R backward kernel (SURVEY.md §8 f1,
 kd_dibr_rasterization_backward_vertices).
 
@@ -26,6 +28,17 @@ def _native():
     from kaolin_amd import _lib
     _lib.load()
     assert torch.cuda.is_available()
+
+
+@pytest.fixture(autouse=True, params=['gather', 'fused'])
+def vertex_backward(request):
+    """both backwards of the from-vertices node: the DIB-R backward + prepare_vertices' gather
+    kernel (default) and the face -> vertex step inside the DIB-R backward kernel"""
+    from kaolin_amd.render.mesh import dibr
+    old = dibr.FUSED_VERTEX_BACKWARD
+    dibr.FUSED_VERTEX_BACKWARD = request.param == 'fused'
+    yield request.param
+    dibr.FUSED_VERTEX_BACKWARD = old
 
 
 def _scene(n_lon, n_lat, B, dt, elevation=0.3, shared=True, seed=0):
@@ -137,3 +150,23 @@ def test_fused_vertex_backward_retained_graph():
     b = torch.autograd.grad([interp, soft], [v, feats], [g1, g2])
     _close(a[0], b[0], dt)
     _close(a[1], b[1], dt)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_from_vertices_forward_outputs_match_prepare(dname):
+    """the binning launch's prepare_vertices outputs equal kd_prepare_vertices_forward's bit for
+    bit, and the render equals dibr_rasterization of them (C3 views, shared and per-view
+    vertices)"""
+    from kaolin_amd import _C
+    from kaolin_amd.render.mesh import dibr_rasterization
+    dt = TORCH_DTYPES[dname]
+    h = 256
+    for shared in (True, False):
+        v, faces, proj, cam, feats = _scene(250, 101, 2, dt, shared=shared)
+        fvc, fvi, nrm, interp, face_idx, weights, soft, _ = \
+            _C.render.mesh.dibr_rasterization_forward_vertices(
+                h, h, v, faces, proj, cam, feats, 7000., 0.02, 30, 1000., 1e-8, want_grad=False)
+        c2, i2, n2 = _C.prepare_vertices_forward(v, faces, proj, cam)
+        assert torch.equal(fvc, c2) and torch.equal(fvi, i2) and torch.equal(nrm, n2)
+        ri, rs, rf = dibr_rasterization(h, h, c2[..., 2], i2, feats, n2[..., 2])
+        assert torch.equal(interp, ri) and torch.equal(soft, rs) and torch.equal(face_idx, rf)
