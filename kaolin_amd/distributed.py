@@ -201,8 +201,7 @@ def dibr_forward_backward(vertices, faces, camera_proj, camera_transform, face_f
     shared mesh to the rank's cameras (``prepare_vertices``, utils.py:128-175), render
     (``dibr_rasterization``, dibr.py:119-209, valid faces = normals z >= 0) and back-propagate
     the fixed upstream gradients ``[grad_interp, grad_soft]`` into ``vertices.grad`` (summed over
-    the rank's views) and the features' gradient.  (The fused alternative,
-    ``dibr_rasterization_from_vertices``, measured slower: see its docstring.)
+    the rank's views) and the features' gradient.
 
     vertices (V, 3) leaf, faces (F, 3) int64, camera_transform (B_rank, 4, 3), face_features
     (B_rank, F, 3, D) or (1, F, 3, D) shared.  `prepare` / `render` default to the HIP kernels
