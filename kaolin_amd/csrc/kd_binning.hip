@@ -115,13 +115,12 @@ __device__ __forceinline__ void bin_count_face(const FaceSet<T> &fs, const BinBu
 // the soft mask's boxes of the same corners, which are loaded once), their counts per coarse
 // tile written tile-major (counts[b][c][chunk]: the scan reads each tile's chunks contiguously).
 //
-// PREP (dibr_rasterization from vertices, NS = 1): the corners come from prepare_vertices'
-// arithmetic (kd_prep.hpp) on the vertices, and the raster set's workgroups (blockIdx.z 0) also
-// write its outputs (fvc, fvi, normals; rows staged in LDS, coalesced) -- no kd_prepare_fwd
-// launch, no reading the corners back.
+// PREP (dibr_rasterization from vertices): the corners come from prepare_vertices' arithmetic
+// (kd_prep.hpp) on the vertices, and the raster set's workgroups (blockIdx.z 0; NS = 2: every
+// workgroup) also write its outputs (fvc, fvi, normals; rows staged in LDS, coalesced) -- no
+// kd_prepare_fwd launch, no reading the corners back.
 template <typename T, int PER, int NS, bool PREP = false>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
-  static_assert(!PREP || NS == 1, "PREP: one face set per workgroup");
   __shared__ int s_cnt[NS][kMaxCtiles];
   __shared__ __align__(16) T s_pc[PREP ? kBlock * 9 : 1];
   __shared__ __align__(16) T s_pi[PREP ? kBlock * 6 : 1];
@@ -156,7 +155,10 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 #pragma unroll
         for (int k = 0; k < 6; ++k) v[k] = fi[k] * fs.scale;  // load_corners' product
         if (z0 == 0) prep_stage<T>(c, fi, n, s_pc, s_pi, s_pn);
-        bin_count_face<T>(fs, jobs.bb[z0], jobs.k[z0], i, v, s_cnt[0], &n[2]);
+#pragma unroll
+        for (int z = 0; z < NS; ++z)
+          bin_count_face<T>(jobs.fs[z0 + z], jobs.bb[z0 + z], jobs.k[z0 + z], i, v, s_cnt[z],
+                            &n[2]);
       }
       if (z0 == 0 && i0 < hi) {  // (workgroup-uniform)
         const int rows = (int)min((int64_t)kBlock, hi - i0);

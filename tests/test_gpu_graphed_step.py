@@ -97,3 +97,25 @@ def test_graphed_step_replays_match_eager(cfg, iou):
     _, gfeat = oracle.rasterize_backward(N(s['g_feat']), rf, rw, N(fvi), feats0, 1e-8)
     np.testing.assert_allclose(N(s['feats'].grad), gfeat, rtol=1e-4,
                                atol=1e-5 * np.abs(gfeat).max())
+
+
+def test_graphed_step_with_close_lists_matches_eager():
+    """the reference-structured path (the (B, H, W, K) close-face lists materialised by the
+    forward and read by the backward, bench.py --lists) captured and replayed"""
+    from kaolin_amd import distributed
+    from kaolin_amd.render.mesh import dibr
+    s = _setup(100, 51, 256, 2, False)
+    with dibr.close_lists(True):
+        e_fidx, e_gv, e_gf = _eager(s)
+        gs = distributed.GraphedStep([s['vertices'], s['feats']], _fn(s),
+                                     params_to_reduce=[s['vertices']])
+        for rep in range(2):
+            s['vertices'].grad.fill_(float('nan'))
+            s['feats'].grad.fill_(float('nan'))
+            gs.out.fill_(-7)
+            fidx = gs()
+            torch.cuda.synchronize()
+            assert torch.equal(fidx, e_fidx), rep
+            for x, y in ((s['vertices'].grad, e_gv), (s['feats'].grad, e_gf)):
+                scale = y.abs().max().item()
+                torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * scale)
