@@ -16,7 +16,9 @@ static int64_t fine_tiles(int H, int W) {
 
 size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view, int ct0) {
   const BinGeom g = bin_geom(H, W, ct0);
-  const int chunk = bin_chunk(B, max_per_view);
+  // sized for the smaller chunk (the most chunks) whatever bin_chunk picks: the diagnostic flag
+  // that forces 256-face chunks may change between a size query and a forward
+  const int chunk = kChunk / 2;
   const int64_t nchunk = (max_per_view + chunk - 1) / chunk;
   size_t s = 0;
   s += align_up(sizeof(Span) * (size_t)N);

@@ -119,3 +119,70 @@ def test_graphed_step_with_close_lists_matches_eager():
             for x, y in ((s['vertices'].grad, e_gv), (s['feats'].grad, e_gf)):
                 scale = y.abs().max().item()
                 torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * scale)
+
+
+def _two_rank_worker(rank, port, out_dir):
+    """One rank of test_graphed_step_two_ranks: the eager dibr_step and the captured step (two
+    reduced parameters: the vertices and a shared feature table, so GradBucket packs both into
+    its flat buffer inside the graph) over a gloo group, both ranks on cuda:0."""
+    import torch.distributed as dist
+    from kaolin_amd import _lib, distributed, workloads
+    dist.init_process_group('gloo', init_method=f'tcp://127.0.0.1:{port}', rank=rank,
+                            world_size=2)
+    try:
+        _lib.load()
+        h, total = 128, 2
+        verts, faces, face_uvs = workloads.uv_sphere(40, 21, seed=0)
+        vertices = verts.to(DEV).requires_grad_(True)
+        faces = faces.to(DEV)
+        cam = workloads.orbit_cameras(total, 0.3)[rank:rank + 1].to(DEV)
+        proj = workloads.generate_perspective_projection(math.pi / 4).to(DEV)
+        uvs = face_uvs.to(DEV).unsqueeze(0)
+        feats = torch.cat([uvs, torch.ones_like(uvs[..., :1])], dim=-1).contiguous()
+        feats.requires_grad_(True)  # (1, F, 3, 3): shared by the views, reduced over the ranks
+        g_feat, g_soft = workloads.view_grads(rank, 1, h, h, 3)
+        g_feat, g_soft = g_feat.to(DEV), g_soft.to(DEV)
+        distributed.dibr_step(vertices, faces, proj, cam, feats, h, h, g_feat, g_soft,
+                              shared=[feats])
+        torch.cuda.synchronize()
+        e_gv, e_gf = vertices.grad.clone(), feats.grad.clone()
+        fn = (lambda: distributed.dibr_forward_backward(vertices, faces, proj, cam, feats, h, h,
+                                                        g_feat, g_soft))
+        gs = distributed.GraphedStep([vertices, feats], fn, params_to_reduce=[vertices, feats])
+        for rep in range(2):
+            vertices.grad.fill_(float('nan'))
+            feats.grad.fill_(float('nan'))
+            gs()
+            torch.cuda.synchronize()
+            for x, y in ((vertices.grad, e_gv), (feats.grad, e_gf)):
+                scale = y.abs().max().item()
+                assert scale > 0
+                torch.testing.assert_close(x, y, rtol=1e-4, atol=1e-5 * scale)
+        torch.save({'gv': e_gv.cpu(), 'gf': e_gf.cpu()}, f'{out_dir}/rank{rank}.pt')
+    finally:
+        dist.destroy_process_group()
+
+
+def test_graphed_step_two_ranks(tmp_path):
+    """GraphedStep's captured GradBucket.pack() and its all-reduce after the replay, with a real
+    process group: two gloo ranks on one GPU, each rendering its own view; the
+    replayed gradients equal the eager dibr_step's, and the reduced gradients agree across ranks"""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context('spawn')
+    procs = [ctx.Process(target=_two_rank_worker, args=(r, port, str(tmp_path))) for r in (0, 1)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    r0 = torch.load(tmp_path / 'rank0.pt', weights_only=True)
+    r1 = torch.load(tmp_path / 'rank1.pt', weights_only=True)
+    for k in ('gv', 'gf'):
+        torch.testing.assert_close(r0[k], r1[k], rtol=0, atol=0)
