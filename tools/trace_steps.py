@@ -32,7 +32,12 @@ for (k, n), v in sorted(agg.items()):
     durs = sorted(x[0] for x in v)
     gaps = sorted(x[1] for x in v)
     print(f'  {k:2d} {n[:60]:60s} dur {durs[len(durs) // 2]:7.2f}  gap {gaps[len(gaps) // 2]:6.2f}')
-# steps' starts: period
-if len(steps) > 2:
-    per = [(steps[i + 1][0][0] - steps[i][0][0]) / 1e3 for i in range(len(steps) - 1)]
-    print(f'step period (start to start) median {sorted(per)[len(per) // 2]:.1f} us')
+# the period of consecutive steps in time order (the timed loop's replays are back to back: the
+# shortest periods), and the gap between one step's last kernel and the next step's first
+allst = [kd[a:b] for a, b in zip(starts, starts[1:])]
+pairs = sorted(((allst[i + 1][0][0] - allst[i][0][0]) / 1e3,
+                (allst[i + 1][0][0] - allst[i][-1][1]) / 1e3) for i in range(len(allst) - 1))
+if pairs:
+    best = pairs[:max(1, len(pairs) // 2)]
+    print(f'step period (start to start, consecutive replays) median '
+          f'{best[len(best) // 2][0]:.1f} us; gap between replays {best[len(best) // 2][1]:.1f} us')
