@@ -87,6 +87,14 @@ int kd_set_tile_split(int split);
  * choice). */
 int kd_set_coarse_tile(int px);
 
+/* Tile cost history of dibr_rasterization's fp32 forward (a tuning hook; 1 by default).  The
+ * one-launch forward records each 16x16 tile's duration in a library-owned device buffer (one
+ * per device, 2 MB, kept for the process), and the next call of the same shape dispatches its
+ * tiles heaviest-first by those durations instead of by their coarse bins' face counts (a
+ * silhouette tile's soft-mask work shows only after its raster phase).  Results never depend
+ * on it; 0 turns it off. */
+int kd_set_tile_history(int on);
+
 /* Pool limits (a test and tuning hook; both 1 by default).  The workspaces hold two bounded
  * pools whose layout depends only on the call's sizes: the coarse bins (16 entries per face row)
  * and the soft mask's (pixel, close face) records (min(knum, 12) per pixel plus block slack).

@@ -137,6 +137,8 @@ def load():
             lib.kd_set_tile_split.restype = c_int
             lib.kd_set_coarse_tile.argtypes = [c_int]
             lib.kd_set_coarse_tile.restype = c_int
+            lib.kd_set_tile_history.argtypes = [c_int]
+            lib.kd_set_tile_history.restype = c_int
             lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
             lib.kd_prepare_vertices_ranges.restype = c_i64
             # diagnostic build only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
@@ -205,6 +207,13 @@ def set_coarse_tile(px=0):
     """dibr_rasterization's coarse bin edge (kd_set_coarse_tile, a test and tuning hook): 16 or
     32 pixels; 0 restores the default (32).  Hold it between a forward and its backward."""
     if load().kd_set_coarse_tile(int(px)) != KD_OK:
+        raise RuntimeError(load().kd_last_error().decode(errors='replace'))
+
+
+def set_tile_history(on=True):
+    """Dispatch the fused fp32 forward's tiles by the previous same-shape call's tile durations
+    (kd_set_tile_history, a tuning hook; on by default).  Results never depend on it."""
+    if load().kd_set_tile_history(1 if on else 0) != KD_OK:
         raise RuntimeError(load().kd_last_error().decode(errors='replace'))
 
 

@@ -55,6 +55,7 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   bb.order = (int2 *)(base + off);
   off += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
   bb.cull_eps = 0.f;
+  bb.hist = nullptr;
   bb.clear = nullptr;
   bb.n_clear = 0;
   bb.clear_b = nullptr;
@@ -340,13 +341,16 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
 
 // Dispatch order of the tile kernels: (view, fine tile) by descending bit length of its coarse
 // bin's face count (a proxy for its work), so the heaviest tiles start first and the grid's
-// tail is short.  Run by one extra 256-thread workgroup of kd_bin_scatter per face set (it only
+// tail is short.  With a tile history (bb.hist: the fused forward's measured duration buckets of
+// the previous same-shape call, per (fine tile, part)), a coarse tile's key is instead the
+// largest bucket of its fine tiles' parts (quarter octaves of the duration) -- the soft-mask
+// work of a silhouette tile does not show in its bin counts.  Run by one extra 256-thread workgroup of kd_bin_scatter per face set (it only
 // needs the scan's totals, so it overlaps the scatter instead of taking a launch of its own):
 // one coarse tile (and its <= (ct/16)^2 fine tiles) per thread and pass, histograms and cursors
 // per wave.  Order within a bucket follows the (view, coarse tile) index; results never depend
 // on the order.  Each entry also carries the coarse bin's face count.
 __device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty) {
-  constexpr int kNB = 33, kWaves = kBlock / kWave, kPer = 8;
+  constexpr int kNB = 64, kWaves = kBlock / kWave, kPer = 8;  // buckets: one per lane
   __shared__ int s_cnt[kWaves][kNB];
   __shared__ int s_base, s_next;
   const int tid = threadIdx.x, w = tid >> 6;
@@ -368,6 +372,18 @@ __device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty) {
       tot[k] = v < n ? bb.totals[v] : 0;
       bk[k] = v < n ? 32 - __clz((unsigned)tot[k]) : -1;
       nf[k] = v < n ? fine_count(v) : 0;
+      if (bb.hist && v < n) {  // the history's bucket when there is one (max over fine tiles)
+        const int b = v / nct, c = v - b * nct;
+        const int cx = c % bb.g.nctx, cy = c / bb.g.nctx;
+        int h = 0;
+        for (int ty = cy * per; ty < min(cy * per + per, nty); ++ty)
+          for (int tx = cx * per; tx < min(cx * per + per, ntx); ++tx) {
+            const uint2 e = *reinterpret_cast<const uint2 *>(
+                bb.hist + 4 * ((int64_t)(b * nty + ty) * ntx + tx));  // 4 parts, 8 B aligned
+            h = max(h, (int)max(max(e.x & 0xffffu, e.x >> 16), max(e.y & 0xffffu, e.y >> 16)));
+          }
+        if (h > 0) bk[k] = min(h - 1, kNB - 1);
+      }
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
@@ -422,18 +438,17 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
     for (int j = 0; j < njobs; ++j) {
       const BinBuffers &b = jobs.bb[j];
       if (b.clear && b.n_clear > 0) {
-        const hipError_t e = hipMemsetAsync(b.clear, 0, sizeof(int) * b.n_clear, stream);
+        const hipError_t e = zero_words(b.clear, sizeof(int) * b.n_clear, stream);
         if (e != hipSuccess) return e;
       }
       if (b.clear_b && b.n_clear_b > 0) {
-        const hipError_t e = hipMemsetAsync(b.clear_b, 0, sizeof(int) * b.n_clear_b, stream);
+        const hipError_t e = zero_words(b.clear_b, sizeof(int) * b.n_clear_b, stream);
         if (e != hipSuccess) return e;
       }
-      hipError_t e = hipMemsetAsync(
-          b.totals, 0, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * b.g.nct(), stream);
+      hipError_t e =
+          zero_words(b.totals, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * b.g.nct(), stream);
       if (e != hipSuccess) return e;
-      e = hipMemsetAsync(b.base, 0, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * b.g.nct(),
-                         stream);
+      e = zero_words(b.base, sizeof(int) * (size_t)(fs.B > 0 ? fs.B : 0) * b.g.nct(), stream);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -548,6 +563,23 @@ int zero_buffers(T *p0, int64_t n0, T *p1, int64_t n1, hipStream_t stream) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "zero: %s", hipGetErrorString(e));
   return KD_OK;
+}
+
+// Zeroes `bytes` (a multiple of 4) at p with a kernel.  Used instead of hipMemsetAsync wherever a
+// call can be captured in a HIP graph: replays of captured memset nodes were measured to leave
+// stale data on this stack (tools/dbg_lists_graph.py: the second replay of the close-list soft
+// backward summed into an unzeroed gradient), while kernel nodes replay in stream order.
+hipError_t zero_words(void *p, size_t bytes, hipStream_t stream) {
+  if (!p || bytes == 0) return hipSuccess;
+  if (bytes % 4) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)(bytes / 4);
+  const unsigned blocks = (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 2048);
+  {
+    ProfScope prof(K_ZERO, stream);
+    hipLaunchKernelGGL(kd_zero2<float>, dim3(blocks), dim3(kBlock), 0, stream, (float *)p, n,
+                       (float *)nullptr, (int64_t)0);
+  }
+  return hipGetLastError();
 }
 
 template hipError_t bin_faces2<float>(const FaceSet<float> &, const BinBuffers &,

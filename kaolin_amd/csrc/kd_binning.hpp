@@ -53,6 +53,9 @@ struct BinBuffers {
   int n_clear_b;
   int2 *order;     // [B * fine tiles] (view * tiles + tile, its coarse bin's face count),
                    // heaviest first (tile_order in kd_bin_scatter): the tile kernels' dispatch order
+  unsigned short *hist;  // nullable: [B * fine tiles][4] per (tile, part) the previous same-shape
+                         // call's duration bucket + 1 (0: none), written by the fused forward and
+                         // ordering the tiles instead of the coarse counts (kd_set_tile_history)
   int nchunk;
   int chunk;       // faces per chunk (bin_chunk: 256 or 512)
   BinGeom g;
@@ -104,6 +107,8 @@ hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSe
                       const BinBuffers &bb1, hipStream_t stream,
                       const PrepOut<T> *prep = nullptr);
 
+// Zeroes `bytes` (a multiple of 4) at p with a kernel, not a memset node (graph-capture safe).
+hipError_t zero_words(void *p, size_t bytes, hipStream_t stream);
 // Zeroes n0 elements at p0 and n1 at p1 (either may be null / 0) in one launch.
 template <typename T>
 int zero_buffers(T *p0, int64_t n0, T *p1, int64_t n1, hipStream_t stream);

@@ -33,6 +33,40 @@ int device_cus() {
   }();
   return cus;
 }
+std::atomic<int> g_hist{1};
+namespace {
+struct HistSlot {
+  unsigned short *buf = nullptr;
+  long long tag = -1;
+};
+constexpr int kHistDevices = 64;
+HistSlot g_hist_slots[kHistDevices];
+std::mutex g_hist_mu;
+}  // namespace
+unsigned short *tile_history(int64_t n, long long tag, hipStream_t stream) {
+  if (!g_hist.load() || n <= 0 || n > kTileHistCap) return nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kHistDevices) return nullptr;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess) return nullptr;
+  const bool capturing = st != hipStreamCaptureStatusNone;
+  std::lock_guard<std::mutex> lk(g_hist_mu);
+  HistSlot &h = g_hist_slots[dev];
+  if (!h.buf) {
+    if (capturing) return nullptr;  // (no allocation inside a capture)
+    void *p = nullptr;
+    if (hipMalloc(&p, sizeof(unsigned short) * (size_t)kTileHistCap) != hipSuccess) return nullptr;
+    h.buf = (unsigned short *)p;
+    h.tag = -1;
+  }
+  if (h.tag != tag) {
+    if (capturing) return nullptr;  // (a memset node would clear it on every replay)
+    if (zero_words(h.buf, sizeof(unsigned short) * (size_t)n, stream) != hipSuccess)
+      return nullptr;
+    h.tag = tag;
+  }
+  return h.buf;
+}
 std::atomic<long long *> g_tbuf{nullptr};
 std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
 float pool_limit_bins() { return g_lim_bins.load(); }
@@ -120,6 +154,13 @@ int kd_set_coarse_tile(int px) {
   if (px != 0 && px != 16 && px != 32)
     return kd::set_error(KD_ERR_INVALID_ARGUMENT, "coarse tile must be 0, 16 or 32 (got %d)", px);
   kd::g_ct.store(px);
+  return KD_OK;
+}
+
+int kd_set_tile_history(int on) {
+  if (on != 0 && on != 1)
+    return kd::set_error(KD_ERR_INVALID_ARGUMENT, "tile history must be 0 or 1 (got %d)", on);
+  kd::g_hist.store(on);
   return KD_OK;
 }
 

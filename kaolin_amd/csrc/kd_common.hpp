@@ -52,6 +52,12 @@ int tile_split();
 int coarse_tile_hook();
 // compute units of the current device (cached on first use; 256 when unknown)
 int device_cus();
+// Tile cost history of the fused fp32 DIB-R forward (kd_set_tile_history): a library-owned
+// device buffer of kTileHistCap ushort entries per device, never freed (captured graphs keep
+// its address), zeroed on the stream when `tag` (the call's shape) changes outside a capture.
+// nullptr: history off, too many entries, or a new shape inside a stream capture.
+constexpr int64_t kTileHistCap = 1 << 20;
+unsigned short *tile_history(int64_t n, long long tag, hipStream_t stream);
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
 
 // Per-workgroup duration (wall clock, 100 MHz ticks) for diagnostics: written by thread 0 when

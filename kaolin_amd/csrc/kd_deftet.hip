@@ -391,7 +391,7 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
   w += align_up(sizeof(int) * cells * (size_t)(N > 0 ? N : 1));
   T *boxes = (T *)w;
   w += align_up(4 * sizeof(T) * (size_t)N);
-  hipError_t e = hipMemsetAsync(cursor, 0, 2 * sizeof(int) * (size_t)B * cells, stream);
+  hipError_t e = zero_words(cursor, 2 * sizeof(int) * (size_t)B * cells, stream);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "deftet: %s", hipGetErrorString(e));
   if (F > 0) {
     ProfScope prof(K_DT_BIN, stream);

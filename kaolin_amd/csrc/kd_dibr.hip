@@ -116,7 +116,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   if (B == 0 || H == 0 || W == 0) {
     const int rc = zero_buffers<T>(gz_fvi, nf * 6, gz_feat, gz_feat ? nf * 3 * D : 0, stream);
     if (rc != KD_OK || !iou.gt || B == 0) return rc;
-    if (hipMemsetAsync(iou.acc, 0, sizeof(double) * 2 * kIouParts * B, stream) != hipSuccess)
+    if (zero_words(iou.acc, sizeof(double) * 2 * kIouParts * B, stream) != hipSuccess)
       return set_error(KD_ERR_LAUNCH, "mask_iou: memset");
     return iou_finish_launch<T>(B, kIouParts, iou.acc, iou.stats, iou.loss, stream);
   }
@@ -136,6 +136,17 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   if (iou.gt) {  // the IoU accumulators start at zero (kd_bin_count)
     d.sbb.clear_b = (int *)iou.acc;
     d.sbb.n_clear_b = 4 * kIouParts * B;
+  }
+  // the one-launch fp32 forward's tile history (kd_set_tile_history): the previous same-shape
+  // call's tile durations order this call's tiles (tile_order) and this call records its own
+  if (std::is_same<T, float>::value && d.rbb.cull && soft && K <= kFuseSlots &&
+      !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT))) {
+    const int64_t nt = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    uint64_t tag = 1469598103934665603ull;  // FNV-1a over the shape and the hooks
+    for (const int64_t x : {(int64_t)B, (int64_t)H, (int64_t)W, F, (int64_t)K,
+                            (int64_t)tile_split(), (int64_t)coarse_tile_hook()})
+      tag = (tag ^ (uint64_t)x) * 1099511628211ull;
+    d.rbb.hist = tile_history(4 * (int64_t)B * nt, (long long)(tag >> 1), stream);
   }
   hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream, prep);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
@@ -272,7 +283,7 @@ static int dibr_bwd_vtx(int B, int H, int W, int64_t F, int D, const T *grad_int
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   if ((int64_t)Bv * V > 0) {
-    const hipError_t e = hipMemsetAsync(gvert, 0, sizeof(T) * 3 * (size_t)Bv * (size_t)V, stream);
+    const hipError_t e = zero_words(gvert, sizeof(T) * 3 * (size_t)Bv * (size_t)V, stream);
     if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
   }
   const int64_t nf = (int64_t)B * F;

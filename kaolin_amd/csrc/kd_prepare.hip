@@ -207,7 +207,7 @@ static int prep_bwd(int B, int Bv, int64_t V, int64_t F, const int64_t *faces, c
   const int64_t total = (int64_t)Bv * V;
   if (total == 0) return KD_OK;
   if (F == 0 || B == 0) {
-    hipError_t e0 = hipMemsetAsync(gvert, 0, sizeof(T) * total * 3, (hipStream_t)stream);
+    hipError_t e0 = zero_words(gvert, sizeof(T) * total * 3, (hipStream_t)stream);
     if (e0 != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e0));
     return KD_OK;
   }

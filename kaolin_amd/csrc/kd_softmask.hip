@@ -320,9 +320,9 @@ int soft_backward(int B, int H, int W, int64_t F, int K, const T *grad_soft, con
                   const uint8_t *ctype, const T *fvi, float sigmainv, float M, T *grad_fvi,
                   hipStream_t stream) {
   const int64_t nf = (int64_t)B * F;
-  if (nf > 0) {
-    hipError_t e = hipMemsetAsync(grad_fvi, 0, sizeof(T) * nf * 6, stream);
-    if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
+  if (nf > 0) {  // (a kernel, not a memset node: see zero_buffers)
+    const int rc = zero_buffers<T>(grad_fvi, nf * 6, (T *)nullptr, 0, stream);
+    if (rc != KD_OK) return rc;
   }
   const int64_t total = (int64_t)B * H * W;
   if (total > 0 && nf > 0 && K > 0) {
@@ -436,9 +436,9 @@ static int soft_bwd_binned(int B, int H, int W, int64_t F, int K, const T *gs, c
   KD_CHECK_ARG(std::isfinite((float)M), "multiplier must be finite");
   KD_CHECK_ARG((int64_t)B * F < (1ll << 31), "too many faces");
   const int64_t nf = (int64_t)B * F;
-  if (nf > 0) {
-    hipError_t e = hipMemsetAsync(gfvi, 0, sizeof(T) * nf * 6, (hipStream_t)stream);
-    if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "memset: %s", hipGetErrorString(e));
+  if (nf > 0) {  // (a kernel, not a memset node: see zero_buffers)
+    const int rc = zero_buffers<T>(gfvi, nf * 6, (T *)nullptr, 0, (hipStream_t)stream);
+    if (rc != KD_OK) return rc;
   }
   SoftArgs<T> a{};
   a.fs = fused_faceset<T>(B, H, W, F, fvi, M, boxlen);

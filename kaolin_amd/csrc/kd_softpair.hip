@@ -805,8 +805,14 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
                                                               SoftPairBuf<float> pb) {
   __shared__ DibrTileLDS<float> U;
   __shared__ uint64_t uncm[4];
+  __shared__ long long s_t0;  // tile history: the workgroup's start and finished waves
+  __shared__ int s_done;
   TileClock clk(DIAG ? a.fs.tbuf : nullptr, 1);
   if (DIAG) clk.start_to(2);
+  if (ra.bb.hist && threadIdx.x == 0) {  // (the walk's barriers order these before any read)
+    s_t0 = (long long)wall_clock64();
+    s_done = 0;
+  }
   int b, tl, nbin, part;
   tile_of_block_split<SPLIT>(ra.bb, ra.fs.H, ra.fs.W, b, tl, part, nbin, ra.fs.dbg);
   if (DIAG && a.fs.tbuf && threadIdx.x == 0) {
@@ -827,6 +833,16 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
   soft_pairs_tile<float, true, SPLIT, DIAG>(
       a, pb, b, tl, -1, U.s, part, uncm,
       DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr);
+  // tile history (kd_set_tile_history): the last wave to finish stores the workgroup's duration
+  // as a quarter-octave bucket (1..63; 0 = none) for the next same-shape call's dispatch order
+  if (ra.bb.hist && (threadIdx.x & (kWave - 1)) == 0 &&
+      atomicAdd(&s_done, 1) == kBlock / kWave - 1) {
+    const long long dt = (long long)wall_clock64() - s_t0;  // 100 MHz ticks
+    const unsigned t = (unsigned)min(max(dt, 1ll), 0x7fffffffll);
+    const int bl = 32 - __clz(t);
+    const int q = bl >= 3 ? 4 * bl + (int)((t >> (bl - 3)) & 3u) : bl;
+    ra.bb.hist[4 * ((int64_t)b * pb.ntiles + tl) + part] = (unsigned short)(min(max(q - 16, 0), 62) + 1);
+  }
 }
 
 // The fp64 DIB-R forward in one launch: the pair raster (fp64 test, fp64-culled candidates, the

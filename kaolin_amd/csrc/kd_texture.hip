@@ -823,7 +823,7 @@ static int tex_backward_tiled(int B, int64_t N, int C, int Ht, int Wt, const T *
   tt.list = tt.chunk_e + mc;
   if (grad_tex) {  // the gradient is added into zeros (all Bt textures)
     const int64_t nt = (int64_t)tt.ntex * C * Ht * Wt;
-    if (nt > 0 && hipMemsetAsync(grad_tex, 0, sizeof(T) * (size_t)nt, stream) != hipSuccess)
+    if (nt > 0 && zero_words(grad_tex, sizeof(T) * (size_t)nt, stream) != hipSuccess)
       return set_error(KD_ERR_LAUNCH, "texture_mapping: memset");
   }
   if (B == 0 || N == 0 || C == 0 || (!grad_tex && !grad_coords)) return KD_OK;
@@ -831,7 +831,7 @@ static int tex_backward_tiled(int B, int64_t N, int C, int Ht, int Wt, const T *
   const dim3 grid((unsigned)((N + kTexSpan - 1) / kTexSpan), (unsigned)B);
   const unsigned gacc = (unsigned)std::min<int64_t>(mc, kTexAccGrid);
   ProfScope prof(K_TEX_BWD, stream);
-  if (grad_tex && hipMemsetAsync(tt.count, 0, sizeof(int) * (size_t)(ntiles + 1), stream) !=
+  if (grad_tex && zero_words(tt.count, sizeof(int) * (size_t)(ntiles + 1), stream) !=
                       hipSuccess)
     return set_error(KD_ERR_LAUNCH, "texture_mapping: memset");
 #define KD_TEX_LAUNCH(M)                                                                   \

@@ -80,3 +80,13 @@ def test_production_library_reads_no_debug_flags():
     assert lib.kd_set_test_forms(8) != _lib.KD_OK
     _lib.set_test_forms(_lib.FORM_SPLIT_FWD | _lib.FORM_SPLIT_BWD | _lib.FORM_SOFT_SPLIT)
     _lib.set_test_forms(0)
+
+
+def test_tuning_hooks_reject_bad_values():
+    """host-only setters: no GPU needed"""
+    from kaolin_amd import _lib
+    for fn, bad in ((_lib.load().kd_set_tile_history, 2), (_lib.load().kd_set_tile_split, 3),
+                    (_lib.load().kd_set_coarse_tile, 8)):
+        assert fn(bad) != 0
+    _lib.set_tile_history(False)
+    _lib.set_tile_history(True)

@@ -1,0 +1,69 @@
+"""GPU: the tile cost history of the fused fp32 DIB-R forward (kd_set_tile_history).
+
+Each call of the one-launch forward records its tiles' durations in a library-owned buffer, and
+the next call of the same shape dispatches its tiles heaviest-first by them (tile_order) instead
+of by the coarse bins' face counts.  Only the dispatch order changes, so the outputs must be
+bit-identical to a call without history -- also when the history comes from another mesh of the
+same shape (stale costs), with split tiles, and on images whose sides are not multiples of 16 --
+and the gradients stay at the float atomics' bar.
+"""
+import pytest
+import torch
+
+from test_gpu_breadth import _check_view, _fwd_bwd
+from test_gpu_split import _same
+
+pytestmark = pytest.mark.gpu
+
+DEV = 'cuda'
+
+
+@pytest.fixture(autouse=True)
+def _restore():
+    yield
+    from kaolin_amd import _lib
+    _lib.set_tile_history(True)
+    _lib.set_tile_split(0)
+
+
+def _run(h, w, v, history):
+    from kaolin_amd import _lib
+    _lib.set_tile_history(history)
+    try:
+        return _fwd_bwd(h, w, v)
+    finally:
+        _lib.set_tile_history(True)
+
+
+@pytest.mark.parametrize('views', [1, 8])
+def test_history_matches_bin_count_order_c3(views):
+    from kaolin_amd import workloads
+    h = w = 512
+    v = workloads.sphere_views(250, 101, h, w, views, DEV)
+    ref = _run(h, w, v, False)
+    _run(h, w, v, True)            # records the durations
+    again = _run(h, w, v, True)    # dispatched by them
+    _same(again, ref)
+
+
+def test_stale_history_from_another_mesh():
+    """same shape, other geometry: the recorded order is wrong for it, the results are not"""
+    from kaolin_amd import workloads
+    h = w = 512
+    a = workloads.sphere_views(250, 101, h, w, 2, DEV)
+    b = workloads.sphere_views(250, 101, h, w, 2, DEV, first_view=5, total_views=8)
+    _run(h, w, a, True)
+    stale = _run(h, w, b, True)
+    _same(stale, _run(h, w, b, False))
+
+
+@pytest.mark.parametrize('split', [1, 2])
+@pytest.mark.parametrize('hw', [(136, 200), (9, 300)])
+def test_history_ragged_vs_oracle(split, hw):
+    from kaolin_amd import _lib, workloads
+    h, w = hw
+    v = workloads.sphere_views(120, 50, h, w, 1, DEV)
+    _lib.set_tile_split(split)
+    _run(h, w, v, True)
+    out = _run(h, w, v, True)
+    _check_view(h, w, 0, out)

@@ -12,8 +12,11 @@ rows = list(csv.DictReader(open(f)))
 ev = sorted(((int(r['Start_Timestamp']), int(r['End_Timestamp']),
               r['Kernel_Name'].split('(')[0].replace('void ', '')) for r in rows))
 kd = [e for e in ev if 'kd::' in e[2]]
-# the step starts at kd_prepare_fwd
-starts = [i for i, e in enumerate(kd) if 'prepare_fwd' in e[2]]
+# the step starts at kd_prepare_fwd, or at kd_bin_count when the projection is inside the
+# binning launch (the from-vertices node)
+n_prep = sum('prepare_fwd' in e[2] for e in kd)
+first = 'prepare_fwd' if n_prep >= sum('bin_count' in e[2] for e in kd) else 'bin_count'
+starts = [i for i, e in enumerate(kd) if first in e[2]]
 steps = [kd[a:b] for a, b in zip(starts, starts[1:])]
 # the graph replays (back-to-back launches) are the steps with the shortest span; the eager
 # profiling pass that follows them in bench.py has host-side gaps
