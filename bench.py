@@ -328,6 +328,9 @@ def main():
                     help='coarse bin edge of the DIB-R binning (kd_set_coarse_tile; 0: auto)')
     ap.add_argument('--tile-split', type=int, default=0, choices=[0, 1, 2, 4],
                     help='workgroups per tile of the fused forward (kd_set_tile_split; 0: auto)')
+    ap.add_argument('--tile-history', type=int, default=1, choices=[0, 1],
+                    help='dispatch the fused forward by the previous same-shape call\'s tile '
+                         'durations (kd_set_tile_history; default on)')
     ap.add_argument('--pmc', default=None,
                     help='PMC traffic summary (default profiles/r04, r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
@@ -343,6 +346,7 @@ def main():
     _lib.load()
     _lib.set_tile_split(args.tile_split)
     _lib.set_coarse_tile(args.coarse_tile)
+    _lib.set_tile_history(bool(args.tile_history))
     soup = args.config in SOUP_CONFIGS
     B_global = SOUP_CONFIGS[args.config][3] if soup else CONFIGS[args.config][4]
     weak_main = args.views_per_gpu is not None
@@ -504,6 +508,7 @@ def main():
                                        args.vertex_path],
                    'tile_split': args.tile_split or 'auto',
                    'coarse_tile': args.coarse_tile or 'auto',
+                   'tile_history': bool(args.tile_history),
                    'close_lists': 'materialised' if args.lists else 'not materialised',
                    'soft_mask_grad': (f'mask_iou(soft, gt) ({args.iou})' if args.iou
                                       else 'fixed seeded grad_soft'),

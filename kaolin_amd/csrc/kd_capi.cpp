@@ -47,24 +47,22 @@ unsigned short *tile_history(int64_t n, long long tag, hipStream_t stream) {
   if (!g_hist.load() || n <= 0 || n > kTileHistCap) return nullptr;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kHistDevices) return nullptr;
-  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(stream, &st) != hipSuccess) return nullptr;
-  const bool capturing = st != hipStreamCaptureStatusNone;
   std::lock_guard<std::mutex> lk(g_hist_mu);
   HistSlot &h = g_hist_slots[dev];
+  if (h.buf && h.tag == tag) return h.buf;  // the common case: no runtime query at all
+  // a first allocation or a new shape: only outside a stream capture (no allocation inside one,
+  // and a captured zero fill would clear the history on every replay)
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
+    return nullptr;
   if (!h.buf) {
-    if (capturing) return nullptr;  // (no allocation inside a capture)
     void *p = nullptr;
     if (hipMalloc(&p, sizeof(unsigned short) * (size_t)kTileHistCap) != hipSuccess) return nullptr;
     h.buf = (unsigned short *)p;
     h.tag = -1;
   }
-  if (h.tag != tag) {
-    if (capturing) return nullptr;  // (a memset node would clear it on every replay)
-    if (zero_words(h.buf, sizeof(unsigned short) * (size_t)n, stream) != hipSuccess)
-      return nullptr;
-    h.tag = tag;
-  }
+  if (zero_words(h.buf, sizeof(unsigned short) * (size_t)n, stream) != hipSuccess) return nullptr;
+  h.tag = tag;
   return h.buf;
 }
 std::atomic<long long *> g_tbuf{nullptr};

@@ -1434,7 +1434,8 @@ int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
 // Workgroups per tile of the fused fp32 forward (kd_dibr_fwd_tiles SPLIT): the tile split hook
 // (kd_set_tile_split) when set, else by the batch's tile count against the chip's workgroup
 // slots.  Split tiles need the fixed record pool (every part owns its pixels' K records).
-int fwd_tile_split(int64_t tiles, bool fixed_pool) {
+// history: the dispatch follows the tile history (kd_set_tile_history).
+int fwd_tile_split(int64_t tiles, bool fixed_pool, bool history) {
   if (!fixed_pool) return 1;
   const int forced = tile_split();
   if (forced > 0) return forced;
@@ -1443,12 +1444,15 @@ int fwd_tile_split(int64_t tiles, bool fixed_pool) {
   // 0.1170 ms per step at 1 / 2 / 4 workgroups per tile; 2 views (2048) 0.1388 / 0.1463 / 0.1624;
   // 8 views 0.310 / 0.352.  A part repeats the tile's raster walk (~10 us of dependent loads at
   // one wave per SIMD), so splitting pays only while the whole tiles fit one round of slots.
-  const int64_t slots = (int64_t)cus * 6;  // kd_dibr_fwd_tiles: 6 workgroups per CU
+  // With the tile history the silhouette parts no longer wait for a second round, and 2 views
+  // split pay too (profiles/r04/ab_split_history.txt: 1 view 0.1142 / 0.0992 / 0.1012 (4), 2
+  // views 0.1298 / 0.1221, 4 views 0.1667 / 0.1903, 8 views 0.2692 / 0.3289 ms).
+  const int64_t slots = (int64_t)cus * (history ? 8 : 6);  // (6 workgroups per CU)
   return tiles <= slots ? 2 : 1;
 }
 
-int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B) {
-  return fwd_tile_split((int64_t)B * pb.ntiles, pb.fixed && !pool_may_overflow(K));
+int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B, bool history) {
+  return fwd_tile_split((int64_t)B * pb.ntiles, pb.fixed && !pool_may_overflow(K), history);
 }
 
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) {
@@ -1463,7 +1467,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
-    const int split = dibr_fwd_split(pb, a.K, ra.fs.B);
+    const int split = dibr_fwd_split(pb, a.K, ra.fs.B, ra.bb.hist != nullptr);
     const dim3 grid((unsigned)pb.ntiles * split, ra.fs.B);
     const bool diag = KD_DIAG && a.fs.tbuf;
 #define KD_FWD_TILES(S)                                                                         \
