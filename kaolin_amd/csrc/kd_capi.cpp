@@ -57,7 +57,10 @@ unsigned short *tile_history(int64_t n, long long tag, hipStream_t stream) {
     return nullptr;
   if (!h.buf) {
     void *p = nullptr;
-    if (hipMalloc(&p, sizeof(unsigned short) * (size_t)kTileHistCap) != hipSuccess) return nullptr;
+    if (hipMalloc(&p, sizeof(unsigned short) * (size_t)kTileHistCap) != hipSuccess) {
+      (void)hipGetLastError();  // (no history: the caller's own launch checks stay clean)
+      return nullptr;
+    }
     h.buf = (unsigned short *)p;
     h.tag = -1;
   }
