@@ -160,6 +160,11 @@ class Workload:
             disc = (((yy - H / 2) ** 2 + (xx - W / 2) ** 2) < (0.4 * min(H, W)) ** 2).to(dt)
             self.gt = disc.expand(n, H, W).contiguous().to(dev)
         self.params = [self.fvi, self.feats] if self.soup else [self.vertices, self.feats]
+        # --perturb LR: the step ends with a signSGD update of the vertices by their own gradient
+        # (the magnitude of an Adam step, ian_dibr.py:172-173, 288-290), captured in the graph, so
+        # every replay renders moved geometry and the tile history always describes the previous
+        # step's mesh, as in a training loop
+        self.perturb = 0.0 if self.soup else float(args.perturb or 0.0)
 
     def forward_backward(self):
         """The GPU part of the step (no collective)."""
@@ -168,10 +173,14 @@ class Workload:
                                                         self.feats, self.nz, **self.kw)
             torch.autograd.backward([interp, soft], [self.g_feat, self.g_soft])
             return face_idx
-        return distributed.dibr_forward_backward(
+        face_idx = distributed.dibr_forward_backward(
             self.vertices, self.faces, self.proj, self.cam, self.feats, self.H, self.W,
             self.g_feat, self.g_soft, gt_mask=self.gt, iou=self.iou or 'fused',
             fused_vertices=self.vertex_path != 'compose', **self.kw)
+        if self.perturb:
+            with torch.no_grad():
+                self.vertices.sub_(self.perturb * self.vertices.grad.sign())
+        return face_idx
 
     def clear(self):
         for p in self.params:
@@ -331,6 +340,10 @@ def main():
     ap.add_argument('--tile-history', type=int, default=1, choices=[0, 1],
                     help='dispatch the fused forward by the previous same-shape call\'s tile '
                          'durations (kd_set_tile_history; default on)')
+    ap.add_argument('--perturb', type=float, default=0.0, metavar='LR',
+                    help='move the mesh every step: a signSGD step of size LR on the vertices '
+                         'with the step\'s own gradient, inside the timed step (1 GPU; tile '
+                         'history A/B under motion)')
     ap.add_argument('--pmc', default=None,
                     help='PMC traffic summary (default profiles/r04, r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
@@ -339,6 +352,8 @@ def main():
     # RCCL refuses two ranks on one device).  The default is RCCL ("nccl").
     backend = os.environ.get('KD_BENCH_BACKEND', 'nccl')
     rank, world, local = distributed.init_from_env(backend)
+    if args.perturb and world > 1:
+        raise SystemExit('--perturb: one GPU only (the update would use un-reduced gradients)')
     if world != args.gpus and rank == 0:
         print(f'[bench] note: --gpus {args.gpus} but WORLD_SIZE {world}', file=sys.stderr)
     dev = torch.device('cuda', local % max(torch.cuda.device_count(), 1))
@@ -359,6 +374,9 @@ def main():
     use_graph = not args.no_graph and not args.lists and backend == 'nccl'
     with dibr.close_lists(args.lists):
         wl = Workload(args, dev, first, n, total)
+        covered0 = None
+        if wl.perturb:  # the workload's coverage before the mesh moves
+            covered0 = int((wl.eager_step() >= 0).sum().item())
         step, launch = make_step(wl, use_graph)
         elapsed, evt = timed(step, args.steps, args.warmup, dev, world)
     ms_per_step = elapsed * 1e3 / args.steps
@@ -509,6 +527,10 @@ def main():
                    'tile_split': args.tile_split or 'auto',
                    'coarse_tile': args.coarse_tile or 'auto',
                    'tile_history': bool(args.tile_history),
+                   'perturb': None if not wl.perturb else {
+                       'lr': wl.perturb, 'update': 'vertices -= lr * sign(vertices.grad) inside '
+                                                   'every timed step (graph)',
+                       'covered_px_first_step': covered0},
                    'close_lists': 'materialised' if args.lists else 'not materialised',
                    'soft_mask_grad': (f'mask_iou(soft, gt) ({args.iou})' if args.iou
                                       else 'fixed seeded grad_soft'),

@@ -217,6 +217,13 @@ def set_tile_history(on=True):
         raise RuntimeError(load().kd_last_error().decode(errors='replace'))
 
 
+def debug_set(flags):
+    """Diagnostic ablation flags (kd_debug_set): the diagnostic library only (KAOLIN_AMD_DIAG=1,
+    tools/); the production library refuses nonzero flags, and that refusal is raised here."""
+    if load().kd_debug_set(int(flags)) != KD_OK:
+        raise RuntimeError(load().kd_last_error().decode(errors='replace'))
+
+
 def pool_limits_active():
     """True while set_pool_limits holds a pool below its full size (the test hook)."""
     return _pool_limited

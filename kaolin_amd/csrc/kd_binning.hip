@@ -459,7 +459,8 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
   // both sets in one workgroup when they share the corners (dibr_rasterization's raster and soft
   // boxes), the corners loaded once: measured slower at C3 (24.6 vs 19.8 us at 8 views, 11.7 vs
   // 7.2 at 1: twice the work per wave at 93 VGPRs), so only on request (debug flag 1 << 21)
-  const bool shared = (debug_flags() & (1 << 21)) && njobs == 2 &&
+  // (not with PREP: that count variant writes prepare_vertices' outputs, this one does not)
+  const bool shared = (debug_flags() & (1 << 21)) && njobs == 2 && !jobs.prep.a.vertices &&
                       jobs.fs[0].fvi == jobs.fs[1].fvi &&
                       jobs.fs[0].scale == jobs.fs[1].scale && jobs.fs[0].F == jobs.fs[1].F &&
                       jobs.fs[0].first_idx == jobs.fs[1].first_idx;

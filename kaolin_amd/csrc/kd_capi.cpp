@@ -23,15 +23,29 @@ std::atomic<int> g_split{0};
 int tile_split() { return g_split.load(); }
 std::atomic<int> g_ct{0};
 int coarse_tile_hook() { return g_ct.load(); }
-int device_cus() {
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      n = 256;
-    return n > 0 ? n : 256;
-  }();
-  return cus;
+// The device a stream belongs to (the null stream: the calling thread's current device).  The C
+// ABI launches on the caller's stream whatever device is current, so per-device state (the tile
+// history, the CU count) is keyed by the stream's device, never by hipGetDevice alone.
+int stream_device(hipStream_t stream) {
+  hipDevice_t d = -1;
+  if (stream && hipStreamGetDevice(stream, &d) == hipSuccess && d >= 0) return (int)d;
+  int cur = 0;
+  if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+  return cur;
+}
+namespace {
+constexpr int kMaxDevices = 64;
+std::atomic<int> g_cus[kMaxDevices];  // 0: not queried yet
+}  // namespace
+int device_cus(hipStream_t stream) {
+  const int dev = stream_device(stream);
+  if (dev < 0 || dev >= kMaxDevices) return 256;
+  int n = g_cus[dev].load(std::memory_order_relaxed);
+  if (n > 0) return n;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    n = 256;
+  g_cus[dev].store(n, std::memory_order_relaxed);
+  return n;
 }
 std::atomic<int> g_hist{1};
 namespace {
@@ -39,25 +53,35 @@ struct HistSlot {
   unsigned short *buf = nullptr;
   long long tag = -1;
 };
-constexpr int kHistDevices = 64;
-HistSlot g_hist_slots[kHistDevices];
+HistSlot g_hist_slots[kMaxDevices];
 std::mutex g_hist_mu;
 }  // namespace
+// One buffer per device for the whole process: streams, threads and captured graphs of that
+// device share it.  Sharing can only degrade the dispatch order (tile_order reads
+// each entry once, so any history gives a permutation of the tiles), never a result.
 unsigned short *tile_history(int64_t n, long long tag, hipStream_t stream) {
   if (!g_hist.load() || n <= 0 || n > kTileHistCap) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kHistDevices) return nullptr;
+  const int dev = stream_device(stream);  // the device the launches will run on
+  if (dev < 0 || dev >= kMaxDevices) return nullptr;
   std::lock_guard<std::mutex> lk(g_hist_mu);
   HistSlot &h = g_hist_slots[dev];
-  if (h.buf && h.tag == tag) return h.buf;  // the common case: no runtime query at all
+  if (h.buf && h.tag == tag) return h.buf;  // the common case: no allocation, no capture query
   // a first allocation or a new shape: only outside a stream capture (no allocation inside one,
   // and a captured zero fill would clear the history on every replay)
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
     return nullptr;
   if (!h.buf) {
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
     void *p = nullptr;
-    if (hipMalloc(&p, sizeof(unsigned short) * (size_t)kTileHistCap) != hipSuccess) {
+    // allocated on the stream's device (a device guard around hipMalloc), whatever is current
+    const bool switched = cur != dev && hipSetDevice(dev) == hipSuccess;
+    const hipError_t ea = (cur == dev || switched)
+                              ? hipMalloc(&p, sizeof(unsigned short) * (size_t)kTileHistCap)
+                              : hipErrorInvalidDevice;
+    if (switched) (void)hipSetDevice(cur);
+    if (ea != hipSuccess) {
       (void)hipGetLastError();  // (no history: the caller's own launch checks stay clean)
       return nullptr;
     }

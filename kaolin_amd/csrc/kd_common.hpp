@@ -50,8 +50,10 @@ int test_forms();
 int tile_split();
 // kd_set_coarse_tile: dibr_rasterization's coarse bin edge (0: chosen by the batch size)
 int coarse_tile_hook();
-// compute units of the current device (cached on first use; 256 when unknown)
-int device_cus();
+// the device `stream` belongs to (null stream: the current device)
+int stream_device(hipStream_t stream);
+// compute units of the stream's device (cached per device on first use; 256 when unknown)
+int device_cus(hipStream_t stream);
 // Tile cost history of the fused fp32 DIB-R forward (kd_set_tile_history): a library-owned
 // device buffer of kTileHistCap ushort entries per device, never freed (captured graphs keep
 // its address), zeroed on the stream when `tag` (the call's shape) changes outside a capture.

@@ -137,19 +137,6 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
     d.sbb.clear_b = (int *)iou.acc;
     d.sbb.n_clear_b = 4 * kIouParts * B;
   }
-  // the one-launch fp32 forward's tile history (kd_set_tile_history): the previous same-shape
-  // call's tile durations order this call's tiles (tile_order) and this call records its own
-  if (std::is_same<T, float>::value && d.rbb.cull && soft && K <= kFuseSlots &&
-      !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT))) {
-    const int64_t nt = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-    uint64_t tag = 1469598103934665603ull;  // FNV-1a over the shape and the hooks
-    for (const int64_t x : {(int64_t)B, (int64_t)H, (int64_t)W, F, (int64_t)K,
-                            (int64_t)tile_split(), (int64_t)coarse_tile_hook()})
-      tag = (tag ^ (uint64_t)x) * 1099511628211ull;
-    d.rbb.hist = tile_history(4 * (int64_t)B * nt, (long long)(tag >> 1), stream);
-  }
-  hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream, prep);
-  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   RasterFwdArgs<T> ra{rfs, d.rbb, fvz, fvz_fs, fvz_cs, feat, D, eps, interp, face_idx, weights};
   SoftArgs<T> sa{};
   sa.fs = sfs;
@@ -167,9 +154,24 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   sa.iou_gt = iou.gt;
   sa.iou_acc = iou.acc;
   sa.iou_B = B;
+  const bool fusable = dibr_fwd_fusable(ra, sa);  // (fp32 and fp64)
+  // the one-launch fp32 forward's tile history (kd_set_tile_history): the previous same-shape
+  // call's tile durations order this call's tiles (tile_order) and this call records its own --
+  // only on the launch that writes it (the fused forward), so no other form reads a history
+  if (std::is_same<T, float>::value && fusable) {
+    const int64_t nt = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
+    uint64_t tag = 1469598103934665603ull;  // FNV-1a over the shape and the hooks
+    for (const int64_t x : {(int64_t)B, (int64_t)H, (int64_t)W, F, (int64_t)K,
+                            (int64_t)tile_split(), (int64_t)coarse_tile_hook()})
+      tag = (tag ^ (uint64_t)x) * 1099511628211ull;
+    d.rbb.hist = tile_history(4 * (int64_t)B * nt, (long long)(tag >> 1), stream);
+    ra.bb.hist = d.rbb.hist;
+  }
+  hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream, prep);
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   int rc = KD_OK;
   bool done = false;
-  if (dibr_fwd_fusable(ra, sa)) {  // (fp32 and fp64)
+  if (fusable) {
     rc = dibr_fwd_fused_launch(ra, sa, d.pb, stream);
     done = true;
   }

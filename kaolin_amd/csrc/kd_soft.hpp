@@ -259,7 +259,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a, SoftPa
                           hipStream_t stream);
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a);
 // workgroups per tile (1, 2, 4) the fused fp32 forward will use for B views
-int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B, bool history);
+int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B, bool history, hipStream_t stream);
 int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPairBuf<float> &pb,
                           hipStream_t stream);
 // The soft-mask backward and the raster backward (kd_raster_bwd.hpp, D <= 3) in one launch.

@@ -1435,11 +1435,11 @@ int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
 // (kd_set_tile_split) when set, else by the batch's tile count against the chip's workgroup
 // slots.  Split tiles need the fixed record pool (every part owns its pixels' K records).
 // history: the dispatch follows the tile history (kd_set_tile_history).
-int fwd_tile_split(int64_t tiles, bool fixed_pool, bool history) {
+int fwd_tile_split(int64_t tiles, bool fixed_pool, bool history, hipStream_t stream) {
   if (!fixed_pool) return 1;
   const int forced = tile_split();
   if (forced > 0) return forced;
-  const int cus = device_cus();
+  const int cus = device_cus(stream);
   // measured at C3 (bench.py --tile-split, same box): 1 view (1024 tiles) 0.1177 / 0.1076 /
   // 0.1170 ms per step at 1 / 2 / 4 workgroups per tile; 2 views (2048) 0.1388 / 0.1463 / 0.1624;
   // 8 views 0.310 / 0.352.  A part repeats the tile's raster walk (~10 us of dependent loads at
@@ -1451,8 +1451,9 @@ int fwd_tile_split(int64_t tiles, bool fixed_pool, bool history) {
   return tiles <= slots ? 2 : 1;
 }
 
-int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B, bool history) {
-  return fwd_tile_split((int64_t)B * pb.ntiles, pb.fixed && !pool_may_overflow(K), history);
+int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B, bool history, hipStream_t stream) {
+  return fwd_tile_split((int64_t)B * pb.ntiles, pb.fixed && !pool_may_overflow(K), history,
+                        stream);
 }
 
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) {
@@ -1467,7 +1468,7 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
-    const int split = dibr_fwd_split(pb, a.K, ra.fs.B, ra.bb.hist != nullptr);
+    const int split = dibr_fwd_split(pb, a.K, ra.fs.B, ra.bb.hist != nullptr, stream);
     const dim3 grid((unsigned)pb.ntiles * split, ra.fs.B);
     const bool diag = KD_DIAG && a.fs.tbuf;
 #define KD_FWD_TILES(S)                                                                         \

@@ -67,3 +67,33 @@ def test_history_ragged_vs_oracle(split, hw):
     _run(h, w, v, True)
     out = _run(h, w, v, True)
     _check_view(h, w, 0, out)
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason='needs two visible GPUs')
+def test_history_on_a_device_other_than_the_current_one():
+    """the forward's tensors (and stream) on cuda:1 while cuda:0 is current: the tile history
+    and the CU count belong to the stream's device, so the outputs equal those of
+    the same call made with cuda:1 current and no history"""
+    from kaolin_amd import _lib, workloads
+    from kaolin_amd.render.mesh import dibr_rasterization
+    h = w = 256
+    v = workloads.sphere_views(100, 51, h, w, 2, 'cuda:1')
+
+    def run(current, history):
+        _lib.set_tile_history(history)
+        with torch.cuda.device(current):
+            fvi = v['fvi'].detach().clone().requires_grad_(True)
+            interp, soft, face_idx = dibr_rasterization(h, w, v['fvz'], fvi, v['feats'],
+                                                        v['normals_z'])
+            torch.autograd.backward([interp, soft], [torch.ones_like(interp),
+                                                     torch.ones_like(soft)])
+            torch.cuda.synchronize('cuda:1')
+        return face_idx, interp, soft, fvi.grad
+
+    run(0, True)
+    other = run(0, True)   # dispatched by a history that must live on cuda:1
+    ref = run(1, False)
+    for x, y in zip(other[:3], ref[:3]):
+        assert torch.equal(x, y)
+    torch.testing.assert_close(other[3], ref[3], rtol=1e-4, atol=1e-5 * ref[3].abs().max().item())

@@ -9,7 +9,7 @@ root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 a, b = int(sys.argv[1]), int(sys.argv[2])
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 3
 code = ("import sys, runpy; sys.argv=['bench.py','--no-cpu-baseline','--steps','40']; "
-        "from kaolin_amd import _lib; _lib.load().kd_debug_set(%d); "
+        "from kaolin_amd import _lib; _lib.debug_set(%d); "
         "runpy.run_path('bench.py', run_name='__main__')")
 res = {a: [], b: []}
 kern = {a: {}, b: {}}

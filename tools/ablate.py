@@ -27,7 +27,7 @@ def run():
 
 
 for flags in [int(x) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "4", "8", "0"])]:
-    _lib.load().kd_debug_set(flags)
+    _lib.debug_set(flags)
     for _ in range(3):
         run()
     torch.cuda.synchronize()
@@ -39,4 +39,4 @@ for flags in [int(x) for x in (sys.argv[2].split(",") if len(sys.argv) > 2 else 
     prof = _lib.profile_collect()
     print(f'flags={flags}: ' + '  '.join(f'{k.replace("kd_", "")}={ms * 1e3 / n:7.1f}us'
                                          for k, (ms, n) in sorted(prof.items())))
-_lib.load().kd_debug_set(0)
+_lib.debug_set(0)

@@ -42,10 +42,10 @@ def main():
     for _ in range(3):
         deftet_sparse_render(px, rr, fvz, fvi, uvs, 30)
     lib.kd_debug_buffer(buf.data_ptr())
-    lib.kd_debug_set(64 | (2048 if KERNEL == "pool" else 1024))
+    _lib.debug_set(64 | (2048 if KERNEL == "pool" else 1024))
     deftet_sparse_render(px, rr, fvz, fvi, uvs, 30)
     torch.cuda.synchronize()
-    lib.kd_debug_set(0)
+    _lib.debug_set(0)
     lib.kd_debug_buffer(None)
     b = buf.reshape(5, nwg).double() / 100.  # 100 MHz ticks -> us
     dur, start, t_walk, t_rank, t_store = b

@@ -32,10 +32,10 @@ lib.kd_debug_buffer(buf.data_ptr())
 for _ in range(3):
     dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
-lib.kd_debug_set(64 | extra)
+_lib.debug_set(64 | extra)
 dibr_rasterization(H, W, fvz, fvi, feats, nz)
 torch.cuda.synchronize()
-lib.kd_debug_set(0)
+_lib.debug_set(0)
 lib.kd_debug_buffer(None)
 t = buf.view(24, n).cpu().numpy()
 dur = t[1] / 100.0          # us (100 MHz wall clock)

@@ -33,10 +33,10 @@ extra = int(sys.argv[2]) if len(sys.argv) > 2 else 0
 for _ in range(3):
     run()
 torch.cuda.synchronize()
-lib.kd_debug_set(64 | extra)
+_lib.debug_set(64 | extra)
 run()
 torch.cuda.synchronize()
-lib.kd_debug_set(0)
+_lib.debug_set(0)
 lib.kd_debug_buffer(None)
 t = buf.view(3, B, nty, ntx).cpu().numpy() / 100.0  # microseconds
 for k, name in enumerate(['raster_fwd_pairs', 'soft_pairs', 'soft_bwd_pairs']):
