@@ -164,7 +164,7 @@ class Workload:
         # (the magnitude of an Adam step, ian_dibr.py:172-173, 288-290), captured in the graph, so
         # every replay renders moved geometry and the tile history always describes the previous
         # step's mesh, as in a training loop
-        self.perturb = 0.0 if self.soup else float(args.perturb or 0.0)
+        self.perturb = 0.0 if self.soup else float(getattr(args, 'perturb', 0.0) or 0.0)
 
     def forward_backward(self):
         """The GPU part of the step (no collective)."""
