@@ -28,7 +28,6 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view,
   s += align_up(sizeof(int) * (size_t)kBinEntriesPerFace * (size_t)(N > 0 ? N : 1));
   s += align_up(sizeof(float4) * 2 * (size_t)N);
   s += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
-  s += align_up(sizeof(int4) * 2 * (size_t)B * fine_tiles(H, W));
   return s;
 }
 
@@ -55,9 +54,6 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   off += align_up(sizeof(float4) * 2 * (size_t)N);
   bb.order = (int2 *)(base + off);
   off += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
-  bb.hdr_store = (int4 *)(base + off);
-  bb.hdr = nullptr;
-  off += align_up(sizeof(int4) * 2 * (size_t)B * fine_tiles(H, W));
   bb.cull_eps = 0.f;
   bb.hist = nullptr;
   bb.clear = nullptr;
@@ -249,20 +245,13 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
   if (live && lane == 0) bb.totals[(int64_t)b * nct + c] = total;
 }
 
-template <typename T>
-__device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty, const FaceSet<T> &fs,
-                           const BinBuffers &ob, const FaceSet<T> &ofs);
-
 template <typename T, int PER>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   const FaceSet<T> &fs = jobs.fs[blockIdx.z];
   const BinBuffers &bb = jobs.bb[blockIdx.z];
   if (blockIdx.x == gridDim.x - 1) {  // the extra column: the set's tile dispatch order
-    // (with dispatch headers: the other set's bins too; kd_dibr.hip's pair of sets)
     if (blockIdx.y == 0)
-      tile_order<T>(bb, fs.B, (fs.W + kTile - 1) / kTile, (fs.H + kTile - 1) / kTile, fs,
-                    jobs.bb[gridDim.z > 1 ? 1 - blockIdx.z : blockIdx.z],
-                    jobs.fs[gridDim.z > 1 ? 1 - blockIdx.z : blockIdx.z]);
+      tile_order(bb, fs.B, (fs.W + kTile - 1) / kTile, (fs.H + kTile - 1) / kTile);
     return;
   }
   // chunk-bit membership mask per coarse tile: bit t set <=> face (chunk * chunk size + t) touches
@@ -303,7 +292,7 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
     }
     int all;
     int run = wg_exclusive_scan(sum, s_scan, all);
-    const int64_t room = bin_room(bb, lo, hi);
+    const int64_t room = (int64_t)((double)bb.limit * (double)bb.xper * (double)(hi - lo));
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int c = tid * kPer + k;
@@ -360,55 +349,12 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
 // one coarse tile (and its <= (ct/16)^2 fine tiles) per thread and pass, histograms and cursors
 // per wave.  Order within a bucket follows the (view, coarse tile) index; results never depend
 // on the order.  Each entry also carries the coarse bin's face count.
-// Bases of view b's bins (bb.base[b][*]): the exclusive scan of its coarse totals over the tiles
-// with the room check -- the values kd_bin_scatter's chunk-0 workgroups store (integer sums: the
-// same numbers whoever computes them).  One wave; lane l holds the contiguous run of tiles
-// [l * per, l * per + per), per <= 16 (nct <= 1024).
-template <typename T>
-__device__ __forceinline__ void wave_view_bases(const BinBuffers &bb, const FaceSet<T> &fs, int b) {
-  const int lane = threadIdx.x & (kWave - 1);
-  const int nct = bb.g.nct(), per = (nct + kWave - 1) / kWave;
-  const int *tot = bb.totals + (int64_t)b * nct;
-  int64_t lo, hi;
-  view_range(fs, b, lo, hi);
-  const int64_t room = bin_room(bb, lo, hi);
-  constexpr int kMaxPer = kMaxCtiles / kWave;
-  int v[kMaxPer], sum = 0;
-#pragma unroll
-  for (int k = 0; k < kMaxPer; ++k) {
-    const int c = lane * per + k;
-    v[k] = (k < per && c < nct) ? tot[c] : 0;
-    sum += v[k];
-  }
-  const int incl = wave_incl_scan(sum);
-  int run = incl - sum;
-#pragma unroll
-  for (int k = 0; k < kMaxPer; ++k) {
-    const int c = lane * per + k;
-    if (k < per && c < nct) bb.base[(int64_t)b * nct + c] = (int64_t)run + v[k] <= room ? run : -1;
-    run += v[k];
-  }
-}
-
-template <typename T>
-__device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty, const FaceSet<T> &fs,
-                           const BinBuffers &ob, const FaceSet<T> &ofs) {
+__device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty) {
   constexpr int kNB = 64, kWaves = kBlock / kWave, kPer = 8;  // buckets: one per lane
   __shared__ int s_cnt[kWaves][kNB];
   __shared__ int s_base, s_next;
   const int tid = threadIdx.x, w = tid >> 6;
   const int nct = bb.g.nct(), n = B * nct;
-  // dispatch headers (bb.hdr): every view's bin bases of both sets first (this workgroup reads
-  // them back below; kd_bin_scatter's chunk-0 workgroups store the same values)
-  if (bb.hdr) {
-    for (int p = w; p < 2 * B; p += kWaves) {
-      if (p & 1)
-        wave_view_bases<T>(ob, ofs, p >> 1);
-      else
-        wave_view_bases<T>(bb, fs, p >> 1);
-    }
-    __syncthreads();
-  }
   const int per = bb.g.ct / kTile;  // fine tiles per coarse tile side
   auto fine_count = [&](int v) {    // fine tiles of (view, coarse tile) v inside the image
     const int c = v % nct;
@@ -472,22 +418,9 @@ __device__ void tile_order(const BinBuffers &bb, int B, int ntx, int nty, const 
       const int b = v / nct, c = v - b * nct;
       const int cx = c % bb.g.nctx, cy = c / bb.g.nctx;
       int pos = atomicAdd(&s_cnt[w][bk[k]], nf[k]);
-      int4 h0 = make_int4(0, tot[k], 0, 0), h1 = make_int4(0, 0, 0, 0);
-      if (bb.hdr) {  // this set's and the other set's bin (count, base) of the coarse tile
-        h0.z = bb.base[v];
-        h1.x = ob.totals[v];
-        h1.y = ob.base[v];
-      }
       for (int ty = cy * per; ty < min(cy * per + per, nty); ++ty)
-        for (int tx = cx * per; tx < min(cx * per + per, ntx); ++tx) {
-          h0.x = (b * nty + ty) * ntx + tx;
-          bb.order[pos] = make_int2(h0.x, tot[k]);
-          if (bb.hdr) {
-            bb.hdr[2 * pos] = h0;
-            bb.hdr[2 * pos + 1] = h1;
-          }
-          ++pos;
-        }
+        for (int tx = cx * per; tx < min(cx * per + per, ntx); ++tx)
+          bb.order[pos++] = make_int2((b * nty + ty) * ntx + tx, tot[k]);
     }
     __syncthreads();
     if (tid == 0) s_base = s_next;

@@ -53,12 +53,6 @@ struct BinBuffers {
   int n_clear_b;
   int2 *order;     // [B * fine tiles] (view * tiles + tile, its coarse bin's face count),
                    // heaviest first (tile_order in kd_bin_scatter): the tile kernels' dispatch order
-  int4 *hdr;       // nullable: [B * fine tiles][2] dispatch headers in the order of `order`:
-                   // {view * tiles + tile, this set's coarse bin count, its base, 0}, {the other
-                   // set's (BinJobs) bin count, its base, 0, 0} -- one load gives a tile kernel
-                   // both bins' places (tile_order; the fused DIB-R forward).  Set to
-                   // hdr_store to have the binning write them.
-  int4 *hdr_store; // the workspace room of hdr (carved always)
   unsigned short *hist;  // nullable: [B * fine tiles][4] per (tile, part) the previous same-shape
                          // call's duration bucket + 1 (0: none), written by the fused forward and
                          // ordering the tiles instead of the coarse counts (kd_set_tile_history)
@@ -73,22 +67,13 @@ template <typename T>
 __device__ void raster_cull_coefs(const T v[6], float M, int H, int W, Span sp, float eps,
                                   float out[8]);
 
-// Usable entries of view rows [lo, hi)'s bin region: a bin ending past it overflows.
-__device__ __forceinline__ int64_t bin_room(const BinBuffers &bb, int64_t lo, int64_t hi) {
-  return (int64_t)((double)bb.limit * (double)bb.xper * (double)(hi - lo));
-}
-
 // Bin (b, c) of view b (rows [lo, lo + nview)): its ascending local face indices and count, or
 // nullptr when the bin overflowed its region -- then the caller walks all nview faces of the
 // view (entry e = local face e) and its exact span filter selects the same faces.
-// nbin / known_base: the bin's count and base when the caller has them (a dispatch header), else
-// -1 / kUnknownBase (read here).
-constexpr int kUnknownBase = -2;
 __device__ __forceinline__ const int *bin_list(const BinBuffers &bb, int b, int c, int64_t lo,
-                                               int nview, int nbin, int &n,
-                                               int known_base = kUnknownBase) {
+                                               int nview, int nbin, int &n) {
   const int64_t bc = (int64_t)b * bb.g.nct() + c;
-  const int base = known_base != kUnknownBase ? known_base : bb.base[bc];
+  const int base = bb.base[bc];
   if (base < 0) {
     n = nview;
     return nullptr;

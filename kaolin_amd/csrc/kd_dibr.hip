@@ -166,9 +166,6 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
       tag = (tag ^ (uint64_t)x) * 1099511628211ull;
     d.rbb.hist = tile_history(4 * (int64_t)B * nt, (long long)(tag >> 1), stream);
     ra.bb.hist = d.rbb.hist;
-    // dispatch headers: the fused forward's workgroups find their tile and both bins in one load
-    // (written by tile_order, which runs only when there are faces: nchunk > 0)
-    if (d.rbb.nchunk > 0) d.rbb.hdr = ra.bb.hdr = d.rbb.hdr_store;
   }
   hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream, prep);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));

@@ -115,8 +115,7 @@ template <typename T, bool CLK = false, int SPLIT = 1>
 __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int b, int tl,
                                                   int nbin, RasterPairsLDS<T> &S,
                                                   long long *clk = nullptr, int part = 0,
-                                                  uint64_t *uncm = nullptr,
-                                                  int bbase = kUnknownBase) {
+                                                  uint64_t *uncm = nullptr) {
   constexpr bool kF64 = sizeof(T) == 8;
   TileLists &L = S.L;
   auto &s_geo = S.geo;
@@ -132,7 +131,6 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   view_range(fs, b, lo, hi);
   TileGeom t = SPLIT == 1 ? tile_geom(H, W, tl) : tile_geom_part<SPLIT>(H, W, tl, part);
   t.nbin = nbin;
-  t.bbase = bbase;
   const int kw = t.sub;  // LDS key row of this wave's pixels
   const float sx = M / (float)W, sy = M / (float)H;  // px_cx / px_cy, first factor
   {  // (the walk's first barrier orders these before any pass B)

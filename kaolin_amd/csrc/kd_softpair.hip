@@ -486,8 +486,7 @@ template <typename T, bool FUSED, int SPLIT = 1, bool CLK = false>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                 int b, int tl, int nbin, SoftPairsLDS<FUSED> &S,
                                                 int part = 0, const uint64_t *uncm = nullptr,
-                                                long long *clk = nullptr,
-                                                int bbase = kUnknownBase) {
+                                                long long *clk = nullptr) {
   static_assert(SPLIT == 1 || FUSED, "split tiles: the fused soft mask only");
   TileLists &L = S.L;
   const FaceSet<T> &fs = a.fs;
@@ -498,7 +497,6 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   const int nview = (int)(hi - lo);
   TileGeom t = SPLIT == 1 ? tile_geom(H, W, tl) : tile_geom_part<SPLIT>(H, W, tl, part);
   t.nbin = nbin;
-  t.bbase = bbase;
   const int tile_q = t.sub * kWave + lane;  // the pixel's index in the 16x16 tile frame
   if (KD_DIAG && fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, bin) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
@@ -553,7 +551,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       const BinGeom &g = a.bb.g;
       const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
       int nb;
-      bin_list(a.bb, b, ct, lo, nview, nbin, nb, bbase);
+      bin_list(a.bb, b, ct, lo, nview, nbin, nb);
       const int64_t room = (int64_t)U * (int64_t)min(K, nb);
       if (room > 0) {
         const int64_t b0 = (int64_t)atomicAdd(pb.cursor, (unsigned long long)room);
@@ -816,19 +814,7 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
     s_done = 0;
   }
   int b, tl, nbin, part;
-  int rbase = kUnknownBase, snbin = -1, sbase = kUnknownBase;
-  if (ra.bb.hdr && ra.bb.nchunk > 0) {  // one header load: the tile and both bins' places
-    const TileHdr h = tile_hdr_of_block<SPLIT>(ra.bb, ra.fs.H, ra.fs.W, ra.fs.dbg);
-    b = h.b;
-    tl = h.tile;
-    part = h.part;
-    nbin = h.rn;
-    rbase = h.rbase;
-    snbin = h.sn;
-    sbase = h.sbase;
-  } else {
-    tile_of_block_split<SPLIT>(ra.bb, ra.fs.H, ra.fs.W, b, tl, part, nbin, ra.fs.dbg);
-  }
+  tile_of_block_split<SPLIT>(ra.bb, ra.fs.H, ra.fs.W, b, tl, part, nbin, ra.fs.dbg);
   if (DIAG && a.fs.tbuf && threadIdx.x == 0) {
     const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
     a.fs.tbuf[slot] = ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
@@ -839,14 +825,14 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
   }
   raster_pairs_tile<float, DIAG, SPLIT>(
       ra, b, tl, nbin, U.r, DIAG && a.fs.tbuf ? a.fs.tbuf + 7ll * gridDim.x * gridDim.y : nullptr,
-      part, uncm, rbase);
+      part, uncm);
   __syncthreads();  // the raster phase is done with the LDS
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
   soft_pairs_tile<float, true, SPLIT, DIAG>(
-      a, pb, b, tl, snbin, U.s, part, uncm,
-      DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr, sbase);
+      a, pb, b, tl, -1, U.s, part, uncm,
+      DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr);
   // tile history (kd_set_tile_history): the last wave to finish stores the workgroup's duration
   // as a quarter-octave bucket (1..63; 0 = none) for the next same-shape call's dispatch order
   if (ra.bb.hist && (threadIdx.x & (kWave - 1)) == 0 &&

@@ -29,7 +29,6 @@ struct TileGeom {
   int px, py;              // this lane's pixel
   bool inimg, wave_live;
   int nbin;                // faces in the tile's coarse bin when known (tile order), else -1
-  int bbase;               // its base when known (dispatch header), else kUnknownBase
   // face filter boxes of tile_rounds (default: the tile and the wave's sub-tile); a caller whose
   // pixels do not all need faces may shrink them to the pixels that do (wave_live = false when
   // the wave has none)
@@ -91,7 +90,6 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
   t.inimg = t.px < W && t.py < H;
   t.wave_live = t.WX0 < W && t.WY0 < H;
   t.nbin = -1;
-  t.bbase = kUnknownBase;
   t.FX0 = t.X0;
   t.FX1 = t.X1;
   t.FY0 = t.Y0;
@@ -136,7 +134,6 @@ __device__ __forceinline__ TileGeom tile_geom_part(int H, int W, int tile, int p
   t.inimg = t.px < W && t.py < H;
   t.wave_live = t.WX0 < W && t.WY0 < H;
   t.nbin = -1;
-  t.bbase = kUnknownBase;
   t.FX0 = t.X0;
   t.FX1 = t.X1;
   t.FY0 = t.Y0;
@@ -179,34 +176,6 @@ __device__ __forceinline__ void tile_of_block_split(const BinBuffers &bb, int H,
     tile = ts - b * ntiles;
     nbin = -1;
   }
-}
-
-// The dispatch header of this workgroup (bb.hdr, tile_order): its (view, fine tile, part) as
-// tile_of_block_split computes them, and both face sets' coarse bins (count, base) -- one 32-byte
-// load instead of the order entry followed by each bin's base.
-struct TileHdr {
-  int b, tile, part;
-  int rn, rbase;  // the header set's bin (the raster's in kd_dibr_fwd_tiles)
-  int sn, sbase;  // the other set's (the soft mask's)
-};
-template <int SPLIT>
-__device__ __forceinline__ TileHdr tile_hdr_of_block(const BinBuffers &bb, int H, int W,
-                                                     int dbg = 0) {
-  const int n = gridDim.x * gridDim.y;
-  int d = blockIdx.y * gridDim.x + blockIdx.x;
-  if ((d | 31) < n && !ablate(dbg, (1 << 17))) d = (d & ~31) | ((d & 7) << 2) | ((d >> 3) & 3);
-  TileHdr h;
-  h.part = d % SPLIT;
-  const int ts = d / SPLIT;
-  const int4 h0 = bb.hdr[2 * ts], h1 = bb.hdr[2 * ts + 1];
-  const int ntiles = ((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
-  h.b = h0.x / ntiles;
-  h.tile = h0.x - h.b * ntiles;
-  h.rn = h0.y;
-  h.rbase = h0.z;
-  h.sn = h1.x;
-  h.sbase = h1.y;
-  return h;
 }
 
 struct TileLists {
@@ -271,7 +240,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
   int n;
-  const int *bin = bin_list(bb, b, ct, lo, nview, t.nbin, n, t.bbase);
+  const int *bin = bin_list(bb, b, ct, lo, nview, t.nbin, n);
   int cnt = 0;
   // kPrefetch chunks of bin entries and their spans are loaded up front (two dependent
   // round trips per kPrefetch * 256 entries instead of per 256)
