@@ -160,11 +160,13 @@ class Workload:
             disc = (((yy - H / 2) ** 2 + (xx - W / 2) ** 2) < (0.4 * min(H, W)) ** 2).to(dt)
             self.gt = disc.expand(n, H, W).contiguous().to(dev)
         self.params = [self.fvi, self.feats] if self.soup else [self.vertices, self.feats]
-        # --perturb LR: the step ends with a signSGD update of the vertices by their own gradient
-        # (the magnitude of an Adam step, ian_dibr.py:172-173, 288-290), captured in the graph, so
-        # every replay renders moved geometry and the tile history always describes the previous
-        # step's mesh, as in a training loop
+        # --perturb LR: the step ends by moving the mesh with its own gradient -- the vertices
+        # become v0 - LR * sign(grad), an Adam-sized step (ian_dibr.py:172-173, 288-290) from the
+        # initial mesh v0, captured in the graph -- so every replay renders geometry the previous
+        # step's tile history was not measured on, while the workload stays the C3 sphere
+        # (anchored at v0: repeated sign steps would otherwise roughen it step after step)
         self.perturb = 0.0 if self.soup else float(getattr(args, 'perturb', 0.0) or 0.0)
+        self.v0 = self.vertices.detach().clone() if self.perturb else None
 
     def forward_backward(self):
         """The GPU part of the step (no collective)."""
@@ -179,7 +181,8 @@ class Workload:
             fused_vertices=self.vertex_path != 'compose', **self.kw)
         if self.perturb:
             with torch.no_grad():
-                self.vertices.sub_(self.perturb * self.vertices.grad.sign())
+                torch.add(self.v0, self.vertices.grad.sign(), alpha=-self.perturb,
+                          out=self.vertices)
         return face_idx
 
     def clear(self):
@@ -341,9 +344,9 @@ def main():
                     help='dispatch the fused forward by the previous same-shape call\'s tile '
                          'durations (kd_set_tile_history; default on)')
     ap.add_argument('--perturb', type=float, default=0.0, metavar='LR',
-                    help='move the mesh every step: a signSGD step of size LR on the vertices '
-                         'with the step\'s own gradient, inside the timed step (1 GPU; tile '
-                         'history A/B under motion)')
+                    help='move the mesh every step: vertices = v0 - LR * sign(grad) with the '
+                         'step\'s own gradient, inside the timed step (1 GPU; tile history A/B '
+                         'under motion)')
     ap.add_argument('--pmc', default=None,
                     help='PMC traffic summary (default profiles/r04, r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
@@ -528,8 +531,8 @@ def main():
                    'coarse_tile': args.coarse_tile or 'auto',
                    'tile_history': bool(args.tile_history),
                    'perturb': None if not wl.perturb else {
-                       'lr': wl.perturb, 'update': 'vertices -= lr * sign(vertices.grad) inside '
-                                                   'every timed step (graph)',
+                       'lr': wl.perturb, 'update': 'vertices = v0 - lr * sign(vertices.grad) '
+                                                   'inside every timed step (graph)',
                        'covered_px_first_step': covered0},
                    'close_lists': 'materialised' if args.lists else 'not materialised',
                    'soft_mask_grad': (f'mask_iou(soft, gt) ({args.iou})' if args.iou

@@ -26,17 +26,33 @@ SLOT = {
 }
 
 
+# per-type VALU instruction counters (tools/pmc_mix.sh); bench.py weights them by issue cost
+VALU_MIX = tuple(f'SQ_INSTS_VALU_{k}' for k in (
+    'ADD_F32', 'MUL_F32', 'FMA_F32', 'TRANS_F32', 'ADD_F64', 'MUL_F64', 'FMA_F64', 'TRANS_F64',
+    'INT32', 'INT64', 'CVT'))
+
+
 def main(summary, out, config, dtype='f32', views=8, lists=False):
     src = json.load(open(summary))
     kern = {}
+    # several device variants can share a slot (e.g. kd_bin_count<.., PREP> of the bench step and
+    # the plain kd_bin_count of bench.py's one pair-count call): the slot takes the variant with
+    # the most dispatches, i.e. the one the timed step runs
+    best = {}
     for name, m in src.items():
         slot = SLOT.get(name.split('<')[0].split('(')[0].replace('void ', ''))
         if slot is None or 'hbm_bytes_raw' not in m:
             continue
+        if slot not in best or m.get('dispatches', 0) > src[best[slot]].get('dispatches', 0):
+            best[slot] = name
+    for slot, name in best.items():
+        m = src[name]
         kern[slot] = {'device_kernel': name,
                       'hbm_bytes_per_launch': round(m['hbm_bytes_fetch_x2']),
                       'FETCH_SIZE_KiB': m['FETCH_SIZE'], 'WRITE_SIZE_KiB': m['WRITE_SIZE']}
-        for c in ('SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_WAVES', 'GRBM_GUI_ACTIVE'):
+        kern[slot]['dispatches'] = m.get('dispatches')
+        for c in ('SQ_INSTS_VALU', 'SQ_INSTS_SALU', 'SQ_WAVES', 'GRBM_GUI_ACTIVE',
+                  'SQ_ACTIVE_INST_VALU', 'SQ_INSTS_LDS', 'SQ_WAVE_CYCLES', 'SQ_WAIT_ANY') + VALU_MIX:
             if c in m:  # per launch (bench.py: VALU issue fraction)
                 kern[slot][c] = m[c]
     json.dump({'config': config, 'dtype': dtype, 'views_per_gpu': views, 'lists': lists,

@@ -11,6 +11,7 @@ from collections import defaultdict
 
 out = sys.argv[1] if len(sys.argv) > 1 else 'gpurun_out/pmc'
 vals = defaultdict(lambda: defaultdict(list))
+disp = defaultdict(set)  # (pass file, dispatch id): dispatches of each kernel variant
 for f in glob.glob(os.path.join(out, 'p*', '**', '*counter_collection.csv'), recursive=True):
     for r in csv.DictReader(open(f)):
         name = r.get('Kernel_Name') or r.get('Kernel-Name') or ''
@@ -18,11 +19,13 @@ for f in glob.glob(os.path.join(out, 'p*', '**', '*counter_collection.csv'), rec
         cn = r.get('Counter_Name') or r.get('Counter-Name')
         v = float(r.get('Counter_Value') or r.get('Counter-Value') or 0)
         vals[short][cn].append(v)
+        disp[short].add((f, r.get('Dispatch_Id') or r.get('Dispatch-Id')))
 res = {}
 for k, d in vals.items():
     if not k.startswith('kd::'):
         continue
     res[k] = {cn: sum(v) / len(v) for cn, v in d.items()}
+    res[k]['dispatches'] = len(disp[k])  # over all passes
     m = res[k]
     if 'FETCH_SIZE' in m and 'WRITE_SIZE' in m:
         m['hbm_bytes_raw'] = (m['FETCH_SIZE'] + m['WRITE_SIZE']) * 1024
