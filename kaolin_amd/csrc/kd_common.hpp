@@ -37,7 +37,8 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       host presets the indices to -1 so that the backward reads no garbage),
 //       1 << 20 256-face binning chunks, 1 << 21 one count workgroup for both face sets,
 //       1 << 29 the lane-per-pixel K-list backward,
-//       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost).
+//       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost),
+//       1 << 24 the fused forward without its soft phase (the raster phase's instruction counts).
 #if KD_DIAG
 int debug_flags();
 #else

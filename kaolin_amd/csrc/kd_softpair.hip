@@ -830,9 +830,10 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
   if (DIAG && a.fs.tbuf && threadIdx.x == 0)
     a.fs.tbuf[3ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
         wall_clock64();
-  soft_pairs_tile<float, true, SPLIT, DIAG>(
-      a, pb, b, tl, -1, U.s, part, uncm,
-      DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr);
+  if (!ablate(a.fs.dbg, 1 << 24))  // diagnostics: the raster phase alone (instruction counts)
+    soft_pairs_tile<float, true, SPLIT, DIAG>(
+        a, pb, b, tl, -1, U.s, part, uncm,
+        DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr);
   // tile history (kd_set_tile_history): the last wave to finish stores the workgroup's duration
   // as a quarter-octave bucket (1..63; 0 = none) for the next same-shape call's dispatch order
   if (ra.bb.hist && (threadIdx.x & (kWave - 1)) == 0 &&
