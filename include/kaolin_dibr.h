@@ -68,13 +68,10 @@ int kd_debug_buffer(void *device_ptr);
  * (the op forms, knum > 32, D > 3).  A test sets these bits to run dibr_rasterization through the
  * separate launches and compare.  Bits: KD_FORM_SPLIT_FWD raster then soft mask as two launches,
  * KD_FORM_SPLIT_BWD the two backwards as two launches, KD_FORM_SOFT_SPLIT the soft mask's pass A,
- * pair math and product as three launches (the K-list pipeline without the lists),
- * KD_FORM_COARSE_RASTER the one-launch fp32 forward's raster phase over the raster set's ordered
- * coarse bins instead of its per-16x16-tile face records (the binning count's fine lists). */
+ * pair math and product as three launches (the K-list pipeline without the lists). */
 #define KD_FORM_SPLIT_FWD 1
 #define KD_FORM_SPLIT_BWD 2
 #define KD_FORM_SOFT_SPLIT 4
-#define KD_FORM_COARSE_RASTER 8
 int kd_set_test_forms(int forms);
 
 /* Workgroups per 16x16 tile of dibr_rasterization's fp32 forward (a test and tuning hook; 0 by

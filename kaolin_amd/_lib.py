@@ -186,7 +186,7 @@ def set_pool_limits(bins=1.0, pairs=1.0):
 _pool_limited = False
 
 # kd_set_test_forms bits (include/kaolin_dibr.h KD_FORM_*)
-FORM_SPLIT_FWD, FORM_SPLIT_BWD, FORM_SOFT_SPLIT, FORM_COARSE_RASTER = 1, 2, 4, 8
+FORM_SPLIT_FWD, FORM_SPLIT_BWD, FORM_SOFT_SPLIT = 1, 2, 4
 
 
 def set_test_forms(forms=0):

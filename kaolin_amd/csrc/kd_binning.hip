@@ -6,7 +6,6 @@
 
 #include "kd_capi.hpp"
 
-#include <algorithm>
 #include <type_traits>
 
 namespace kd {
@@ -30,49 +29,6 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view,
   s += align_up(sizeof(float4) * 2 * (size_t)N);
   s += align_up(sizeof(int2) * (size_t)B * fine_tiles(H, W));
   return s;
-}
-
-// record slots per view: chunks x chunk x kRecPerFace for the larger of the two chunk sizes
-static int64_t fine_slots(int64_t F) {
-  int64_t m = 0;
-  for (const int64_t c : {(int64_t)kChunk / 2, (int64_t)kChunk})
-    m = std::max(m, (F + c - 1) / c * c * kRecPerFace);
-  return m;
-}
-
-bool fine_possible(int B, int H, int W, int64_t F) {
-  const int64_t nft = fine_tiles(H, W);
-  const int64_t nchunk_max = (F + kChunk / 2 - 1) / (kChunk / 2);  // the smaller chunk
-  return B > 0 && F > 0 && nft > 0 && nft <= kMaxFineTiles && nft <= kMaxCtiles &&
-         nchunk_max <= kMaxFineChunks && (int64_t)B * F < (1ll << 31);
-}
-
-size_t fine_workspace_bytes(int B, int H, int W, int64_t F) {
-  if (!fine_possible(B, H, W, F)) return 0;
-  // sized for either chunk bin_chunk may pick: the smaller one has the most chunks (row
-  // entries), the larger one the most rounding (record slots)
-  const int64_t nchunk = (F + kChunk / 2 - 1) / (kChunk / 2);
-  size_t s = align_up(sizeof(int) * (size_t)B * (size_t)fine_tiles(H, W) * (size_t)nchunk);
-  s += align_up(sizeof(RasterRec) * (size_t)B * (size_t)fine_slots(F));
-  return s;
-}
-
-FineLists fine_carve(void *ws, size_t &off, int B, int H, int W, int64_t F) {
-  FineLists fl{};
-  if (!fine_possible(B, H, W, F)) return fl;
-  char *base = (char *)ws;
-  const int64_t nchunk_max = (F + kChunk / 2 - 1) / (kChunk / 2);
-  fl.chunk = bin_chunk(B, F);
-  fl.nchunk = (int)((F + fl.chunk - 1) / fl.chunk);
-  fl.ftx = (W + kTile - 1) / kTile;
-  fl.nft = (int)fine_tiles(H, W);
-  // kd_set_pool_limits' bin fraction limits the segments too (a test of the overflow path)
-  fl.cap = (int)((double)pool_limit_bins() * (double)(fl.chunk * kRecPerFace));
-  fl.tab = (int *)(base + off);
-  off += align_up(sizeof(int) * (size_t)B * (size_t)fl.nft * (size_t)nchunk_max);
-  fl.rec = (RasterRec *)(base + off);
-  off += align_up(sizeof(RasterRec) * (size_t)B * (size_t)fine_slots(F));
-  return fl;
 }
 
 BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
@@ -121,18 +77,15 @@ struct BinJobs {
   BinBuffers bb[2];
   SpanConsts k[2];  // make_span constants of each set (host-computed)
   PrepOut<T> prep;  // prep.a.vertices set: the corners come from prepare_vertices (kd_bin_count PREP)
-  FineIn<T> fine;   // fine.fl.tab set: set 0 is written as raster fine lists (kd_bin_count FINE)
-  int zbase;        // the set of blockIdx.z 0 in the scan / scatter launches (1 with fine lists)
 };
 
 // One face of one set: its exact span (stored), the raster set's cull coefficients, and its
 // coarse tiles counted in LDS.  v: the face's scaled corners (loaded once for both sets).
 // nzv (PREP): the face's normal z just computed, used instead of reading fs.nz.
-// ftx > 0 (raster fine lists): the face is counted per 16x16 tile (ftx tiles per row) instead.
 template <typename T>
 __device__ __forceinline__ void bin_count_face(const FaceSet<T> &fs, const BinBuffers &bb,
                                                const SpanConsts &k, int64_t i, const T v[6],
-                                               int *s_cnt, const T *nzv = nullptr, int ftx = 0) {
+                                               int *s_cnt, const T *nzv = nullptr) {
   Span s;
   const bool ok = (!fs.valid || fs.valid[i]) &&
                   (!fs.nz || (nzv ? *nzv : fs.nz[i * fs.nz_stride]) >= (T)0);
@@ -153,11 +106,7 @@ __device__ __forceinline__ void bin_count_face(const FaceSet<T> &fs, const BinBu
     s.y1 = 0;
   }
   bb.spans[i] = s;
-  if (ftx > 0) {
-    if (!span_empty(s))
-      for (int ty = s.y0 >> 4; ty <= s.y1 >> 4; ++ty)
-        for (int tx = s.x0 >> 4; tx <= s.x1 >> 4; ++tx) atomicAdd(&s_cnt[ty * ftx + tx], 1);
-  } else if (!span_empty(s) && !ablate(fs.dbg, 1 << 19)) {
+  if (!span_empty(s) && !ablate(fs.dbg, 1 << 19)) {
     const int cx0 = s.x0 >> bb.g.sh, cx1 = s.x1 >> bb.g.sh;
     const int cy0 = s.y0 >> bb.g.sh, cy1 = s.y1 >> bb.g.sh;
     for (int cy = cy0; cy <= cy1; ++cy)
@@ -173,99 +122,18 @@ __device__ __forceinline__ void bin_count_face(const FaceSet<T> &fs, const BinBu
 // (kd_prep.hpp) on the vertices, and the raster set's workgroups (blockIdx.z 0; NS = 2: every
 // workgroup) also write its outputs (fvc, fvi, normals; rows staged in LDS, coalesced) -- no
 // kd_prepare_fwd launch, no reading the corners back.
-// The raster fine lists of one chunk (kd_binning.hpp FineLists), after its faces were counted
-// per 16x16 tile into s_cnt: the exclusive scan of the counts gives each tile its group in the
-// chunk's segment (written to the tile's row entry), then every face writes its record into each
-// tile it touches (an LDS cursor per tile; the order inside a group does not matter to the
-// raster).  A chunk whose records exceed its segment marks its groups overflowed and writes none.
-// The record's data are the ones this workgroup has just written (spans, culling coefficients,
-// prepare_vertices' outputs) or read (corners, depths).
-template <typename T, int PER, bool PREP>
-__device__ __forceinline__ void fine_finish(const BinJobs<T> &jobs, int b, int chunk, int64_t lo,
-                                            int64_t hi, int *s_cnt) {
-  if constexpr (std::is_same<T, float>::value) {
-    __shared__ int s_scan[kBlock / kWave];
-    const FineLists &fl = jobs.fine.fl;
-    const BinBuffers &bb = jobs.bb[0];
-    const FaceSet<T> &fs = jobs.fs[0];
-    const int tid = threadIdx.x, nft = fl.nft, ftx = fl.ftx;
-    constexpr int kPer = kMaxFineTiles / kBlock;
-    int v[kPer], sum = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int t = tid * kPer + k;
-      v[k] = t < nft ? s_cnt[t] : 0;
-      sum += v[k];
-    }
-    int total;
-    int run = wg_exclusive_scan(sum, s_scan, total);
-    const bool ovf = total > fl.cap;
-    int *tab = fl.tab + (int64_t)b * nft * fl.nchunk + chunk;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int t = tid * kPer + k;
-      if (t < nft) {
-        tab[(int64_t)t * fl.nchunk] = ovf ? (v[k] ? kFineOvf : 0) : ((run << 16) | v[k]);
-        s_cnt[t] = run;  // the tile's cursor
-      }
-      run += v[k];
-    }
-    if (ovf) return;  // (workgroup-uniform)
-    __syncthreads();
-    RasterRec *seg =
-        fl.rec + ((int64_t)b * fl.nchunk + chunk) * (int64_t)fl.chunk * kRecPerFace;
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int64_t i = lo + (int64_t)chunk * (PER * kBlock) + u * kBlock + tid;
-      if (i >= hi) continue;
-      const Span sp = bb.spans[i];  // (this thread's own stores)
-      if (span_empty(sp)) continue;
-      float c[6], z[3];
-      if constexpr (PREP) {
-        const float *fi = jobs.prep.fvi + i * 6, *zc = jobs.prep.fvc + i * 9;
-#pragma unroll
-        for (int k = 0; k < 6; ++k) c[k] = fi[k] * fs.scale;  // load_corners' product
-#pragma unroll
-        for (int k = 0; k < 3; ++k) z[k] = zc[k * 3 + 2];  // = the raster's fvc[..., 2]
-      } else {
-        load_corners(fs, i, c);
-        const float *zz = jobs.fine.fvz + i * jobs.fine.fvz_fs;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) z[k] = zz[k * jobs.fine.fvz_cs];
-      }
-      const PSpan ps = pack_span(sp);
-      RasterRec r;
-      r.g0 = make_float4(c[0], c[1], c[2], c[3]);
-      r.g1 = make_float4(c[4], c[5], z[0], z[1]);
-      r.g2 = make_float4(z[2], __int_as_float((int)(i - lo)), __uint_as_float(ps.lo),
-                         __uint_as_float(ps.hi));
-      r.cl = bb.cull[2 * i];
-      r.ch = bb.cull[2 * i + 1];
-      for (int ty = sp.y0 >> 4; ty <= sp.y1 >> 4; ++ty)
-        for (int tx = sp.x0 >> 4; tx <= sp.x1 >> 4; ++tx)
-          seg[atomicAdd(&s_cnt[ty * ftx + tx], 1)] = r;
-    }
-  }
-}
-
-// FINE (NS = 1): set 0's workgroups (blockIdx.z 0: the raster's valid faces) count per 16x16 tile
-// and write the raster fine lists (fine_finish) instead of coarse counts.
-template <typename T, int PER, int NS, bool PREP = false, bool FINE = false>  // PER = chunk / 256
+template <typename T, int PER, int NS, bool PREP = false>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
-  static_assert(!FINE || NS == 1, "fine lists: one set per workgroup");
   __shared__ int s_cnt[NS][kMaxCtiles];
   __shared__ __align__(16) T s_pc[PREP ? kBlock * 9 : 1];
   __shared__ __align__(16) T s_pi[PREP ? kBlock * 6 : 1];
   __shared__ __align__(16) T s_pn[PREP ? kBlock * 3 : 1];
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int z0 = NS == 2 ? 0 : blockIdx.z;  // NS = 1: blockIdx.z selects the set
-  const bool fine = FINE && z0 == 0;        // (workgroup-uniform)
   const int nct = jobs.bb[z0].g.nct();
-  const int ftx = fine ? jobs.fine.fl.ftx : 0;
-  const int ncnt = fine ? jobs.fine.fl.nft : nct;  // (both <= kMaxCtiles)
 #pragma unroll
   for (int z = 0; z < NS; ++z)
-    for (int c = tid; c < ncnt; c += kBlock) s_cnt[z][c] = 0;
+    for (int c = tid; c < nct; c += kBlock) s_cnt[z][c] = 0;
   if (b == 0 && chunk == 0) {
 #pragma unroll
     for (int z = 0; z < NS; ++z) {
@@ -293,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 #pragma unroll
         for (int z = 0; z < NS; ++z)
           bin_count_face<T>(jobs.fs[z0 + z], jobs.bb[z0 + z], jobs.k[z0 + z], i, v, s_cnt[z],
-                            &n[2], ftx);
+                            &n[2]);
       }
       if (z0 == 0 && i0 < hi) {  // (workgroup-uniform)
         const int rows = (int)min((int64_t)kBlock, hi - i0);
@@ -308,17 +176,10 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
       load_corners(jobs.fs[z0], i, v);
 #pragma unroll
       for (int z = 0; z < NS; ++z)
-        bin_count_face<T>(jobs.fs[z0 + z], jobs.bb[z0 + z], jobs.k[z0 + z], i, v, s_cnt[z],
-                          nullptr, ftx);
+        bin_count_face<T>(jobs.fs[z0 + z], jobs.bb[z0 + z], jobs.k[z0 + z], i, v, s_cnt[z]);
     }
   }
   __syncthreads();
-  if constexpr (FINE) {
-    if (fine) {  // (workgroup-uniform)
-      fine_finish<T, PER, PREP>(jobs, b, chunk, lo, hi, s_cnt[0]);
-      return;
-    }
-  }
 #pragma unroll
   for (int z = 0; z < NS; ++z) {
     const BinBuffers &bb = jobs.bb[z0 + z];
@@ -334,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 // chip.
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
-  const BinBuffers &bb = jobs.bb[jobs.zbase + blockIdx.z];
+  const BinBuffers &bb = jobs.bb[blockIdx.z];
   const int nct = bb.g.nct();
   const int wv = threadIdx.x >> 6;
   const int c = blockIdx.x * (kBlock / kWave) + wv;
@@ -386,8 +247,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
 
 template <typename T, int PER>  // PER = chunk / 256 faces per thread
 __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
-  const FaceSet<T> &fs = jobs.fs[jobs.zbase + blockIdx.z];
-  const BinBuffers &bb = jobs.bb[jobs.zbase + blockIdx.z];
+  const FaceSet<T> &fs = jobs.fs[blockIdx.z];
+  const BinBuffers &bb = jobs.bb[blockIdx.z];
   if (blockIdx.x == gridDim.x - 1) {  // the extra column: the set's tile dispatch order
     if (blockIdx.y == 0)
       tile_order(bb, fs.B, (fs.W + kTile - 1) / kTile, (fs.H + kTile - 1) / kTile);
@@ -615,21 +476,8 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
       done = shared;
     }
     const bool prep = jobs.prep.a.vertices != nullptr;
-    const bool fine = jobs.fine.fl.tab != nullptr && njobs == 2;
     if (done) {
-    } else if (fine && prep && two)
-      hipLaunchKernelGGL((kd_bin_count<T, 2, 1, true, true>), grid_c, dim3(kBlock), 0, stream,
-                         jobs);
-    else if (fine && prep)
-      hipLaunchKernelGGL((kd_bin_count<T, 1, 1, true, true>), grid_c, dim3(kBlock), 0, stream,
-                         jobs);
-    else if (fine && two)
-      hipLaunchKernelGGL((kd_bin_count<T, 2, 1, false, true>), grid_c, dim3(kBlock), 0, stream,
-                         jobs);
-    else if (fine)
-      hipLaunchKernelGGL((kd_bin_count<T, 1, 1, false, true>), grid_c, dim3(kBlock), 0, stream,
-                         jobs);
-    else if (prep && two)
+    } else if (prep && two)
       hipLaunchKernelGGL((kd_bin_count<T, 2, 1, true>), grid_c, dim3(kBlock), 0, stream, jobs);
     else if (prep)
       hipLaunchKernelGGL((kd_bin_count<T, 1, 1, true>), grid_c, dim3(kBlock), 0, stream, jobs);
@@ -638,13 +486,9 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
     else
       hipLaunchKernelGGL((kd_bin_count<T, 1, 1>), grid_c, dim3(kBlock), 0, stream, jobs);
   }
-  // with fine lists set 0 is done: the scan and the scatter bin set 1 alone
-  jobs.zbase = (jobs.fine.fl.tab != nullptr && njobs == 2) ? 1 : 0;
-  const int nsets = njobs - jobs.zbase;
-  const dim3 grid_s2(grid_t.x, fs.B, nsets);
   {
     ProfScope prof(K_BIN_SCAN, stream);
-    hipLaunchKernelGGL(kd_bin_scan<T>, grid_s2, dim3(kBlock), 0, stream, jobs);
+    hipLaunchKernelGGL(kd_bin_scan<T>, grid_t, dim3(kBlock), 0, stream, jobs);
   }
   {  // + one column of workgroups for the tile order (kd_bin_scatter, tile_order)
     // chunk-bit masks per coarse tile: up to 64 KB of dynamic LDS at 1024 coarse tiles (a
@@ -658,10 +502,10 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
     }
     ProfScope prof(K_BIN_SCATTER, stream);
     if (two)
-      hipLaunchKernelGGL((kd_bin_scatter<T, 2>), dim3(bb.nchunk + 1, fs.B, nsets), dim3(kBlock),
+      hipLaunchKernelGGL((kd_bin_scatter<T, 2>), dim3(bb.nchunk + 1, fs.B, njobs), dim3(kBlock),
                          dyn, stream, jobs);
     else
-      hipLaunchKernelGGL((kd_bin_scatter<T, 1>), dim3(bb.nchunk + 1, fs.B, nsets), dim3(kBlock),
+      hipLaunchKernelGGL((kd_bin_scatter<T, 1>), dim3(bb.nchunk + 1, fs.B, njobs), dim3(kBlock),
                          dyn, stream, jobs);
   }
   return hipGetLastError();
@@ -678,22 +522,13 @@ hipError_t bin_faces(const FaceSet<T> &fs, const BinBuffers &bb, hipStream_t str
 
 template <typename T>
 hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSet<T> &fs1,
-                      const BinBuffers &bb1, hipStream_t stream, const PrepOut<T> *prep,
-                      const FineIn<T> *fine) {
+                      const BinBuffers &bb1, hipStream_t stream, const PrepOut<T> *prep) {
   // both sets must describe the same views, faces and image (same chunking and tile grid)
   if (fs0.B != fs1.B || fs0.N != fs1.N || fs0.H != fs1.H || fs0.W != fs1.W ||
       bb0.nchunk != bb1.nchunk || bb0.g.nct() != bb1.g.nct())
     return hipErrorInvalidValue;
   BinJobs<T> jobs{};
   if (prep) jobs.prep = *prep;
-  if (fine && fine->fl.tab) {
-    // fine lists: fp32 only, within the count's LDS (tiles) and the row scan (chunks)
-    if (!std::is_same<T, float>::value || fine->fl.nft > kMaxFineTiles ||
-        fine->fl.nft > kMaxCtiles || bb0.nchunk > kMaxFineChunks ||
-        fine->fl.nchunk != bb0.nchunk || fine->fl.chunk != bb0.chunk)
-      return hipErrorInvalidValue;
-    jobs.fine = *fine;
-  }
   jobs.fs[0] = fs0;
   jobs.fs[1] = fs1;
   jobs.bb[0] = bb0;
@@ -750,10 +585,10 @@ hipError_t zero_words(void *p, size_t bytes, hipStream_t stream) {
 
 template hipError_t bin_faces2<float>(const FaceSet<float> &, const BinBuffers &,
                                       const FaceSet<float> &, const BinBuffers &, hipStream_t,
-                                      const PrepOut<float> *, const FineIn<float> *);
+                                      const PrepOut<float> *);
 template hipError_t bin_faces2<double>(const FaceSet<double> &, const BinBuffers &,
                                        const FaceSet<double> &, const BinBuffers &, hipStream_t,
-                                       const PrepOut<double> *, const FineIn<double> *);
+                                       const PrepOut<double> *);
 template int zero_buffers<float>(float *, int64_t, float *, int64_t, hipStream_t);
 template int zero_buffers<double>(double *, int64_t, double *, int64_t, hipStream_t);
 template hipError_t bin_faces<float>(const FaceSet<float> &, const BinBuffers &, hipStream_t);

@@ -61,45 +61,6 @@ struct BinBuffers {
   BinGeom g;
 };
 
-// ------------------------------------------------------------------------------------------
-// Raster fine lists (the one-launch fp32 DIB-R forward).  The raster's result does not depend on
-// the order in which a pixel meets its faces (the winner is a maximum of (depth, ~face) keys,
-// kd_raster_pairs.hpp), so the raster set needs no ordered bins: the binning count writes, per
-// (view, binning chunk), the chunk's valid faces as 80-byte records grouped by the 16x16 tile
-// they touch, and per (view, tile, chunk) the group's place.  A tile's faces are then read as
-// contiguous records -- no coarse-bin walk, no span filter, no gathers of corners / depths /
-// culling coefficients -- and the raster set needs neither the scan nor the scatter launch.
-//   tab  [B][nft][nchunk] int32, tile-major (a tile's row is contiguous): (offset in the chunk's
-//        segment << 16) | count; count kFineOvf: the chunk's records did not fit its segment
-//        (the tile then walks every face of its view with the exact span filter instead)
-//   rec  [B][nchunk][cap] RasterRec: segment of (view, chunk), cap = chunk * kRecPerFace slots
-// ------------------------------------------------------------------------------------------
-constexpr int kRecPerFace = 4;         // segment slots per face of a chunk
-constexpr int kMaxFineTiles = 1024;    // 16x16 tiles per view (LDS of the count)
-constexpr int kMaxFineChunks = 1024;   // binning chunks per view (4 row entries per thread)
-constexpr int kFineOvf = 0xffff;
-
-struct RasterRec {
-  float4 g0;  // ax ay bx by (scaled corners)
-  float4 g1;  // cx cy az bz
-  float4 g2;  // cz, the local face index (int bits), span lo / hi (PSpan bits)
-  float4 cl;  // raster_cull_coefs lo0 / lo1
-  float4 ch;  // hi0 / hi1
-};
-
-struct FineLists {
-  int *tab;        // nullptr: off (the raster set is binned into ordered coarse bins)
-  RasterRec *rec;
-  int nft, ftx;    // 16x16 tiles per view, per row
-  int cap;         // record slots per (view, chunk) segment usable by this call
-  int nchunk, chunk;
-};
-
-// whether the shape allows the fine lists, and their workspace (0 when it does not)
-bool fine_possible(int B, int H, int W, int64_t F);
-size_t fine_workspace_bytes(int B, int H, int W, int64_t F);
-FineLists fine_carve(void *ws, size_t &offset, int B, int H, int W, int64_t F);
-
 // Edge-culling coefficients of one face in its own frame (column span.x0, row span.y0); see
 // kd_cull.hpp.  out: {lo0 P0, lo0 P1, lo1 P0, lo1 P1, hi0 P0, hi0 P1, hi1 P0, hi1 P1}.
 template <typename T>
@@ -109,15 +70,10 @@ __device__ void raster_cull_coefs(const T v[6], float M, int H, int W, Span sp, 
 // Bin (b, c) of view b (rows [lo, lo + nview)): its ascending local face indices and count, or
 // nullptr when the bin overflowed its region -- then the caller walks all nview faces of the
 // view (entry e = local face e) and its exact span filter selects the same faces.
-// known_base: the bin's base when the caller knows it (-1: treat the bin as overflowed, i.e.
-// walk every face of the view -- e.g. the raster set binned as fine lists has no coarse bins),
-// else kUnknownBase (read here).
-constexpr int kUnknownBase = -2;
 __device__ __forceinline__ const int *bin_list(const BinBuffers &bb, int b, int c, int64_t lo,
-                                               int nview, int nbin, int &n,
-                                               int known_base = kUnknownBase) {
+                                               int nview, int nbin, int &n) {
   const int64_t bc = (int64_t)b * bb.g.nct() + c;
-  const int base = known_base != kUnknownBase ? known_base : bb.base[bc];
+  const int base = bb.base[bc];
   if (base < 0) {
     n = nview;
     return nullptr;
@@ -146,18 +102,10 @@ struct PrepOut;  // kd_prep.hpp
 // by the same three launches (blockIdx.z selects the set).  prep (nullable): the corners are
 // computed from the vertices by prepare_vertices' arithmetic in the count launch, which also
 // writes its outputs (prep->fvc / fvi / nrm; fs*.fvi must point at prep->fvi).
-// fine (nullable, fine->tab set): set 0 (the raster's) is written as fine lists by the count
-// (depths from fvz / prep) and gets no scan / scatter; set 1 alone is binned into ordered bins.
-template <typename T>
-struct FineIn {
-  FineLists fl;
-  const T *fvz;            // depth of corner j of face row i at fvz[i * fvz_fs + j * fvz_cs]
-  int64_t fvz_fs, fvz_cs;  // (prep: the camera-space depths prep.fvc[.., 2] are used instead)
-};
 template <typename T>
 hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSet<T> &fs1,
                       const BinBuffers &bb1, hipStream_t stream,
-                      const PrepOut<T> *prep = nullptr, const FineIn<T> *fine = nullptr);
+                      const PrepOut<T> *prep = nullptr);
 
 // Zeroes `bytes` (a multiple of 4) at p with a kernel, not a memset node (graph-capture safe).
 hipError_t zero_words(void *p, size_t bytes, hipStream_t stream);

@@ -162,7 +162,7 @@ int kd_debug_set(int flags) {
 }
 
 int kd_set_test_forms(int forms) {
-  if (forms & ~(KD_FORM_SPLIT_FWD | KD_FORM_SPLIT_BWD | KD_FORM_SOFT_SPLIT | KD_FORM_COARSE_RASTER))
+  if (forms & ~(KD_FORM_SPLIT_FWD | KD_FORM_SPLIT_BWD | KD_FORM_SOFT_SPLIT))
     return kd::set_error(KD_ERR_INVALID_ARGUMENT, "unknown launch form bits 0x%x", forms);
   kd::g_forms.store(forms);
   return KD_OK;

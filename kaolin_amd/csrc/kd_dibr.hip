@@ -35,12 +35,10 @@ static int dibr_ct0(int, int, int) {
 }
 
 size_t dibr_workspace_bytes(int B, int H, int W, int64_t F, int K, int esize) {
-  // sized for the smallest coarse tile (the most bins): covers every dibr_ct0 choice; the raster
-  // fine lists whenever the shape allows them (fp32 or not: the layout does not depend on dtype)
+  // sized for the smallest coarse tile (the most bins): covers every dibr_ct0 choice
   const int64_t N = (int64_t)B * F;
   return bin_workspace_bytes(B, H, W, N, F, kTile) +
-         soft_pair_workspace_bytes(B, H, W, N, F, K, esize, kTile) +
-         fine_workspace_bytes(B, H, W, F);
+         soft_pair_workspace_bytes(B, H, W, N, F, K, esize, kTile);
 }
 
 template <typename T>
@@ -48,7 +46,6 @@ struct DibrBuffers {
   BinBuffers rbb;      // raster bins (+ cull coefficients)
   BinBuffers sbb;      // soft-mask bins
   SoftPairBuf<T> pb;   // soft-mask records
-  FineLists fl;        // raster fine lists (tab nullptr: the shape does not allow them)
 };
 
 // The pair buffers first: their place does not depend on the coarse tile (dibr_ct0), so a
@@ -62,7 +59,6 @@ static DibrBuffers<T> dibr_carve(void *ws, int B, int H, int W, int64_t F, int K
   d.pb = soft_pair_carve<T>(ws, off, B, H, W, K);
   d.rbb = bin_carve(ws, off, B, H, W, N, F, ct0);
   d.sbb = bin_carve(ws, off, B, H, W, N, F, ct0);
-  d.fl = fine_carve(ws, off, B, H, W, F);
   return d;
 }
 
@@ -159,20 +155,6 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   sa.iou_acc = iou.acc;
   sa.iou_B = B;
   const bool fusable = dibr_fwd_fusable(ra, sa);  // (fp32 and fp64)
-  // the raster fine lists (kd_binning.hpp FineLists): the one-launch fp32 forward's raster phase
-  // reads its tile's face records, written by the binning count; the raster set then has no
-  // coarse bins (no scan / scatter for it), so the tiles are dispatched in the soft set's order
-  const bool fine = std::is_same<T, float>::value && fusable && d.fl.tab != nullptr &&
-                    !(test_forms() & KD_FORM_COARSE_RASTER);
-  FineIn<T> fin{};
-  if (fine) {
-    fin.fl = d.fl;
-    fin.fvz = fvz;
-    fin.fvz_fs = fvz_fs;
-    fin.fvz_cs = fvz_cs;
-    ra.fine = d.fl;
-    ra.bb.order = d.sbb.order;
-  }
   // the one-launch fp32 forward's tile history (kd_set_tile_history): the previous same-shape
   // call's tile durations order this call's tiles (tile_order) and this call records its own --
   // only on the launch that writes it (the fused forward), so no other form reads a history
@@ -180,13 +162,12 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
     const int64_t nt = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     uint64_t tag = 1469598103934665603ull;  // FNV-1a over the shape and the hooks
     for (const int64_t x : {(int64_t)B, (int64_t)H, (int64_t)W, F, (int64_t)K,
-                            (int64_t)tile_split(), (int64_t)coarse_tile_hook(), (int64_t)fine})
+                            (int64_t)tile_split(), (int64_t)coarse_tile_hook()})
       tag = (tag ^ (uint64_t)x) * 1099511628211ull;
-    unsigned short *hist = tile_history(4 * (int64_t)B * nt, (long long)(tag >> 1), stream);
-    ra.bb.hist = hist;  // written by the forward, read by the dispatching set's tile_order
-    (fine ? d.sbb : d.rbb).hist = hist;
+    d.rbb.hist = tile_history(4 * (int64_t)B * nt, (long long)(tag >> 1), stream);
+    ra.bb.hist = d.rbb.hist;
   }
-  hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream, prep, fine ? &fin : nullptr);
+  hipError_t e = bin_faces2<T>(rfs, d.rbb, sfs, d.sbb, stream, prep);
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "binning: %s", hipGetErrorString(e));
   int rc = KD_OK;
   bool done = false;

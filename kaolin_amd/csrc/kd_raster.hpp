@@ -18,8 +18,6 @@ struct RasterFwdArgs {
   T *interp;
   int64_t *face_idx;
   T *weights;
-  FineLists fine;      // fine.tab set (fp32 one-launch forward): the raster phase reads its tile's
-                       // face records (kd_binning.hpp) instead of walking bb's coarse bin
 };
 
 // The face -> vertex step of the backward fused into the DIB-R backward: a

@@ -338,94 +338,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     }
     if (total) test_batch(total);
   };
-  // the fine walk (a.fine, fp32): the tile's row of per-chunk record groups, then its records in
-  // batches of kCap -- staged straight from the contiguous records (no coarse-bin walk, no span
-  // filter, no gathers).  false: a chunk of the row overflowed its segment (nothing staged yet)
-  auto fine_walk = [&]() -> bool {
-    const FineLists &fl = a.fine;
-    const int tid = threadIdx.x;
-    const int *row = fl.tab + ((int64_t)b * fl.nft + tl) * fl.nchunk;
-    constexpr int kE = kMaxFineChunks / kBlock;  // row entries (chunks tid * kE + e) per thread
-    const RasterRec *vrec = fl.rec + (int64_t)b * fl.nchunk * fl.chunk * kRecPerFace;
-    int *s_src = reinterpret_cast<int *>(&s_pair[0][0]);  // (free between rounds: 2 KB >= 1 KB)
-    for (int q0 = 0;; q0 += kCap) {
-      // the row is read again per batch (cache hits) so that nothing of it stays live across
-      // the rounds' registers; its runs give this batch's record indices (within the view)
-      int total;
-      {
-        int ecnt[kE], eoff[kE];
-        int sum = 0;
-        bool ovf = false;
-#pragma unroll
-        for (int e = 0; e < kE; ++e) {
-          const int j = tid * kE + e;
-          const int x = j < fl.nchunk ? row[j] : 0;
-          const int c = x & 0xffff;
-          ovf = ovf || c == kFineOvf;
-          ecnt[e] = c == kFineOvf ? 0 : c;
-          eoff[e] = (int)((unsigned)x >> 16);
-          sum += ecnt[e];
-        }
-        if (q0 == 0 && __syncthreads_or(ovf)) return false;
-        int run = wg_exclusive_scan(sum, L.cnt, total);
-        if (q0 >= total) break;  // (workgroup-uniform)
-        const int nb = min(kCap, total - q0);
-#pragma unroll
-        for (int e = 0; e < kE; ++e) {
-          const int a0 = max(run, q0), a1 = min(run + ecnt[e], q0 + nb);
-          const int sb = (tid * kE + e) * fl.chunk * kRecPerFace + eoff[e] - run;
-          for (int i = a0; i < a1; ++i) s_src[i - q0] = sb + i;
-          run += ecnt[e];
-        }
-      }
-      const int nb = min(kCap, total - q0);
-      __syncthreads();
-      if (tid < nb) {
-        const RasterRec r = vrec[s_src[tid]];
-        L.f[tid] = __float_as_int(r.g2.y);
-        PSpan ps;
-        ps.lo = __float_as_uint(r.g2.z);
-        ps.hi = __float_as_uint(r.g2.w);
-        L.span[tid] = unpack_span(ps);
-        s_geo[0][tid] = r.g0.x;
-        s_geo[1][tid] = r.g0.y;
-        s_geo[2][tid] = r.g0.z;
-        s_geo[3][tid] = r.g0.w;
-        s_geo[4][tid] = r.g1.x;
-        s_geo[5][tid] = r.g1.y;
-        s_geo[6][tid] = r.g1.z;
-        s_geo[7][tid] = r.g1.w;
-        s_geo[8][tid] = r.g2.x;
-        if constexpr (!kF64) {
-          s_cull[0][tid] = r.cl;
-          s_cull[1][tid] = r.ch;
-        }
-      }
-      __syncthreads();
-      int nsub = 0;  // this wave's sub-list (tile_rounds' flush)
-      for (int k0 = 0; k0 < nb; k0 += kWave) {
-        const int k = k0 + lane;
-        const bool ok =
-            t.wave_live && k < nb && span_overlaps(L.span[k], t.SX0, t.SX1, t.SY0, t.SY1);
-        const uint64_t m = __ballot(ok);
-        if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
-        nsub += __popcll(m);
-      }
-      if (lane == 0) L.nsub[w] = nsub;
-      __syncthreads();
-      if (!ablate(fs.dbg, 4)) round(nsub, nb);
-      __syncthreads();
-    }
-    return true;
-  };
-  bool walked = false;
-  if constexpr (!kF64) walked = a.fine.tab && fine_walk();
-  if (!walked) {
-    // fine lists without coarse raster bins (an overflowed row): every face of the view, span-
-    // filtered (bin_list's overflow walk)
-    if (a.fine.tab) t.bbase = -1;
-    tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
-  }
+  tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
   if (CLK && KD_DIAG && clk && threadIdx.x == 0) {
     const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
     clk[slot] = wall_clock64();
@@ -469,8 +382,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     const BinGeom &g = a.bb.g;
     const int ct = (t.py >> g.sh) * g.nctx + (t.px >> g.sh);
     int n;
-    // (fine lists: no coarse raster bins -- every face of the view, in order)
-    const int *bin = bin_list(a.bb, b, ct, lo, (int)(hi - lo), -1, n, a.fine.tab ? -1 : kUnknownBase);
+    const int *bin = bin_list(a.bb, b, ct, lo, (int)(hi - lo), -1, n);
     T max_z0 = (T)-INFINITY;
     for (int e = 0; e < n; ++e) {
       const int f = bin ? bin[e] : e;

@@ -29,8 +29,6 @@ struct TileGeom {
   int px, py;              // this lane's pixel
   bool inimg, wave_live;
   int nbin;                // faces in the tile's coarse bin when known (tile order), else -1
-  int bbase;               // its base when known (-1: walk every face of the view), else
-                           // kUnknownBase
   // face filter boxes of tile_rounds (default: the tile and the wave's sub-tile); a caller whose
   // pixels do not all need faces may shrink them to the pixels that do (wave_live = false when
   // the wave has none)
@@ -92,7 +90,6 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
   t.inimg = t.px < W && t.py < H;
   t.wave_live = t.WX0 < W && t.WY0 < H;
   t.nbin = -1;
-  t.bbase = kUnknownBase;
   t.FX0 = t.X0;
   t.FX1 = t.X1;
   t.FY0 = t.Y0;
@@ -137,7 +134,6 @@ __device__ __forceinline__ TileGeom tile_geom_part(int H, int W, int tile, int p
   t.inimg = t.px < W && t.py < H;
   t.wave_live = t.WX0 < W && t.WY0 < H;
   t.nbin = -1;
-  t.bbase = kUnknownBase;
   t.FX0 = t.X0;
   t.FX1 = t.X1;
   t.FY0 = t.Y0;
@@ -200,14 +196,6 @@ __device__ __forceinline__ PSpan pack_span(Span s) {
   p.hi = (uint32_t)(uint16_t)s.y0 | ((uint32_t)(uint16_t)s.y1 << 16);
   return p;
 }
-__device__ __forceinline__ Span unpack_span(PSpan p) {
-  Span s;
-  s.x0 = (short)(p.lo & 0xffff);
-  s.x1 = (short)(p.lo >> 16);
-  s.y0 = (short)(p.hi & 0xffff);
-  s.y1 = (short)(p.hi >> 16);
-  return s;
-}
 __device__ __forceinline__ bool pspan_has(PSpan p, int x, int y) {
   const int x0 = (int)(int16_t)(p.lo & 0xffff), x1 = (int)(int16_t)(p.lo >> 16);
   const int y0 = (int)(int16_t)(p.hi & 0xffff), y1 = (int)(int16_t)(p.hi >> 16);
@@ -252,7 +240,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
   int n;
-  const int *bin = bin_list(bb, b, ct, lo, nview, t.nbin, n, t.bbase);
+  const int *bin = bin_list(bb, b, ct, lo, nview, t.nbin, n);
   int cnt = 0;
   // kPrefetch chunks of bin entries and their spans are loaded up front (two dependent
   // round trips per kPrefetch * 256 entries instead of per 256)
