@@ -61,13 +61,17 @@ __device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], con
   const T dw2[6] = {-(dw2dm + dw2dn + dw2ds), -(dw2dp + dw2dq + dw2dt), dw2dm, dw2dp, dw2dn,
                     dw2dq};
   const T kk = k3 * k3;
+  // fp32: one hardware reciprocal (1 ulp) for the D quotients g_d / k3^2 -- gradient accuracy, not
+  // bit-exactness, is the bar here (the reference's own float atomics reorder these sums)
+  T rkk = (T)0;
+  if constexpr (sizeof(T) == 4) rkk = __builtin_amdgcn_rcpf(kk);
 #pragma unroll
   for (int j = 0; j < 6; ++j) out[j] = (T)0;
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
     if (d < D) {
       const T c0 = c[d], c1 = c[D + d], c2 = c[2 * D + d];
-      const T dldI = gd[d] / kk;
+      const T dldI = sizeof(T) == 4 ? gd[d] * rkk : gd[d] / kk;
 #pragma unroll
       for (int j = 0; j < 6; ++j) out[j] += dldI * ((c1 - c0) * dw1[j] + (c2 - c0) * dw2[j]);
     }

@@ -139,11 +139,8 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     if (lane == 0) s_nan[kw] = 0ull;
     if (uncm && lane == 0 && t.role == 0) uncm[t.sub] = 0ull;
   }
-  // this wave's row centres relative to its first row
+  // this wave's first row centre (pass A: row r's centre relative to it)
   const float ysub = px_cy(M, H, t.WY0);
-  float drow[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) drow[r] = px_cy(M, H, t.WY0 + r) - ysub;
   constexpr float kSlack = 1.f / 64.f;
 
   auto stage = [&](int k, int64_t fi) {
@@ -274,15 +271,15 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
           ch = s_cull[1][k];
         }
         const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float d = drow[r] + dref;
+        // only the rows of the face's own span (a lane's loop: the wave runs the longest span,
+        // not all 8 rows); drow[r] is recomputed from sy (px_cy's first factor: the same bits)
+        for (int r = ry0; r <= ry1; ++r) {
+          const float d = (sy * (float)(H - 2 * (oy + r) - 1) - ysb) + dref;
           const float plo = fmaxf(fmaf(cl.y, d, l0), fmaf(cl.w, d, l2)) - kSlack;
           const float phi = fminf(fmaf(ch.y, d, h0), fmaf(ch.w, d, h2)) + kSlack;
           const int xs = max((int)ceilf(__builtin_amdgcn_fmed3f(plo, -1.f, 9.f)), rx0);
           const int xe = min((int)floorf(__builtin_amdgcn_fmed3f(phi, -1.f, 9.f)), rx1);
-          const bool row = r >= ry0 && r <= ry1 && xs <= xe;
-          const uint32_t bits = row ? ((2u << xe) - (1u << xs)) : 0u;
+          const uint32_t bits = xs <= xe ? ((2u << xe) - (1u << xs)) : 0u;
           fm |= (uint64_t)bits << (8 * r);
         }
       }

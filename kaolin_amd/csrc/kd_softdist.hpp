@@ -57,8 +57,10 @@ __host__ __device__ __forceinline__ float quo_f(double n, double d, double r) {
   memcpy(&b, &q, sizeof b);
 #endif
   const unsigned lo = (unsigned)b & 0x1fffffffu;
-  const double aq = fabs(q);
-  const bool safe = (lo - (0x10000000u - 32u)) > 64u && aq >= 0x1p-120 && aq < 0x1p120;
+  // 2^-120 <= |q| < 2^120 <=> its biased exponent lies in [1023 - 120, 1023 + 120) (zero, NaN,
+  // inf and subnormals fall outside), one unsigned compare
+  const unsigned ex = (unsigned)(b >> 52) & 0x7ffu;
+  const bool safe = (lo - (0x10000000u - 32u)) > 64u && ex - (1023u - 120u) < 240u;
   float res = (float)q;
   if (__builtin_expect(!safe, 0)) {
 #ifdef __HIP_DEVICE_COMPILE__

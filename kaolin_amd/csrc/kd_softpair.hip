@@ -416,17 +416,26 @@ __device__ __forceinline__ void iou_tile_terms(const SoftArgs<T> &a, int b, int 
 
 // Side job of the fused forward launches: the backward's gradient buffers, zeroed grid-stride
 // (coalesced) by every workgroup of the grid -- also by those without a tile.
+// (16-byte stores where the buffer is 16-byte aligned, element stores for the rest)
+template <typename T>
+__device__ __forceinline__ void zero_range(T *p, int64_t n, int64_t gtid, int64_t gstride) {
+  if (!p || n <= 0) return;
+  int64_t done = 0;
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {
+    constexpr int E = 16 / (int)sizeof(T);
+    const int64_t nv = n / E;
+    float4 *q = reinterpret_cast<float4 *>(p);
+    for (int64_t i = gtid; i < nv; i += gstride) q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    done = nv * E;
+  }
+  for (int64_t i = done + gtid; i < n; i += gstride) p[i] = (T)0;
+}
 template <typename T>
 __device__ __forceinline__ void zero_side_job(const SoftArgs<T> &a) {
-  const int64_t nz = a.nzero0 + a.nzero1;
-  const int64_t nblk = (int64_t)gridDim.x * gridDim.y;
-  for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x; i < nz;
-       i += nblk * kBlock) {
-    if (i < a.nzero0)
-      a.zero0[i] = (T)0;
-    else
-      a.zero1[i - a.nzero0] = (T)0;
-  }
+  const int64_t gstride = (int64_t)gridDim.x * gridDim.y * kBlock;
+  const int64_t gtid = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kBlock + threadIdx.x;
+  zero_range<T>(a.zero0, a.nzero0, gtid, gstride);
+  zero_range<T>(a.zero1, a.nzero1, gtid, gstride);
 }
 
 template <bool FUSED>
