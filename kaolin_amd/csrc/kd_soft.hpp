@@ -197,6 +197,90 @@ struct SoftCoef {
   T h[4];
 };
 
+// Backward coefficients h_j of one pair (kd_softpair.hip, file comment); the geometric factors are the
+// reference's expressions (dibr_soft_mask_cuda.cu:288-343) in T.
+template <typename T>
+__device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et, T prob, float M,
+                                               T h[4]) {
+  if constexpr (std::is_same<T, float>::value) {
+    {
+      // fp32 with hardware reciprocals (1 ulp): the gradient's accuracy is that of the
+      // reference's fp32 terms, whose double divisions end in float roundings too
+      const float s = prob * __builtin_amdgcn_rcpf((1.f - prob + 1e-7f) * M);
+      if (et >= 3) {
+        const int ps = (et - 3) * 2;
+        h[0] = s * (2.f * (v[ps] - x0));
+        h[1] = s * (2.f * (v[ps + 1] - y0));
+        h[2] = 0.f;
+        h[3] = 0.f;
+      } else {
+        const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
+        const float x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
+        const float A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+        const float up = A * x0 + Bc * y0 + C;
+        const float rd = __builtin_amdgcn_rcpf(A * A + Bc * Bc + 1e-7f);
+        const float dissquare = up * up * rd;
+        const float dzdA = 2.f * (x0 * up - dissquare * A) * rd;
+        const float dzdB = 2.f * (y0 * up - dissquare * Bc) * rd;
+        const float dzdC = 2.f * up * rd;
+        h[0] = s * (dzdB - y2 * dzdC);
+        h[1] = s * (x2 * dzdC - dzdA);
+        h[2] = s * (y1 * dzdC - dzdB);
+        h[3] = s * (dzdA - x1 * dzdC);
+      }
+      return;
+    }
+  }
+  // the backward's coefficients need gradient accuracy, not bit-exactness: reciprocals
+  const double s = (double)prob * (1.0 / ((1.0 - (double)prob + KD_SOFT_EPS) * (double)M));
+  if (et >= 3) {
+    const int ps = (et - 3) * 2;
+    h[0] = (T)(s * (double)((T)2 * (v[ps] - x0)));
+    h[1] = (T)(s * (double)((T)2 * (v[ps + 1] - y0)));
+    h[2] = (T)0;
+    h[3] = (T)0;
+  } else {
+    const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
+    const T x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
+    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
+    const T up = A * x0 + Bc * y0 + C;
+    const T down = A * A + Bc * Bc;
+    const double rd = 1.0 / ((double)down + KD_SOFT_EPS);
+    const T dissquare = (T)((double)(up * up) * rd);
+    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) * rd);
+    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) * rd);
+    const T dzdC = (T)((double)((T)2 * up) * rd);
+    h[0] = (T)(s * (double)(dzdB - y2 * dzdC));
+    h[1] = (T)(s * (double)(x2 * dzdC - dzdA));
+    h[2] = (T)(s * (double)(y1 * dzdC - dzdB));
+    h[3] = (T)(s * (double)(dzdA - x1 * dzdC));
+  }
+}
+
+// Adds one pair's contribution s_p * h_j to the register sums g[6] of its face's corners.
+template <typename T>
+__device__ __forceinline__ void soft_add_pair(T g[6], int et, double sp, const SoftCoef<T> &c) {
+  const int ps = et >= 3 ? (et - 3) * 2 : et * 2;
+  const int ps2 = et >= 3 ? -8 : ((et + 1) % 3) * 2;  // vertex types touch one corner only
+  T v0, v1, v2, v3;
+  if (std::is_same<T, float>::value) {
+    const T spf = (T)sp;
+    v0 = spf * c.h[0];
+    v1 = spf * c.h[1];
+    v2 = spf * c.h[2];
+    v3 = spf * c.h[3];
+  } else {
+    v0 = (T)(sp * (double)c.h[0]);
+    v1 = (T)(sp * (double)c.h[1]);
+    v2 = (T)(sp * (double)c.h[2]);
+    v3 = (T)(sp * (double)c.h[3]);
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i)
+    g[i] += i == ps ? v0 : i == ps + 1 ? v1 : i == ps2 ? v2 : i == ps2 + 1 ? v3 : (T)0;
+}
+
+
 constexpr int kFuseSlots = 32;           // knum bound of the one-launch soft mask (LDS slot table)
 constexpr int kPoolPairsPerPixel = kFuseSlots;  // record pool: min(knum, 32) records per pixel
 

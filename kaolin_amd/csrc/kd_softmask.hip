@@ -162,15 +162,18 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_atomic(
 }
 
 // The same backward over given close lists, per 16x16 tile of pixels (grid-stride): the tile's
-// uncovered pixels whose first slot holds a face are compacted in LDS; each half-wave (K <= 32)
-// or wave (K > 32, 64 slots at a time) takes one listed pixel's row of K slots -- consecutive
-// lanes, consecutive elements -- and its lanes up to the row's first -1 (a ballot: the
-// reference's loop stops there, dibr_soft_mask_cuda.cu:273-276) compute their pair's terms.  The
-// terms are summed per face in an LDS hash table (a face is close to many pixels of a tile) and
-// each (tile, face, coordinate) sum goes out with one float atomic: the per-pair atomics of the
-// lane-per-pixel form (10 M at C3, ~85 % of its time) contended on the faces' lines.  A pair
-// whose face finds no slot (a full table) adds its terms directly.
-constexpr int kListHash = 1024;  // LDS face slots per tile
+// uncovered pixels whose first slot holds a face are compacted in LDS with their factor
+// s_p = -sigmainv * dL/dsoft * (1 - soft); each half-wave (K <= 32) or wave (K > 32, 64 slots at
+// a time) takes one listed pixel's row of K slots -- consecutive lanes, consecutive elements,
+// the slot's face, probability and type loaded together -- and its lanes up to the row's first
+// -1 (a ballot: the reference's loop stops there, dibr_soft_mask_cuda.cu:273-276) add their
+// pair's terms s_p * h_j (kd_soft.hpp soft_pair_coef: the coefficients of the fused path, the
+// reference's factors, dibr_soft_mask_cuda.cu:281-348, up to rounding).  The terms are summed per
+// face in an LDS hash table (a face is close to many pixels of a tile) and each (tile, face,
+// coordinate) sum goes out with one float atomic; a pair whose face finds no slot (a full table)
+// adds its terms directly.  Load chain per tile: face_idx / grad / soft -> the first slot ->
+// the rows -> the faces' corners.  Small LDS (11 KB fp32), so several tiles per CU hide it.
+constexpr int kListHash = 256;  // LDS face slots per tile
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
@@ -178,7 +181,8 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
     const T *__restrict__ soft, const int64_t *__restrict__ face_idx, const T *__restrict__ prob,
     const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
     const T *__restrict__ fvi, float sigmainv, float M, T *grad_fvi, int dbg) {
-  __shared__ int64_t s_pix[kBlock];
+  __shared__ int64_t s_pix[kBlock];  // listed pixel: image index | tile pixel << 48
+  __shared__ double s_sp[kBlock];    // its s_p
   __shared__ int s_cnt[kBlock / kWave];
   __shared__ int s_key[kListHash];
   __shared__ T s_acc[kListHash][6];
@@ -190,20 +194,21 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
 #pragma unroll
     for (int c = 0; c < 6; ++c) s_acc[i][c] = (T)0;
   }
-  auto pair = [&](int64_t p, int b, int x, int h, int s) {  // one (pixel, slot) entry, face >= 0
-    const int64_t e = p * K + s;
-    const int64_t sf = (int64_t)b * F + cidx[e];
+  // one (pixel, slot) pair with a face (c >= 0): its terms into the tile's face sums
+  auto pair = [&](int b, int x, int h, int64_t c, T pr, int et, double sp) {
+    const int64_t sf = (int64_t)b * F + c;
     T v[6];
 #pragma unroll
-    for (int c = 0; c < 6; ++c) v[c] = fvi[sf * 6 + c];
+    for (int q = 0; q < 6; ++q) v[q] = fvi[sf * 6 + q];
+    SoftCoef<T> cf;
+    soft_pair_coef<T>((T)px_cx(M, W, x), (T)px_cy(M, H, h), v, et, pr, M, cf.h);
     T g[6] = {0, 0, 0, 0, 0, 0};
-    soft_bwd_terms<T>((T)px_cx(M, W, x), (T)px_cy(M, H, h), v, (int)ctype[e] - 1, prob[e],
-                      grad_soft[p], soft[p], sigmainv, M, g);
+    soft_add_pair<T>(g, et, sp, cf);
     if (ablate(dbg, 1 << 22)) {  // diagnostics: no accumulation (one plain store keeps the math)
       if (g[0] + g[1] + g[2] + g[3] + g[4] + g[5] == (T)12345) grad_fvi[0] = (T)1;
       return;
     }
-    unsigned u = ((unsigned)sf * 2654435761u) >> 22;  // 10 bits
+    unsigned u = ((unsigned)sf * 2654435761u) >> 24;  // 8 bits
     int slot = -1;
     for (int probe = 0; probe < 32; ++probe) {
       const int old = atomicCAS(&s_key[u], -1, (int)sf);
@@ -214,12 +219,12 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
       u = (u + 1) & (kListHash - 1);
     }
 #pragma unroll
-    for (int c = 0; c < 6; ++c)
-      if (g[c] != (T)0) {
+    for (int q = 0; q < 6; ++q)
+      if (g[q] != (T)0) {
         if (slot >= 0)
-          atomicAdd(&s_acc[slot][c], g[c]);
+          atomicAdd(&s_acc[slot][q], g[q]);
         else
-          atomicAdd(grad_fvi + sf * 6 + c, g[c]);
+          atomicAdd(grad_fvi + sf * 6 + q, g[q]);
       }
   };
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -229,37 +234,63 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
     const int px = X0 + (tid & 15), py = Y0 + (tid >> 4);
     const bool in = px < W && py < H;
     const int64_t p = ((int64_t)b * H + py) * W + px;
-    const bool live = in && face_idx[p] < 0 && cidx[p * K] >= 0;
+    int64_t fi = 0;
+    T gsv = (T)0, sov = (T)0;
+    if (in) {  // (independent loads, issued together)
+      fi = face_idx[p];
+      gsv = grad_soft[p];
+      sov = soft[p];
+    }
+    const bool live = in && fi < 0 && cidx[p * K] >= 0;
     int n;
     const int pos = wg_compact(live, s_cnt, n);  // (its barriers also order the table reset)
-    if (live) s_pix[pos] = ((int64_t)tid << 48) | p;  // tile pixel + image pixel
+    if (live) {
+      s_pix[pos] = ((int64_t)tid << 48) | p;  // tile pixel + image pixel
+      s_sp[pos] = -(double)sigmainv * (double)gsv * (1.0 - (double)sov);
+    }
     __syncthreads();
-    auto run = [&](int i, int s) {  // pixel i of the list, slot s
-      const int64_t ent = s_pix[i];
-      const int q = (int)(ent >> 48);
-      pair(ent & 0xffffffffffffll, b, X0 + (q & 15), Y0 + (q >> 4), s);
-    };
     if (K <= 32) {  // two rows per wave step (half-waves), rows dealt to the waves in turn
       const int half = lane >> 5, s = lane & 31;
       for (int i0 = 2 * w; i0 < n; i0 += 2 * (kBlock / kWave)) {
         const int i = i0 + half;
-        const int64_t pp = i < n ? (s_pix[i] & 0xffffffffffffll) : 0;
         const bool in2 = i < n && s < K;
-        const bool stop = !in2 || cidx[pp * K + s] < 0;
-        const uint64_t sm = __ballot(stop);
+        const int64_t ent = i < n ? s_pix[i] : 0;
+        const int64_t e = (ent & 0xffffffffffffll) * K + s;
+        int64_t c = -1;
+        T pr = (T)0;
+        int ty = 0;
+        if (in2) {  // the slot's face, probability and type together
+          c = cidx[e];
+          pr = prob[e];
+          ty = ctype[e];
+        }
+        const uint64_t sm = __ballot(!in2 || c < 0);
         const uint32_t hm = (uint32_t)(sm >> (32 * half));  // this half's stops
         const int first = hm ? __builtin_ctz(hm) : 32;
-        if (in2 && s < first) run(i, s);
+        if (in2 && s < first) {
+          const int q = (int)(ent >> 48);
+          pair(b, X0 + (q & 15), Y0 + (q >> 4), c, pr, ty - 1, s_sp[i]);
+        }
       }
     } else {  // one row per wave, 64 slots at a time until its first -1
       for (int i = w; i < n; i += kBlock / kWave) {
-        const int64_t pp = s_pix[i] & 0xffffffffffffll;
+        const int64_t ent = s_pix[i];
+        const int64_t pp = ent & 0xffffffffffffll;
+        const int q = (int)(ent >> 48);
+        const double sp = s_sp[i];
         for (int s0 = 0; s0 < K; s0 += kWave) {
           const int s = s0 + lane;
-          const bool stop = s >= K || cidx[pp * K + s] < 0;
-          const uint64_t sm = __ballot(stop);
+          int64_t c = -1;
+          T pr = (T)0;
+          int ty = 0;
+          if (s < K) {
+            c = cidx[pp * K + s];
+            pr = prob[pp * K + s];
+            ty = ctype[pp * K + s];
+          }
+          const uint64_t sm = __ballot(c < 0);
           const int first = sm ? __builtin_ctzll(sm) : kWave;
-          if (lane < first) run(i, s);
+          if (lane < first) pair(b, X0 + (q & 15), Y0 + (q >> 4), c, pr, ty - 1, sp);
           if (sm) break;
         }
       }

@@ -109,66 +109,6 @@ __device__ __forceinline__ void tile_pixel(int tx, int ty, int q, int &px, int &
   py = ty * kTile + (w >> 1) * 8 + (l >> 3);
 }
 
-// Backward coefficients h_j of one pair (see the file comment); the geometric factors are the
-// reference's expressions (dibr_soft_mask_cuda.cu:288-343) in T.
-template <typename T>
-__device__ __forceinline__ void soft_pair_coef(T x0, T y0, const T v[6], int et, T prob, float M,
-                                               T h[4]) {
-  if constexpr (std::is_same<T, float>::value) {
-    {
-      // fp32 with hardware reciprocals (1 ulp): the gradient's accuracy is that of the
-      // reference's fp32 terms, whose double divisions end in float roundings too
-      const float s = prob * __builtin_amdgcn_rcpf((1.f - prob + 1e-7f) * M);
-      if (et >= 3) {
-        const int ps = (et - 3) * 2;
-        h[0] = s * (2.f * (v[ps] - x0));
-        h[1] = s * (2.f * (v[ps + 1] - y0));
-        h[2] = 0.f;
-        h[3] = 0.f;
-      } else {
-        const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
-        const float x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
-        const float A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-        const float up = A * x0 + Bc * y0 + C;
-        const float rd = __builtin_amdgcn_rcpf(A * A + Bc * Bc + 1e-7f);
-        const float dissquare = up * up * rd;
-        const float dzdA = 2.f * (x0 * up - dissquare * A) * rd;
-        const float dzdB = 2.f * (y0 * up - dissquare * Bc) * rd;
-        const float dzdC = 2.f * up * rd;
-        h[0] = s * (dzdB - y2 * dzdC);
-        h[1] = s * (x2 * dzdC - dzdA);
-        h[2] = s * (y1 * dzdC - dzdB);
-        h[3] = s * (dzdA - x1 * dzdC);
-      }
-      return;
-    }
-  }
-  // the backward's coefficients need gradient accuracy, not bit-exactness: reciprocals
-  const double s = (double)prob * (1.0 / ((1.0 - (double)prob + KD_SOFT_EPS) * (double)M));
-  if (et >= 3) {
-    const int ps = (et - 3) * 2;
-    h[0] = (T)(s * (double)((T)2 * (v[ps] - x0)));
-    h[1] = (T)(s * (double)((T)2 * (v[ps + 1] - y0)));
-    h[2] = (T)0;
-    h[3] = (T)0;
-  } else {
-    const int ps = et * 2, ps2 = ((et + 1) % 3) * 2;
-    const T x1 = v[ps], y1 = v[ps + 1], x2 = v[ps2], y2 = v[ps2 + 1];
-    const T A = y2 - y1, Bc = x1 - x2, C = x2 * y1 - x1 * y2;
-    const T up = A * x0 + Bc * y0 + C;
-    const T down = A * A + Bc * Bc;
-    const double rd = 1.0 / ((double)down + KD_SOFT_EPS);
-    const T dissquare = (T)((double)(up * up) * rd);
-    const T dzdA = (T)((double)((T)2 * (x0 * up - dissquare * A)) * rd);
-    const T dzdB = (T)((double)((T)2 * (y0 * up - dissquare * Bc)) * rd);
-    const T dzdC = (T)((double)((T)2 * up) * rd);
-    h[0] = (T)(s * (double)(dzdB - y2 * dzdC));
-    h[1] = (T)(s * (double)(x2 * dzdC - dzdA));
-    h[2] = (T)(s * (double)(y1 * dzdC - dzdB));
-    h[3] = (T)(s * (double)(dzdA - x1 * dzdC));
-  }
-}
-
 // ------------------------------------------------------------------------------------------
 // pass A: (pixel, slot, face) records per tile
 // ------------------------------------------------------------------------------------------
@@ -949,13 +889,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_lists(SoftArgs<T> a, SoftPairB
   int *s_np = (int *)(s_raw + (sizeof(T) + sizeof(int)) * R * HP);
   const int K = a.K, H = a.fs.H, W = a.fs.W;
   const int tid = threadIdx.x;
-  const int64_t nz = a.nzero0 + a.nzero1;  // side job: zero fills (grid-stride, coalesced)
-  for (int64_t i = (int64_t)blockIdx.x * kBlock + tid; i < nz; i += (int64_t)gridDim.x * kBlock) {
-    if (i < a.nzero0)
-      a.zero0[i] = (T)0;
-    else
-      a.zero1[i - a.nzero0] = (T)0;
-  }
+  zero_side_job(a);  // side job: the backward's zero fills
   // half tiles: rows 0-7 (tile pixels q < 128) and rows 8-15 of a tile, so that the tables are
   // half the size and twice the workgroups fit a CU (the loop is store / load latency bound)
   const int64_t nht = 2 * (int64_t)a.fs.B * pb.ntiles;
@@ -1020,10 +954,11 @@ __global__ __launch_bounds__(kBlock) void kd_soft_lists(SoftArgs<T> a, SoftPairB
       // pixel (r, i) of the half tile -> its table row (tile_geom's q minus q0)
       auto hq = [](int r, int i) { return ((i >> 3) * kWave) + (r & 7) * 8 + (i & 7); };
       if ((K & 1) == 0) {  // slot pairs: every pair starts at an even element
+        // a row's nx x S2 slot pairs (<= 16 x 16 = 256) are one pass of the workgroup: thread
+        // tid takes pixel i, pair s of every row (no divisions in the loop)
         const int S2 = S >> 1, per_row = nx * S2;
-        for (int e = tid; e < ny * per_row; e += kBlock) {
-          const int r = e / per_row, rem = e - r * per_row;
-          const int i = rem / S2, s = 2 * (rem - i * S2);
+        const int i = tid / S2, s = 2 * (tid - i * S2);
+        for (int r = 0; tid < per_row && r < ny; ++r) {
           const int q = hq(r, i);
           const int64_t o = (((int64_t)b * H + Y0 + r) * W + X0 + i) * K + s0 + s;
           T p0, p1;
@@ -1092,29 +1027,6 @@ __global__ __launch_bounds__(kBlock) void kd_soft_pair_math(SoftArgs<T> a, SoftP
 // ------------------------------------------------------------------------------------------
 // backward
 // ------------------------------------------------------------------------------------------
-// Adds one pair's contribution s_p * h_j to the register sums g[6] of its face's corners.
-template <typename T>
-__device__ __forceinline__ void soft_add_pair(T g[6], int et, double sp, const SoftCoef<T> &c) {
-  const int ps = et >= 3 ? (et - 3) * 2 : et * 2;
-  const int ps2 = et >= 3 ? -8 : ((et + 1) % 3) * 2;  // vertex types touch one corner only
-  T v0, v1, v2, v3;
-  if (std::is_same<T, float>::value) {
-    const T spf = (T)sp;
-    v0 = spf * c.h[0];
-    v1 = spf * c.h[1];
-    v2 = spf * c.h[2];
-    v3 = spf * c.h[3];
-  } else {
-    v0 = (T)(sp * (double)c.h[0]);
-    v1 = (T)(sp * (double)c.h[1]);
-    v2 = (T)(sp * (double)c.h[2]);
-    v3 = (T)(sp * (double)c.h[3]);
-  }
-#pragma unroll
-  for (int i = 0; i < 6; ++i)
-    g[i] += i == ps ? v0 : i == ps + 1 ? v1 : i == ps2 ? v2 : i == ps2 + 1 ? v3 : (T)0;
-}
-
 // Flat over the (tile, 256-record chunk) items, one record per thread: s_p * h_j expanded to
 // the face's 6 corner coordinates, summed over the record's run of equal faces inside its wave
 // by a segmented inclusive scan (records are face-major runs; no LDS), and the run's last lane
