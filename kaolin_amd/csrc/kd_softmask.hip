@@ -162,7 +162,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_atomic(
 }
 
 // The same backward over given close lists, per 16x16 tile of pixels (grid-stride): the tile's
-// uncovered pixels whose first slot holds a face are compacted in LDS with their factor
+// uncovered pixels whose terms can be nonzero are compacted in LDS with their factor
 // s_p = -sigmainv * dL/dsoft * (1 - soft); each half-wave (K <= 32) or wave (K > 32, 64 slots at
 // a time) takes one listed pixel's row of K slots -- consecutive lanes, consecutive elements,
 // the slot's face, probability and type loaded together -- and its lanes up to the row's first
@@ -171,8 +171,8 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_atomic(
 // reference's factors, dibr_soft_mask_cuda.cu:281-348, up to rounding).  The terms are summed per
 // face in an LDS hash table (a face is close to many pixels of a tile) and each (tile, face,
 // coordinate) sum goes out with one float atomic; a pair whose face finds no slot (a full table)
-// adds its terms directly.  Load chain per tile: face_idx / grad / soft -> the first slot ->
-// the rows -> the faces' corners.  Small LDS (11 KB fp32), so several tiles per CU hide it.
+// adds its terms directly.  Load chain per tile: face_idx / grad / soft -> the rows -> the
+// faces' corners.  Small LDS (11 KB fp32), so several tiles per CU hide it.
 constexpr int kListHash = 256;  // LDS face slots per tile
 
 template <typename T>
@@ -241,7 +241,14 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
       gsv = grad_soft[p];
       sov = soft[p];
     }
-    const bool live = in && fi < 0 && cidx[p * K] >= 0;
+    // a listed pixel needs its rows read unless every term of its row is exactly zero: soft 0
+    // (every probability 0, e.g. no close face at all: most uncovered pixels), soft 1 (the
+    // factor 1 - soft) or a zero incoming gradient -- with both finite (a NaN or inf must reach
+    // the gradients as in the reference).  This replaces a read of each uncovered pixel's first
+    // slot (a cache line per pixel) before the compaction.
+    const bool zero_terms = (sov == (T)0 || sov == (T)1 || gsv == (T)0) && isfinite(sov) &&
+                            isfinite(gsv);
+    const bool live = in && fi < 0 && !zero_terms;
     int n;
     const int pos = wg_compact(live, s_cnt, n);  // (its barriers also order the table reset)
     if (live) {
