@@ -659,7 +659,8 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   }
   T sval = unc ? (T)0.0 : (T)1.0;  // this pixel's soft value (FUSED: the product below)
   if (t.inimg && owner) {
-    if (!FUSED) pb.npix[p] = my_kid;  // the split pipeline's reduce
+    // the split pipeline's reduce / the close-list writer (kd_soft_lists, also after FUSED)
+    if (!FUSED || a.prob) pb.npix[p] = my_kid;
     if (a.soft && !unc) a.soft[p] = (T)1.0;  // dibr_soft_mask_cuda.cu:69
     else if (a.soft && my_kid == 0) a.soft[p] = (T)0.0;
     if (a.last && my_kid < K) a.last[p] = -1;
@@ -1279,16 +1280,30 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   const FaceSet<T> &fs = a.fs;
   a.fs.dbg = debug_flags();
   a.fs.tbuf = debug_tile_buffer();
-  // one launch for the whole soft mask (the autograd path: no close-face lists)
-  const bool fused =
-      reduce && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
-      !(test_forms() & KD_FORM_SOFT_SPLIT);
+  // one launch for the whole soft mask (knum <= 32); with the close-face lists (the op form,
+  // dibr.py's SAVE_CLOSE_LISTS) the lists writer follows it, reading the records, types and
+  // probabilities the one launch left (no separate pair-math launch)
+  const bool fused = reduce && a.soft && !a.last && a.K <= kFuseSlots &&
+                     !(test_forms() & KD_FORM_SOFT_SPLIT);
   if (fused) {
-    ProfScope prof(K_SOFT_PAIRS, stream);
-    // 6 workgroups per CU (the 16 KB record-index table); 4 and 8 measured no faster
-    hipLaunchKernelGGL((kd_soft_pairs<T, true, 6>), dim3((unsigned)pb.ntiles, fs.B),
-                       dim3(kBlock), 0, stream, a, pb);
-    if (pool_may_overflow(a.K)) ovf_fwd_launch<T, true>(a, pb, stream);
+    {
+      ProfScope prof(K_SOFT_PAIRS, stream);
+      // 6 workgroups per CU (the 16 KB record-index table); 4 and 8 measured no faster
+      hipLaunchKernelGGL((kd_soft_pairs<T, true, 6>), dim3((unsigned)pb.ntiles, fs.B),
+                         dim3(kBlock), 0, stream, a, pb);
+    }
+    if (a.prob) {
+      // an overflowed tile: its soft mask and lists from the streaming walk (the split form)
+      if (pool_may_overflow(a.K)) ovf_fwd_launch<T, false>(a, pb, stream);
+      KD_CHECK_ARG(fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
+      SoftArgs<T> al = a;  // (the backward's zero fills were the one launch's side job)
+      al.nzero0 = al.nzero1 = 0;
+      const size_t dyn = ((sizeof(T) + sizeof(int)) * (kReduceSlots + 1) + sizeof(int)) * kBlock / 2;
+      ProfScope prof(K_SOFT_REDUCE, stream);
+      hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), dyn, stream, al, pb);
+    } else if (pool_may_overflow(a.K)) {
+      ovf_fwd_launch<T, true>(a, pb, stream);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft mask: %s", hipGetErrorString(e));
     return KD_OK;
