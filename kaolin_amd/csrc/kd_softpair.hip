@@ -936,7 +936,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_lists(SoftArgs<T> a, SoftPairB
         }
       }
       lds_barrier();
-      const int e_hi = min(np - s0, S);
+      const int e_hi = a.soft ? min(np - s0, S) : 0;  // (no soft: the one launch wrote it)
       for (int s = 0; s < e_hi; ++s) prod = (T)((double)prod * (1.0 - (double)s_val[tid][s]));
       // the pass's slots of the half tile's rows, in memory order
       auto value = [&](int q, int s, T &pv, int64_t &cv, uint8_t &tv) {
@@ -986,7 +986,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_lists(SoftArgs<T> a, SoftPairB
         }
       }
     }
-    if (np > 0) a.soft[p] = (T)(1.0 - (double)prod);
+    if (np > 0 && a.soft) a.soft[p] = (T)(1.0 - (double)prod);
   }
 }
 
@@ -1298,6 +1298,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
       KD_CHECK_ARG(fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
       SoftArgs<T> al = a;  // (the backward's zero fills were the one launch's side job)
       al.nzero0 = al.nzero1 = 0;
+      al.soft = nullptr;  // (and the soft mask)
       const size_t dyn = ((sizeof(T) + sizeof(int)) * (kReduceSlots + 1) + sizeof(int)) * kBlock / 2;
       ProfScope prof(K_SOFT_REDUCE, stream);
       hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), dyn, stream, al, pb);
