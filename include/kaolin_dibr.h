@@ -68,12 +68,10 @@ int kd_debug_buffer(void *device_ptr);
  * (the op forms, knum > 32, D > 3).  A test sets these bits to run dibr_rasterization through the
  * separate launches and compare.  Bits: KD_FORM_SPLIT_FWD raster then soft mask as two launches,
  * KD_FORM_SPLIT_BWD the two backwards as two launches, KD_FORM_SOFT_SPLIT the soft mask's pass A,
- * pair math and product as three launches (the K-list pipeline without the lists),
- * KD_FORM_DT_PIXEL deftet_sparse_render's per-pixel walk for every pixel (no cell-major walk). */
+ * pair math and product as three launches (the K-list pipeline without the lists). */
 #define KD_FORM_SPLIT_FWD 1
 #define KD_FORM_SPLIT_BWD 2
 #define KD_FORM_SOFT_SPLIT 4
-#define KD_FORM_DT_PIXEL 8
 int kd_set_test_forms(int forms);
 
 /* Workgroups per 16x16 tile of dibr_rasterization's fp32 forward (a test and tuning hook; 0 by
@@ -537,8 +535,7 @@ int kd_rast_interpolate_f64(int batch, int height, int width, int64_t num_faces,
  * kd_deftet_workspace_size.  The backward writes grad_fvi (B, F, 3, 2) and grad_feat
  * (B, F, 3, D) (NULL: skipped).
  * ------------------------------------------------------------------------------------------- */
-size_t kd_deftet_workspace_size(int batch, int64_t num_pixels, int64_t num_faces,
-                                int feat_dim, int double_precision);
+size_t kd_deftet_workspace_size(int batch, int64_t num_faces, int double_precision);
 int kd_deftet_sparse_render_forward_f32(int batch, int64_t num_pixels, int64_t num_faces,
                                         int knum, int feat_dim, const float *pixel_coords,
                                         const float *render_ranges, const float *fvz,

@@ -744,7 +744,7 @@ def deftet_sparse_render_forward(pixel_coords, render_ranges, face_vertices_z,
     interp = torch.empty((B, P, knum, D), **opts)
     face_idx = torch.empty((B, P, knum), device=dev, dtype=torch.long)
     weights = torch.empty((B, P, knum, 3), **opts)
-    nb = int(_lib.load().kd_deftet_workspace_size(B, P, F, D, 1 if sfx == 'f64' else 0))
+    nb = int(_lib.load().kd_deftet_workspace_size(B, F, 1 if sfx == 'f64' else 0))
     ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
     _lib.call(f'kd_deftet_sparse_render_forward_{sfx}', B, P, F, knum, D, *(_ptr(t) for t in c),
               float(eps), _ptr(interp), _ptr(face_idx), _ptr(weights), _ptr(ws), nb,
@@ -798,7 +798,7 @@ def deftet_sparse_render_forward_cuda(face_vertices_z, face_vertices_image, face
     depths = torch.empty((B, P, knum), **opts)
     w0 = torch.empty((B, P, knum), **opts)
     w1 = torch.empty((B, P, knum), **opts)
-    nb = int(_lib.load().kd_deftet_workspace_size(B, P, F, 0, 1 if sfx == 'f64' else 0))
+    nb = int(_lib.load().kd_deftet_workspace_size(B, F, 1 if sfx == 'f64' else 0))
     ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
     _lib.call(f'kd_deftet_sparse_render_forward_raw_{sfx}', B, P, F, knum, _ptr(face_vertices_z),
               _ptr(face_vertices_image), _ptr(face_bboxes), _ptr(pixel_coords),

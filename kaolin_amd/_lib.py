@@ -111,7 +111,7 @@ def load():
             lib.kd_dibr_pair_count.restype = c_i64
             lib.kd_mask_iou_workspace_size.argtypes = [c_int, c_i64, c_int]
             lib.kd_mask_iou_workspace_size.restype = c_size
-            lib.kd_deftet_workspace_size.argtypes = [c_int, c_i64, c_i64, c_int, c_int]
+            lib.kd_deftet_workspace_size.argtypes = [c_int, c_i64, c_int]
             lib.kd_deftet_workspace_size.restype = c_size
             lib.kd_texture_mapping_backward_workspace_size.argtypes = [c_int, c_i64, c_int, c_int,
                                                                        c_int]
@@ -186,7 +186,7 @@ def set_pool_limits(bins=1.0, pairs=1.0):
 _pool_limited = False
 
 # kd_set_test_forms bits (include/kaolin_dibr.h KD_FORM_*)
-FORM_SPLIT_FWD, FORM_SPLIT_BWD, FORM_SOFT_SPLIT, FORM_DT_PIXEL = 1, 2, 4, 8
+FORM_SPLIT_FWD, FORM_SPLIT_BWD, FORM_SOFT_SPLIT = 1, 2, 4
 
 
 def set_test_forms(forms=0):

@@ -116,8 +116,7 @@ const char *kNames[K_NUM_KERNELS] = {
     "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs",
     "kd_prepare_fwd", "kd_prepare_bwd", "kd_tile_order", "kd_iou_partial", "kd_iou_bwd",
     "kd_tex_fwd", "kd_tex_bwd", "kd_rast_interp", "kd_dt_bin",
-    "kd_dt_fwd", "kd_dibr_bwd", "kd_dibr_fwd", "kd_soft_ovf_fwd", "kd_soft_ovf_bwd",
-    "kd_dt_sort", "kd_dt_walk", "kd_dt_out"};
+    "kd_dt_fwd", "kd_dibr_bwd", "kd_dibr_fwd", "kd_soft_ovf_fwd", "kd_soft_ovf_bwd"};
 }  // namespace
 
 ProfScope::ProfScope(int id_, hipStream_t s) : id(id_), stream(s), on(g_prof.load()) {
@@ -163,7 +162,7 @@ int kd_debug_set(int flags) {
 }
 
 int kd_set_test_forms(int forms) {
-  if (forms & ~(KD_FORM_SPLIT_FWD | KD_FORM_SPLIT_BWD | KD_FORM_SOFT_SPLIT | KD_FORM_DT_PIXEL))
+  if (forms & ~(KD_FORM_SPLIT_FWD | KD_FORM_SPLIT_BWD | KD_FORM_SOFT_SPLIT))
     return kd::set_error(KD_ERR_INVALID_ARGUMENT, "unknown launch form bits 0x%x", forms);
   kd::g_forms.store(forms);
   return KD_OK;

@@ -41,9 +41,6 @@ enum KernelId {
   K_DIBR_FWD,
   K_SOFT_OVF_FWD,
   K_SOFT_OVF_BWD,
-  K_DT_SORT,
-  K_DT_WALK,
-  K_DT_OUT,
   K_NUM_KERNELS
 };
 

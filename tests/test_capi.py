@@ -77,9 +77,8 @@ def test_production_library_reads_no_debug_flags():
     assert lib.kd_debug_set(0) == _lib.KD_OK
     assert lib.kd_debug_set(256) != _lib.KD_OK
     assert b'diagnostic' in lib.kd_last_error()
-    assert lib.kd_set_test_forms(16) != _lib.KD_OK
-    _lib.set_test_forms(_lib.FORM_SPLIT_FWD | _lib.FORM_SPLIT_BWD | _lib.FORM_SOFT_SPLIT |
-                        _lib.FORM_DT_PIXEL)
+    assert lib.kd_set_test_forms(8) != _lib.KD_OK
+    _lib.set_test_forms(_lib.FORM_SPLIT_FWD | _lib.FORM_SPLIT_BWD | _lib.FORM_SOFT_SPLIT)
     _lib.set_test_forms(0)
 
 

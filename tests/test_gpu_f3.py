@@ -300,48 +300,3 @@ def test_forward_dense_soups(dt, size):
     ofi, od, oa0, oa1 = f3.deftet_forward_raw(px, rr, fvz, fvi, bbox, knum)
     for a, b in zip(raw, (ofi, od, oa0, oa1)):
         np.testing.assert_array_equal(a, b)
-
-
-@pytest.mark.parametrize('case', ['grid', 'one_cell', 'poles'])
-def test_cell_walk_matches_pixel_walk(case):
-    """The cell-major walk (kd_dt_walk: sorted pixels, hit records, re-walk past kDtHitCap) is
-    bit-identical to every pixel walking its own cell list (KD_FORM_DT_PIXEL), sorted and raw:
-    a pixel grid over a sphere, all pixels in one cell (many 64-pixel items against many
-    128-face chunks, hit counts past the record capacity), and a soup whose cell lists are long."""
-    from kaolin_amd import _lib, workloads
-    if case == 'grid':
-        v = workloads.sphere_views(80, 41, 128, 128, 1, DEV, seed=1, elevation=0.9)
-        fvz, fvi, feat = N(v['fvz']), N(v['fvi']), N(v['feats'])
-        H = W = 200
-        xs = (2 * np.arange(W) + 1 - W) / W
-        ys = (H - 2 * np.arange(H) - 1.) / H
-        px = np.stack(np.broadcast_arrays(xs[None, :], ys[:, None]), -1).reshape(1, -1, 2)
-        px = px.astype(np.float32)
-        rr = np.broadcast_to(np.array([-1e9, 0.], np.float32), (1, H * W, 2)).copy()
-        knum = 30
-    else:
-        px, rr, fvz, fvi, feat = soup(1, 1500, 3000, np.float32, 9,
-                                      size=0.6 if case == 'one_cell' else 2.5)
-        if case == 'one_cell':
-            px = (px * np.float32(0.01)).astype(np.float32)  # every pixel inside one 1/32 cell
-        knum = 40 if case == 'one_cell' else 12
-    bbox = np.concatenate([fvi.min(2), fvi.max(2)], -1)
-    out = {}
-    try:
-        for form in (0, _lib.FORM_DT_PIXEL):
-            _lib.set_test_forms(form)
-            out[form] = (_forward(px, rr, fvz, fvi, feat, knum),
-                         _forward(px, rr, fvz, fvi, feat, knum, raw_boxes=bbox))
-    finally:
-        _lib.set_test_forms(0)
-    (si, sf), raw = out[0]
-    (pi, pf), praw = out[_lib.FORM_DT_PIXEL]
-    assert (sf >= 0).sum() > 0
-    np.testing.assert_array_equal(sf, pf)
-    np.testing.assert_array_equal(si, pi)
-    for a, b in zip(raw, praw):
-        np.testing.assert_array_equal(a, b)
-    if case != 'grid':
-        oi, of, _ = f3.deftet_forward(px, rr, fvz, fvi, feat, knum)
-        np.testing.assert_array_equal(sf, of)
-        np.testing.assert_array_equal(si, oi)
