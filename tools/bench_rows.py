@@ -96,7 +96,10 @@ def torch_texture_mapping(uv, tex, mode):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--rows', default='mask_iou,texture_mapping,rast_interpolate,deftet')
+    ap.add_argument('--dt-fwd', action='store_true', help='deftet: the forward alone (no grad)')
     args = ap.parse_args()
+    rows = args.rows.split(',')
     _lib.load()
     torch.manual_seed(0)
     B, H, W = 8, 512, 512
@@ -104,18 +107,19 @@ def main():
     S = args.steps
 
     # mask_iou ------------------------------------------------------------------------------
-    soft = torch.rand((B, H, W), device=DEV).requires_grad_(True)
-    gt = (torch.rand((B, H, W), device=DEV) > 0.5).float()
+    if 'mask_iou' in rows:
+        soft = torch.rand((B, H, W), device=DEV).requires_grad_(True)
+        gt = (torch.rand((B, H, W), device=DEV) > 0.5).float()
 
-    def iou_step():
-        mask_iou(soft, gt).backward()
+        def iou_step():
+            mask_iou(soft, gt).backward()
 
-    def iou_ref():
-        torch_mask_iou(soft, gt).backward()
-    wall, kern = timed(iou_step, S)
-    r = line('mask_iou', wall, kern, {'kd_iou_partial': 8 * P, 'kd_iou_bwd': 12 * P})
-    r['torch_reference_us'] = round(torch_time(iou_ref, S) * 1e6, 1)
-    print(json.dumps(r))
+        def iou_ref():
+            torch_mask_iou(soft, gt).backward()
+        wall, kern = timed(iou_step, S)
+        r = line('mask_iou', wall, kern, {'kd_iou_partial': 8 * P, 'kd_iou_bwd': 12 * P})
+        r['torch_reference_us'] = round(torch_time(iou_ref, S) * 1e6, 1)
+        print(json.dumps(r))
 
     # the C3 render: interpolated uvs, face index, barycentrics of the real DIB-R forward
     from kaolin_amd.render.mesh import dibr_rasterization
@@ -135,36 +139,37 @@ def main():
 
     # texture_mapping (ian_dibr.py:248-252: the rendered uvs, background uv = 0; the image loss
     # gradient is masked, so background samples carry a zero gradient) ----------------------
-    uv = interp.detach().clone().requires_grad_(True)
-    tex = torch.rand((B, 3, 512, 512), device=DEV).requires_grad_(True)
-    go = torch.rand((B, H, W, 3), device=DEV) * mask
-    texb = tex.numel() * 4
+    if 'texture_mapping' in rows or 'rast_interpolate' in rows:
+        uv = interp.detach().clone().requires_grad_(True)
+        tex = torch.rand((B, 3, 512, 512), device=DEV).requires_grad_(True)
+        go = torch.rand((B, H, W, 3), device=DEV) * mask
+        texb = tex.numel() * 4
 
-    def tex_step():
-        torch.autograd.backward(texture_mapping(uv, tex, mode='bilinear'), go)
+        def tex_step():
+            torch.autograd.backward(texture_mapping(uv, tex, mode='bilinear'), go)
 
-    def tex_ref():
-        torch.autograd.backward(torch_texture_mapping(uv, tex, 'bilinear'), go)
-    wall, kern = timed(tex_step, S)
-    r = line('texture_mapping', wall, kern,
-             {'kd_tex_fwd': P * (8 + 12) + texb, 'kd_tex_bwd': P * (8 + 12 + 8) + 2 * texb})
-    r['torch_reference_us'] = round(torch_time(tex_ref, S) * 1e6, 1)
-    print(json.dumps(r))
+        def tex_ref():
+            torch.autograd.backward(torch_texture_mapping(uv, tex, 'bilinear'), go)
+        wall, kern = timed(tex_step, S)
+        r = line('texture_mapping', wall, kern,
+                 {'kd_tex_fwd': P * (8 + 12) + texb, 'kd_tex_bwd': P * (8 + 12 + 8) + 2 * texb})
+        r['torch_reference_us'] = round(torch_time(tex_ref, S) * 1e6, 1)
+        print(json.dumps(r))
 
-    # rast_interpolate: a rast buffer holding the C3 render (u, v, 0, face + 1) ------------
-    feat = uvs_b.clone().requires_grad_(True)
-    fvi = fvi_r.clone().requires_grad_(True)
-    rast = torch.cat([weights[..., :2], torch.zeros_like(weights[..., :1]),
-                      (face_idx + 1).float().unsqueeze(-1)], dim=-1).contiguous()
-    cov = int((face_idx >= 0).sum())
-    go2 = torch.rand((B, H, W, 2), device=DEV)
+        # rast_interpolate: a rast buffer holding the C3 render (u, v, 0, face + 1) ------------
+        feat = uvs_b.clone().requires_grad_(True)
+        fvi = fvi_r.clone().requires_grad_(True)
+        rast = torch.cat([weights[..., :2], torch.zeros_like(weights[..., :1]),
+                          (face_idx + 1).float().unsqueeze(-1)], dim=-1).contiguous()
+        cov = int((face_idx >= 0).sum())
+        go2 = torch.rand((B, H, W, 2), device=DEV)
 
-    def ri_step():
-        out, _ = rasterize_from_rast(rast, fvi, feat)
-        out.backward(go2)
-    wall, kern = timed(ri_step, S)
-    print(json.dumps(line('rast_interpolate', wall, kern,
-                          {'kd_rast_interp': P * (16 + 8 + 8 + 12) + cov * 24})))
+        def ri_step():
+            out, _ = rasterize_from_rast(rast, fvi, feat)
+            out.backward(go2)
+        wall, kern = timed(ri_step, S)
+        print(json.dumps(line('rast_interpolate', wall, kern,
+                              {'kd_rast_interp': P * (16 + 8 + 8 + 12) + cov * 24})))
 
     # deftet --------------------------------------------------------------------------------
     cam = cams[:1]
@@ -183,6 +188,10 @@ def main():
     gdt = torch.rand((1, H * W, K, 2), device=DEV)
 
     def dt_step():
+        if args.dt_fwd:
+            with torch.no_grad():
+                deftet_sparse_render(px, rr, fvz1, fvi1, uvs1, K)
+            return
         interp, _ = deftet_sparse_render(px, rr, fvz1, fvi1, uvs1, K)
         interp.backward(gdt)
     wall, kern = timed(dt_step, S)
