@@ -284,6 +284,25 @@ int kd_dibr_rasterization_forward_f64(int batch, int height, int width, int64_t 
                                       int64_t *face_idx, double *weights, double *soft,
                                       int want_grad, double *grad_fvi_zero, double *grad_feat_zero,
                                       void *workspace, size_t workspace_bytes, void *stream);
+/* The same forward keeping the close-face lists of its soft mask (dibr.py's DibrSoftMaskCuda
+ * inside the reference composition, dibr.py:193-208, dibr_soft_mask_cuda.cu:165-171): prob
+ * (B, H, W, knum), cidx (B, H, W, knum) int64 (-1 = empty), ctype (B, H, W, knum) uint8, read
+ * by kd_dibr_soft_mask_backward_* (with kd_rasterize_backward_* for the raster part).  No
+ * workspace backward (want_grad 0). */
+int kd_dibr_rasterization_forward_lists_f32(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const float *fvz,
+    int64_t fvz_face_stride, int64_t fvz_corner_stride, const float *fvi, const float *feat,
+    const float *normals_z, int64_t normals_z_stride, double multiplier, float eps,
+    float sigmainv, double boxlen, int knum, float *interp, int64_t *face_idx, float *weights,
+    float *soft, float *prob, int64_t *cidx, uint8_t *ctype, void *workspace,
+    size_t workspace_bytes, void *stream);
+int kd_dibr_rasterization_forward_lists_f64(
+    int batch, int height, int width, int64_t num_faces, int feat_dim, const double *fvz,
+    int64_t fvz_face_stride, int64_t fvz_corner_stride, const double *fvi, const double *feat,
+    const double *normals_z, int64_t normals_z_stride, double multiplier, float eps,
+    float sigmainv, double boxlen, int knum, double *interp, int64_t *face_idx, double *weights,
+    double *soft, double *prob, int64_t *cidx, uint8_t *ctype, void *workspace,
+    size_t workspace_bytes, void *stream);
 /* The same forward from the vertices (prepare_vertices, camera transform form,
  * kaolin/render/mesh/utils.py:128-175, followed by dibr_rasterization of its outputs, the DIB-R
  * training step of examples/tutorial/ian_dibr.py): vertices (vertex_batch, V, 3) with

@@ -411,12 +411,14 @@ def _rows_view(t, F, inner):
 def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertices_image,
                                      face_features, face_normals_z, sigmainv, boxlen, knum,
                                      multiplier, eps, want_grad=True, grad_buffers=None,
-                                     iou_gt=None):
+                                     iou_gt=None, with_lists=False):
     """rasterize(valid = normals_z >= 0) + dibr_soft_mask in one launch sequence.  Returns
     (interp, face_idx, weights, soft, workspace), and with iou_gt (B, H, W) also (iou_loss,
     iou_stats): mask_iou(soft, iou_gt) fused in (kd_dibr_rasterization_iou_forward).
     grad_buffers = (grad_fvi, grad_feat or None): buffers of the backward that this forward
-    zeroes (see kd_dibr_rasterization_forward)."""
+    zeroes (see kd_dibr_rasterization_forward).  with_lists: also the soft mask's close-face
+    lists (prob, cidx, ctype) (B, H, W, knum), appended to the returns (no workspace backward;
+    kd_dibr_rasterization_forward_lists)."""
     fn = 'dibr_rasterization'
     dev = _check_same_gpu(fn, face_vertices_z=face_vertices_z,
                           face_vertices_image=face_vertices_image, face_features=face_features,
@@ -461,6 +463,16 @@ def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertic
                   1 if want_grad else 0, _ptr(grad_buffers[0]) if grad_buffers else None,
                   _ptr(grad_buffers[1]) if grad_buffers else None, _ptr(ws), nb, _stream(dev))
         return interp, face_idx, weights, soft, ws, loss, stats
+    if with_lists:
+        prob = torch.empty((B, height, width, knum), **opts)
+        cidx = torch.empty((B, height, width, knum), device=dev, dtype=torch.long)
+        ctype = torch.empty((B, height, width, knum), device=dev, dtype=torch.uint8)
+        _lib.call(f'kd_dibr_rasterization_forward_lists_{sfx}', B, height, width, F, D, _ptr(fvz),
+                  fvz_fs, fvz_cs, _ptr(fvi), _ptr(feat), _ptr(nz), nz_s, float(multiplier),
+                  float(eps), float(sigmainv), float(boxlen), knum, _ptr(interp), _ptr(face_idx),
+                  _ptr(weights), _ptr(soft), _ptr(prob), _ptr(cidx), _ptr(ctype), _ptr(ws), nb,
+                  _stream(dev))
+        return interp, face_idx, weights, soft, ws, prob, cidx, ctype
     _lib.call(f'kd_dibr_rasterization_forward_{sfx}', B, height, width, F, D, _ptr(fvz), fvz_fs,
               fvz_cs, _ptr(fvi), _ptr(feat), _ptr(nz), nz_s, float(multiplier), float(eps),
               float(sigmainv), float(boxlen), knum, _ptr(interp), _ptr(face_idx), _ptr(weights),

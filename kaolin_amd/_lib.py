@@ -44,6 +44,10 @@ _SIGS = {
                                       c_p, c_p, c_i64, c_double, c_float, c_float, c_double,
                                       c_int, c_p, c_p, c_p, c_p, c_int, c_p, c_p, c_p, c_size,
                                       c_p],
+    'kd_dibr_rasterization_forward_lists': [c_int, c_int, c_int, c_i64, c_int, c_p, c_i64, c_i64,
+                                            c_p, c_p, c_p, c_i64, c_double, c_float, c_float,
+                                            c_double, c_int, c_p, c_p, c_p, c_p, c_p, c_p, c_p,
+                                            c_p, c_size, c_p],
     'kd_dibr_rasterization_forward_vertices': [c_int, c_int, c_int, c_int, c_i64, c_i64, c_int,
                                                c_p, c_p, c_p, c_p, c_p, c_double, c_float,
                                                c_float, c_double, c_int, c_p, c_p, c_p, c_p, c_p,

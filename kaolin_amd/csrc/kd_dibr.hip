@@ -97,7 +97,8 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
                     double M, float eps, float sigmainv, double boxlen, int K, T *interp,
                     int64_t *face_idx, T *weights, T *soft, int want_grad, T *gz_fvi,
                     T *gz_feat, void *ws, size_t wsb, void *stream_,
-                    const IouIo<T> &iou = IouIo<T>{}, const PrepOut<T> *prep = nullptr) {
+                    const IouIo<T> &iou = IouIo<T>{}, const PrepOut<T> *prep = nullptr,
+                    T *prob = nullptr, int64_t *cidx = nullptr, uint8_t *ctype = nullptr) {
   hipStream_t stream = (hipStream_t)stream_;
   KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && D >= 0, "negative size");
   KD_CHECK_ARG(K >= 1 && K <= 65535, "knum must be in [1, 65535]");
@@ -108,6 +109,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   if (wsb < need || (need && !ws))
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   KD_CHECK_ARG(!iou.gt || (iou.loss && iou.stats && iou.acc), "mask_iou: NULL output");
+  KD_CHECK_ARG(!prob == !cidx && !prob == !ctype, "close lists: give all three outputs or none");
   KD_CHECK_ARG(!iou.gt || (K <= kFuseSlots && pool_limit_pairs() >= 1.f &&
                             !(test_forms() & KD_FORM_SOFT_SPLIT)),
                "fused mask_iou needs knum <= 32 (the one-launch soft mask)");
@@ -154,6 +156,9 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
   sa.iou_gt = iou.gt;
   sa.iou_acc = iou.acc;
   sa.iou_B = B;
+  sa.prob = prob;  // the close-face lists (dibr_soft_mask_cuda.cu:165-171)
+  sa.cidx = cidx;
+  sa.ctype = ctype;
   const bool fusable = dibr_fwd_fusable(ra, sa);  // (fp32 and fp64)
   // the one-launch fp32 forward's tile history (kd_set_tile_history): the previous same-shape
   // call's tile durations order this call's tiles (tile_order) and this call records its own --
@@ -355,6 +360,30 @@ int kd_dibr_rasterization_forward_f32(int B, int H, int W, int64_t F, int D, con
                          normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
                          face_idx, weights, soft, want_grad, grad_fvi_zero, grad_feat_zero, ws,
                          wsb, stream);
+}
+int kd_dibr_rasterization_forward_lists_f32(
+    int B, int H, int W, int64_t F, int D, const float *fvz, int64_t fvz_face_stride,
+    int64_t fvz_corner_stride, const float *fvi, const float *feat, const float *normals_z,
+    int64_t normals_z_stride, double M, float eps, float sigmainv, double boxlen, int knum,
+    float *interp, int64_t *face_idx, float *weights, float *soft, float *prob, int64_t *cidx,
+    uint8_t *ctype, void *ws, size_t wsb, void *stream) {
+  KD_CHECK_ARG(prob && cidx && ctype, "close lists: NULL output");
+  return dibr_fwd<float>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
+                         normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
+                         face_idx, weights, soft, 0, nullptr, nullptr, ws, wsb, stream,
+                         IouIo<float>{}, nullptr, prob, cidx, ctype);
+}
+int kd_dibr_rasterization_forward_lists_f64(
+    int B, int H, int W, int64_t F, int D, const double *fvz, int64_t fvz_face_stride,
+    int64_t fvz_corner_stride, const double *fvi, const double *feat, const double *normals_z,
+    int64_t normals_z_stride, double M, float eps, float sigmainv, double boxlen, int knum,
+    double *interp, int64_t *face_idx, double *weights, double *soft, double *prob,
+    int64_t *cidx, uint8_t *ctype, void *ws, size_t wsb, void *stream) {
+  KD_CHECK_ARG(prob && cidx && ctype, "close lists: NULL output");
+  return dibr_fwd<double>(B, H, W, F, D, fvz, fvz_face_stride, fvz_corner_stride, fvi, feat,
+                          normals_z, normals_z_stride, M, eps, sigmainv, boxlen, knum, interp,
+                          face_idx, weights, soft, 0, nullptr, nullptr, ws, wsb, stream,
+                          IouIo<double>{}, nullptr, prob, cidx, ctype);
 }
 int kd_dibr_rasterization_forward_vertices_f32(
     int B, int H, int W, int vertex_batch, int64_t V, int64_t F, int D, const float *vertices,

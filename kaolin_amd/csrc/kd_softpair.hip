@@ -1239,7 +1239,7 @@ __global__ __launch_bounds__(kBlock) void kd_dibr_bwd(SoftArgs<T> a, SoftPairBuf
   if (blk < nr)
     raster_bwd_tile_body<T, 3, VTX>(ra, blk, nr, ntl);
   else
-    soft_bwd_items_body<T, 1, VTX>(a, pb, blk - nr, ns);
+    soft_bwd_items_body<T, 2, VTX>(a, pb, blk - nr, ns);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1274,6 +1274,22 @@ static void ovf_bwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipSt
                        pb);
 }
 
+// The close-face lists after a one-launch soft mask (kd_soft_pairs FUSED or kd_dibr_fwd_tiles,
+// which leave every record's probability and distance type): an overflowed tile's soft mask and
+// lists from the streaming walk (the split form), then the lists writer over the records.
+template <typename T>
+static int lists_after_one_launch(const SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream) {
+  if (pool_may_overflow(a.K)) ovf_fwd_launch<T, false>(a, pb, stream);
+  KD_CHECK_ARG(a.fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
+  SoftArgs<T> al = a;  // (the backward's zero fills were the one launch's side job)
+  al.nzero0 = al.nzero1 = 0;
+  al.soft = nullptr;  // (and the soft mask)
+  const size_t dyn = ((sizeof(T) + sizeof(int)) * (kReduceSlots + 1) + sizeof(int)) * kBlock / 2;
+  ProfScope prof(K_SOFT_REDUCE, stream);
+  hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), dyn, stream, al, pb);
+  return KD_OK;
+}
+
 template <typename T>
 int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce,
                       hipStream_t stream) {
@@ -1293,15 +1309,8 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
                          dim3(kBlock), 0, stream, a, pb);
     }
     if (a.prob) {
-      // an overflowed tile: its soft mask and lists from the streaming walk (the split form)
-      if (pool_may_overflow(a.K)) ovf_fwd_launch<T, false>(a, pb, stream);
-      KD_CHECK_ARG(fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
-      SoftArgs<T> al = a;  // (the backward's zero fills were the one launch's side job)
-      al.nzero0 = al.nzero1 = 0;
-      al.soft = nullptr;  // (and the soft mask)
-      const size_t dyn = ((sizeof(T) + sizeof(int)) * (kReduceSlots + 1) + sizeof(int)) * kBlock / 2;
-      ProfScope prof(K_SOFT_REDUCE, stream);
-      hipLaunchKernelGGL(kd_soft_lists<T>, dim3(8192), dim3(kBlock), dyn, stream, al, pb);
+      const int rc = lists_after_one_launch<T>(a, pb, stream);
+      if (rc != KD_OK) return rc;
     } else if (pool_may_overflow(a.K)) {
       ovf_fwd_launch<T, true>(a, pb, stream);
     }
@@ -1349,7 +1358,7 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
 }
 
 bool dibr_fwd_fusable(const RasterFwdArgs<double> &ra, const SoftArgs<double> &a) {
-  return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
+  return ra.bb.cull && a.soft && !a.last && a.K <= kFuseSlots &&
          !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT));
 }
 
@@ -1363,7 +1372,12 @@ int dibr_fwd_fused_launch(RasterFwdArgs<double> &ra, SoftArgs<double> &a,
     hipLaunchKernelGGL(kd_dibr_fwd_tiles_f64, dim3((unsigned)pb.ntiles, ra.fs.B), dim3(kBlock), 0,
                        stream, ra, a, pb);
   }
-  if (pool_may_overflow(a.K)) ovf_fwd_launch<double, true>(a, pb, stream);
+  if (a.prob) {  // the close-face lists (dibr_rasterization inside close_lists())
+    const int rc = lists_after_one_launch<double>(a, pb, stream);
+    if (rc != KD_OK) return rc;
+  } else if (pool_may_overflow(a.K)) {
+    ovf_fwd_launch<double, true>(a, pb, stream);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr fwd: %s", hipGetErrorString(e));
   return KD_OK;
@@ -1395,7 +1409,7 @@ int dibr_fwd_split(const SoftPairBuf<float> &pb, int K, int B, bool history, hip
 }
 
 bool dibr_fwd_fusable(const RasterFwdArgs<float> &ra, const SoftArgs<float> &a) {
-  return ra.bb.cull && a.soft && !a.prob && !a.last && a.K <= kFuseSlots &&
+  return ra.bb.cull && a.soft && !a.last && a.K <= kFuseSlots &&
          !(test_forms() & (KD_FORM_SPLIT_FWD | KD_FORM_SOFT_SPLIT));
 }
 
@@ -1406,7 +1420,8 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
   a.fs.tbuf = debug_tile_buffer();
   {
     ProfScope prof(K_DIBR_FWD, stream);
-    const int split = dibr_fwd_split(pb, a.K, ra.fs.B, ra.bb.hist != nullptr, stream);
+    // (the lists writer reads each tile's records as one run: whole tiles)
+    const int split = a.prob ? 1 : dibr_fwd_split(pb, a.K, ra.fs.B, ra.bb.hist != nullptr, stream);
     const dim3 grid((unsigned)pb.ntiles * split, ra.fs.B);
     const bool diag = KD_DIAG && a.fs.tbuf;
 #define KD_FWD_TILES(S)                                                                         \
@@ -1426,7 +1441,12 @@ int dibr_fwd_fused_launch(RasterFwdArgs<float> &ra, SoftArgs<float> &a, SoftPair
       KD_FWD_TILES(1);
 #undef KD_FWD_TILES
   }
-  if (pool_may_overflow(a.K)) ovf_fwd_launch<float, true>(a, pb, stream);
+  if (a.prob) {  // the close-face lists (dibr_rasterization inside close_lists())
+    const int rc = lists_after_one_launch<float>(a, pb, stream);
+    if (rc != KD_OK) return rc;
+  } else if (pool_may_overflow(a.K)) {
+    ovf_fwd_launch<float, true>(a, pb, stream);
+  }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "dibr fwd: %s", hipGetErrorString(e));
   return KD_OK;

@@ -147,16 +147,66 @@ class DibrRasterizationHip(Function):
                 None, None)
 
 
+class DibrRasterizationListsHip(Function):
+    """dibr_rasterization inside ``close_lists()``: the fused forward also writes the soft
+    mask's close-face lists (kd_dibr_rasterization_forward_lists: one binning pass, one launch for
+    the raster and the soft mask, then the lists writer), and the backward is the reference
+    composition's (dibr.py:193-208): rasterize's (rasterization_cuda.cu) plus dibr_soft_mask's over
+    the lists (dibr_soft_mask_cuda.cu), summed into grad_fvi as autograd sums the two uses."""
+
+    @staticmethod
+    def forward(ctx, height, width, face_vertices_z, face_vertices_image, face_features,
+                face_normals_z, sigmainv, boxlen, knum, multiplier, eps):
+        face_vertices_image = face_vertices_image.contiguous()
+        face_features = face_features.contiguous()
+        interp, face_idx, weights, soft, _, prob, cidx, ctype = \
+            _C.render.mesh.dibr_rasterization_forward_fused(
+                height, width, face_vertices_z, face_vertices_image, face_features,
+                face_normals_z, sigmainv, boxlen, knum, multiplier, eps, want_grad=False,
+                with_lists=True)
+        ctx.save_for_backward(face_idx, weights, soft, face_vertices_image, face_features, prob,
+                              cidx, ctype)
+        ctx.params = (eps, multiplier, sigmainv)
+        ctx.mark_non_differentiable(face_idx)
+        ctx.set_materialize_grads(False)
+        return interp, soft, face_idx
+
+    @staticmethod
+    def backward(ctx, grad_interp, grad_soft, grad_face_idx):
+        need_fvi, need_feat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
+        if not (need_fvi or need_feat) or (grad_interp is None and grad_soft is None):
+            return (None,) * 11
+        face_idx, weights, soft, fvi, feat, prob, cidx, ctype = ctx.saved_tensors
+        eps, multiplier, sigmainv = ctx.params
+        gfvi = gfeat = None
+        if grad_interp is not None:
+            gfvi, gfeat = _C.render.mesh.rasterize_backward_autograd(
+                grad_interp.contiguous(), face_idx, weights, fvi, feat, eps, need_feat=need_feat)
+        if grad_soft is not None and need_fvi:
+            gs = _C.render.mesh.dibr_soft_mask_backward_cuda(
+                grad_soft.contiguous(), soft, face_idx, prob, cidx, ctype,
+                (fvi * multiplier).contiguous(), sigmainv, multiplier)
+            gfvi = gs if gfvi is None else gfvi + gs
+        return (None, None, None, gfvi if need_fvi else None, gfeat if need_feat else None, None,
+                None, None, None, None, None)
+
+
+# Inside close_lists(): the fused forward with lists (True) or the two ops of the reference
+# composition (False; the tests compare both)
+LISTS_FUSED = True
+
+
 def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face_features,
                        face_normals_z, sigmainv=7000, boxlen=0.02, knum=30, multiplier=None,
                        eps=None, rast_backend='cuda'):
     r"""DIB-R renderer (dibr.py:119-209): rasterize the front faces (normal z >= 0), then the
     soft mask over all faces.  Returns (interpolated_features, soft_mask, face_idx).
 
-    Runs as one fused forward / backward (DibrRasterizationHip); inside ``close_lists()`` it is
-    the reference composition of ``rasterize`` and ``dibr_soft_mask`` instead."""
+    Runs as one fused forward / backward (DibrRasterizationHip); inside ``close_lists()`` the
+    fused forward keeps the close-face lists and the backward is the reference composition's
+    (DibrRasterizationListsHip)."""
     _multiplier = 1000. if multiplier is None else multiplier
-    if _lists_enabled() or rast_backend != 'cuda':
+    if (_lists_enabled() and not LISTS_FUSED) or rast_backend != 'cuda':
         # the reference composition (dibr.py:193-208); other backends go through rasterize
         interpolated_features, face_idx = rasterize(
             height, width, face_vertices_z, face_vertices_image, face_features,
@@ -170,7 +220,8 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
         raise RuntimeError('internal: multiplier defaults disagree')
     feats = torch.cat(face_features, dim=-1) \
         if isinstance(face_features, (list, tuple)) else face_features
-    interp, soft, face_idx = DibrRasterizationHip.apply(
+    fn = DibrRasterizationListsHip if _lists_enabled() else DibrRasterizationHip
+    interp, soft, face_idx = fn.apply(
         height, width, face_vertices_z, face_vertices_image, feats, face_normals_z, sigmainv,
         boxlen, knum, _multiplier, _eps)
     if isinstance(face_features, (list, tuple)):

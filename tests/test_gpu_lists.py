@@ -85,3 +85,63 @@ def test_op_backward_on_lists_with_holes(dname, knum):
                                                       sfvi, sig, M)
     torch.cuda.synchronize()
     np.testing.assert_allclose(N(gop), ref, rtol=tol, atol=tol * 0.1 * np.abs(ref).max())
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('knum', [30, 40])
+def test_fused_forward_lists_vs_oracle(dname, knum):
+    """kd_dibr_rasterization_forward_lists (dibr_rasterization inside close_lists()): the one
+    binning pass and one launch of the fused forward, then the lists writer -- the lists and soft
+    mask against the oracle, bit-exact indices / types, and the raster outputs equal to the op
+    form's (rasterize)."""
+    from kaolin_amd import _C, workloads
+    from kaolin_amd.render.mesh import rasterize
+    dt = TORCH_DTYPES[dname]
+    v = workloads.sphere_views(100, 51, 256, 256, 2, DEV, dtype=dt, elevation=0.7)
+    sig, box, M = 7000., 0.03, 1000.
+    interp, face_idx, weights, soft, _, prob, cidx, ctype = \
+        _C.render.mesh.dibr_rasterization_forward_fused(
+            256, 256, v['fvz'], v['fvi'], v['feats'], v['normals_z'], sig, box, knum, M, 1e-8,
+            want_grad=False, with_lists=True)
+    ri, rf = rasterize(256, 256, v['fvz'], v['fvi'], v['feats'], v['normals_z'] >= 0)
+    np.testing.assert_array_equal(N(face_idx), N(rf))
+    np.testing.assert_array_equal(N(interp), N(ri))
+    osoft, oprob, ocidx, octype, _ = oracle.soft_mask_forward(N(v['fvi']), N(face_idx), sig, box,
+                                                              knum)
+    np.testing.assert_array_equal(N(cidx), ocidx)
+    np.testing.assert_array_equal(N(ctype), octype)
+    np.testing.assert_allclose(N(prob), oprob, rtol=1e-6, atol=1e-37)
+    np.testing.assert_allclose(N(soft), osoft, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+def test_close_lists_fused_matches_composition(dname):
+    """dibr_rasterization inside close_lists(): the fused forward with lists
+    (DibrRasterizationListsHip) against the reference composition (rasterize + dibr_soft_mask):
+    equal outputs, and gradients equal up to the lists backward's atomic summation order."""
+    from kaolin_amd import workloads
+    from kaolin_amd.render.mesh import dibr, dibr_rasterization
+    from kaolin_amd.render.mesh.dibr import close_lists
+    dt = TORCH_DTYPES[dname]
+    v = workloads.sphere_views(100, 51, 192, 192, 2, DEV, dtype=dt, elevation=0.5)
+    g = torch.Generator().manual_seed(3)
+    gi = torch.rand((2, 192, 192, v['feats'].shape[-1]), generator=g, dtype=torch.float64)
+    gsft = torch.rand((2, 192, 192), generator=g, dtype=torch.float64)
+    out = {}
+    try:
+        for fused in (True, False):
+            dibr.LISTS_FUSED = fused
+            fvi = v['fvi'].detach().clone().requires_grad_(True)
+            feat = v['feats'].detach().clone().requires_grad_(True)
+            with close_lists():
+                interp, soft, fidx = dibr_rasterization(192, 192, v['fvz'], fvi, feat,
+                                                        v['normals_z'], 7000., 0.02, 30)
+            torch.autograd.backward([interp, soft], [gi.to(DEV, dt), gsft.to(DEV, dt)])
+            out[fused] = [N(t) for t in (interp, soft, fidx, fvi.grad, feat.grad)]
+    finally:
+        dibr.LISTS_FUSED = True
+    for a, b in zip(out[True][:3], out[False][:3]):
+        np.testing.assert_array_equal(a, b)
+    tol = 1e-4 if dname == 'f32' else 1e-9
+    for a, b in zip(out[True][3:], out[False][3:]):
+        np.testing.assert_allclose(a, b, rtol=tol, atol=tol * 0.1 * np.abs(b).max())
