@@ -167,7 +167,8 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
     const int64_t nt = (int64_t)((W + kTile - 1) / kTile) * ((H + kTile - 1) / kTile);
     uint64_t tag = 1469598103934665603ull;  // FNV-1a over the shape and the hooks
     for (const int64_t x : {(int64_t)B, (int64_t)H, (int64_t)W, F, (int64_t)K,
-                            (int64_t)tile_split(), (int64_t)coarse_tile_hook()})
+                            (int64_t)tile_split(), (int64_t)coarse_tile_hook(),
+                            (int64_t)(prob != nullptr)})  // (the lists path runs whole tiles)
       tag = (tag ^ (uint64_t)x) * 1099511628211ull;
     d.rbb.hist = tile_history(4 * (int64_t)B * nt, (long long)(tag >> 1), stream);
     ra.bb.hist = d.rbb.hist;
