@@ -143,6 +143,26 @@ def test_dibr_soft_mask_pool_overflow(limits, knum, lists):
     np.testing.assert_allclose(N(g1), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
 
 
+@pytest.mark.parametrize('limits', LIMITS)
+@pytest.mark.parametrize('knum', [30, 40])
+def test_dibr_rasterization_close_lists_pool_overflow(limits, knum):
+    """dibr_rasterization inside close_lists() (the fused forward with lists, knum 30; the split
+    path with lists, knum 40) with the pools limited: outputs bit-identical to the default run,
+    gradients up to summation order, and the soft mask / gradient against the oracle."""
+    from kaolin_amd.render.mesh import dibr
+    h = 128
+    fvz, fvi, feats, nz = _views(60, 31, h, 2)
+    with dibr.close_lists():
+        ref = _dibr(h, fvz, fvi, feats, nz, (1.0, 1.0), knum=knum)
+        out = _dibr(h, fvz, fvi, feats, nz, limits, knum=knum)
+    for a, b in zip(out[:3], ref[:3]):
+        assert torch.equal(a, b)
+    _close(out[3], ref[3], torch.float32)
+    _close(out[4], ref[4], torch.float32)
+    osoft, _, _, _, _ = oracle.soft_mask_forward(N(fvi), N(out[2]), 7000, 0.02, knum)
+    np.testing.assert_allclose(N(out[1]), osoft, rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize('limits', [(0.0, 0.0), (0.5, 0.1)])
 def test_close_lists_op_pool_overflow(limits):
     """The reference op with close-face lists (_C.render.mesh.dibr_soft_mask_forward_fused with
