@@ -49,7 +49,7 @@ int kd_version(void);
 /* In-library kernel timing (HIP events recorded around every launch on the launch stream).
  * kd_profile_enable(1) starts recording; kd_profile_collect() waits for the recorded events,
  * adds each kernel's elapsed milliseconds / launch count into total_ms[id] / launches[id]
- * (arrays of n entries), clears the records and returns the number of kernel ids.
+ * (arrays of n entries), clears the records and returns min(n, number of kernel ids).
  * kd_profile_kernel_name(id) names them.  Not for use under stream capture. */
 void kd_profile_enable(int on);
 int kd_profile_collect(double *total_ms, int64_t *launches, int n);

@@ -247,7 +247,7 @@ def profile_enable(on=True):
 def profile_collect():
     """{kernel name: (total ms, launches)} for the launches recorded since the last collect."""
     lib = load()
-    n = 32
+    n = 64
     ms = (ctypes.c_double * n)()
     cnt = (ctypes.c_int64 * n)()
     k = lib.kd_profile_collect(ctypes.cast(ms, c_p), ctypes.cast(cnt, c_p), n)

@@ -116,7 +116,8 @@ const char *kNames[K_NUM_KERNELS] = {
     "kd_zero", "kd_soft_pairs", "kd_soft_pair_math", "kd_soft_reduce", "kd_soft_bwd_pairs",
     "kd_prepare_fwd", "kd_prepare_bwd", "kd_tile_order", "kd_iou_partial", "kd_iou_bwd",
     "kd_tex_fwd", "kd_tex_bwd", "kd_rast_interp", "kd_dt_bin",
-    "kd_dt_fwd", "kd_dibr_bwd", "kd_dibr_fwd", "kd_soft_ovf_fwd", "kd_soft_ovf_bwd"};
+    "kd_dt_fwd", "kd_dibr_bwd", "kd_dibr_fwd", "kd_soft_ovf_fwd", "kd_soft_ovf_bwd",
+    "kd_dt_bwd"};
 }  // namespace
 
 ProfScope::ProfScope(int id_, hipStream_t s) : id(id_), stream(s), on(g_prof.load()) {
@@ -219,7 +220,7 @@ int kd_profile_collect(double *total_ms, int64_t *launches, int n) {
     (void)hipEventDestroy(r.start);
     (void)hipEventDestroy(r.stop);
   }
-  return kd::K_NUM_KERNELS;
+  return n < kd::K_NUM_KERNELS ? n : kd::K_NUM_KERNELS;  // the entries written
 }
 
 const char *kd_profile_kernel_name(int id) {

@@ -41,6 +41,7 @@ enum KernelId {
   K_DIBR_FWD,
   K_SOFT_OVF_FWD,
   K_SOFT_OVF_BWD,
+  K_DT_BWD,
   K_NUM_KERNELS
 };
 

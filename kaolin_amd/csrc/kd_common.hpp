@@ -38,7 +38,9 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       1 << 20 256-face binning chunks, 1 << 21 one count workgroup for both face sets,
 //       1 << 29 the lane-per-pixel K-list backward,
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost),
-//       1 << 24 the fused forward without its soft phase (the raster phase's instruction counts).
+//       1 << 24 the fused forward without its soft phase (the raster phase's instruction counts),
+//       1 << 25 the DefTet backward as the raster tile kernel over the P x knum samples,
+//       1 << 27 kd_dt_bwd: the sample compaction only (no per-face sums).
 #if KD_DIAG
 int debug_flags();
 #else

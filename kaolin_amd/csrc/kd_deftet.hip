@@ -21,14 +21,17 @@
 //                 order; the reference's torch.argsort is not stable, so tied depths are the one
 //                 place it is unpinned), and each slot writes its face index, weights
 //                 (w0, w1, 1 - (w0 + w1)) and interpolated features; empty slots get -1 / 0.
-//   backward      the rasterize backward (kd_raster.hip, the same per-sample math:
-//                 deftet_cuda.cu:238-402 == rasterization_cuda.cu:238-402) over the (pixel, slot)
-//                 samples laid out as a P x knum image.
+//   kd_dt_bwd     the rasterize backward's per-sample math (deftet_cuda.cu:238-402 ==
+//                 rasterization_cuda.cu:238-402, kd_raster_bwd.hpp) over the (pixel, slot)
+//                 samples that hold a face: a workgroup takes kDtBwdSpan consecutive samples,
+//                 compacts the occupied ones into LDS (most slots are empty) and sums their terms
+//                 per face 256 at a time (raster_bwd_group), one atomic per (group, face, term).
 // The eps of the box-normalisation is the reference's float parameter (copysignf of it), also for
 // fp64 data.
 #include "kd_capi.hpp"
 #include "kd_common.hpp"
 #include "kd_raster.hpp"
+#include "kd_raster_bwd.hpp"
 #include "kd_tile.hpp"
 
 namespace kd {
@@ -417,6 +420,51 @@ static int dt_forward(int B, int64_t P, int64_t F, int K, int D, const T *px, co
   return KD_OK;
 }
 
+constexpr int kDtBwdSpan = 512;  // samples per workgroup: 2 per lane
+
+template <typename T, int DMAX>
+__global__ __launch_bounds__(kBlock) void kd_dt_bwd(RasterBwdArgs<T> ra) {
+  constexpr int PER = kDtBwdSpan / kBlock;
+  __shared__ short s_hit[kDtBwdSpan];
+  __shared__ int s_scan[4];
+  const int64_t PK = (int64_t)ra.H * ra.W;
+  const int64_t total = ra.B * PK;
+  const int tid = threadIdx.x;
+  // XCD-aware as the raster tiles: XCD x gets a contiguous band of groups (neighbouring pixels
+  // share faces)
+  int d = blockIdx.x;
+  const int n = gridDim.x;
+  if ((n & 7) == 0) d = (d & 7) * (n >> 3) + (d >> 3);
+  const int64_t e0 = (int64_t)d * kDtBwdSpan;
+  // occupied samples of the span, in sample order
+  bool hit[PER];
+  int cnt = 0;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int64_t e = e0 + tid * PER + i;
+    const int64_t f = e < total ? ra.face_idx[e] : -1;
+    hit[i] = f >= 0 && f < ra.F;
+    cnt += hit[i];
+  }
+  int nh;
+  int o = wg_exclusive_scan(cnt, s_scan, nh);
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+    if (hit[i]) s_hit[o++] = (short)(tid * PER + i);
+  __syncthreads();
+  if (ablate(ra.dbg, 1 << 27)) return;
+  for (int base = 0; base < nh; base += kBlock) {
+    if (base) __syncthreads();  // the previous group is done with the LDS table
+    int64_t p = -1;
+    int b = 0;
+    if (base + tid < nh) {
+      p = e0 + s_hit[base + tid];
+      b = ra.B == 1 ? 0 : (int)(p / PK);
+    }
+    raster_bwd_group<T, DMAX, false, true>(ra, p, b);
+  }
+}
+
 template <typename T>
 static int dt_backward(int B, int64_t P, int64_t F, int K, int D, const T *grad,
                        const int64_t *face_idx, const T *weights, const T *fvi, const T *feat,
@@ -427,9 +475,27 @@ static int dt_backward(int B, int64_t P, int64_t F, int K, int D, const T *grad,
   const int64_t nf = (int64_t)B * F;
   int rc = zero_buffers<T>(gfvi, nf * 6, gfeat, gfeat ? nf * 3 * D : 0, stream);
   if (rc != KD_OK || B == 0 || P == 0) return rc;
-  // (pixel, slot) samples as a P x K image: deftet_cuda.cu:238-402 is rasterization_cuda.cu's math
-  return raster_backward_launch<T>(B, (int)P, K, F, D, grad, face_idx, weights, fvi, feat, eps,
-                                   gfvi, gfeat, stream);
+  const int64_t total = (int64_t)B * P * K;
+  if (D > 8 || nf >= (1ll << 31) || (debug_flags() & (1 << 25)))
+    // (pixel, slot) samples as a P x K image (one atomic per sample and term past 8 features)
+    return raster_backward_launch<T>(B, (int)P, K, F, D, grad, face_idx, weights, fvi, feat, eps,
+                                     gfvi, gfeat, stream);
+  const int64_t nblk = (total + kDtBwdSpan - 1) / kDtBwdSpan;
+  KD_CHECK_ARG(nblk < (1ll << 31), "deftet: too many samples");
+  const RasterBwdArgs<T> ra{B,       (int)P, K,   F,    D,     grad, face_idx,
+                            weights, fvi,    feat, eps, gfvi, gfeat, debug_flags()};
+  {
+    ProfScope prof(K_DT_BWD, stream);
+    if (D <= 3)
+      hipLaunchKernelGGL((kd_dt_bwd<T, 3>), dim3((unsigned)nblk), dim3(kBlock), 0, stream, ra);
+    else if (D <= 4)
+      hipLaunchKernelGGL((kd_dt_bwd<T, 4>), dim3((unsigned)nblk), dim3(kBlock), 0, stream, ra);
+    else
+      hipLaunchKernelGGL((kd_dt_bwd<T, 8>), dim3((unsigned)nblk), dim3(kBlock), 0, stream, ra);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "deftet bwd: %s", hipGetErrorString(e));
+  return KD_OK;
 }
 
 }  // namespace kd

@@ -78,17 +78,18 @@ __device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], con
   }
 }
 
-// One workgroup per 16x16 tile.  Every pixel writes its terms to LDS; pixels are grouped by face:
-// an LDS hash table gives each face a slot, the slot's LDS counter gives each pixel its rank
-// among the slot's pixels, a prefix sum over the slots turns (slot, rank) into a position, and
-// the tile sum of each (face, term) is then added by one lane and flushed with one float atomic
-// per (tile, face, term), a face's terms on adjacent lanes (its 6 corner terms and its 3*D
-// feature terms are contiguous in memory).  (Summation order varies with the LDS counters, as it
-// does across tiles with the float atomics.)
-template <typename T, int DMAX, bool VTX = false>
-__device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra, int d, int n,
-                                                     int ntl) {
-  const int H = ra.H, W = ra.W, D = ra.D, dbg = ra.dbg;
+// A workgroup's samples, at most one per lane (p < 0: none), summed per face.  Every sample writes
+// its terms to LDS; samples are grouped by face: an LDS hash table gives each face a slot, the
+// slot's LDS counter gives each sample its rank among the slot's samples, a prefix sum over the
+// slots turns (slot, rank) into a position, and the group sum of each (face, term) is then added
+// by one lane and flushed with one float atomic per (group, face, term), a face's terms on
+// adjacent lanes (its 6 corner terms and its 3*D feature terms are contiguous in memory).
+// (Summation order varies with the LDS counters, as it does across groups with the float atomics.)
+// ROWKEY: the lanes' samples may belong to different views b, so the keys are the rows b*F + f
+// (the launcher checks B*F < 2^31); otherwise all lanes share view b and the keys are faces.
+template <typename T, int DMAX, bool VTX, bool ROWKEY>
+__device__ __forceinline__ void raster_bwd_group(const RasterBwdArgs<T> &ra, int64_t p, int b) {
+  const int D = ra.D, dbg = ra.dbg;
   const int64_t F = ra.F;
   const T *__restrict__ grad = ra.grad;
   const int64_t *__restrict__ face_idx = ra.face_idx;
@@ -103,49 +104,41 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
   // feature terms -- so it is 20 KB instead of 32 and the kernel keeps five workgroups per CU
   constexpr bool kSplit = sizeof(T) == 8;
   constexpr int CW = kSplit ? (3 * DMAX > 6 ? 3 * DMAX : 6) : SMAX;  // table columns
-  // odd row stride (in 4-byte words): a pixel's row write (lanes on different rows, one term)
+  // odd row stride (in 4-byte words): a sample's row write (lanes on different rows, one term)
   // and a slot's column sums (lanes on one row, consecutive terms) are both bank-conflict free
   constexpr int SROW = (CW * (int)sizeof(T) / 4) % 2 ? CW : CW + 1;
-  constexpr int HT = kBlock;  // slots >= distinct faces of a tile
+  constexpr int HT = kBlock;  // slots >= distinct faces of a group
   __shared__ int s_key[HT];
-  __shared__ int s_n[HT];  // pixels per slot (their ranks come from the counter)
+  __shared__ int s_n[HT];  // samples per slot (their ranks come from the counter)
   __shared__ T s_con[kBlock][SROW];
   __shared__ short s_off[HT];
   __shared__ int s_list[HT];
   __shared__ int s_cnt[4];
   const int S = 6 + 3 * D;
   const int tid = threadIdx.x;
-  const int ntx = (W + kTile - 1) / kTile;
-  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (d % 8 is the XCD: callers keep
-  // it so), so XCD x gets the contiguous band of tiles [x n/8, (x+1) n/8): neighbouring tiles
-  // (which share faces) share one L2
-  if ((n & 7) == 0 && !ablate(dbg, (1 << 17))) d = (d & 7) * (n >> 3) + (d >> 3);
-  const int b = d / ntl, tl = d - b * ntl;
-  const int px = (tl % ntx) * kTile + (tid & 15);
-  const int py = (tl / ntx) * kTile + (tid >> 4);
   s_key[tid] = -1;
   s_n[tid] = 0;
   __syncthreads();
   int h = -1, rank = 0;
   T c[SMAX];
-  if (px < W && py < H) {
-    const int64_t p = ((int64_t)b * H + py) * W + px;
-    // the pixel's weights and incoming gradient do not depend on its face: issued with it
+  if (p >= 0) {
+    // the sample's weights and incoming gradient do not depend on its face: issued with it
     const int64_t f = face_idx[p];
     const T wts[3] = {weights[p * 3], weights[p * 3 + 1], weights[p * 3 + 2]};
     T gd[DMAX];
 #pragma unroll
     for (int d = 0; d < DMAX; ++d) gd[d] = d < D ? grad[p * D + d] : (T)0;
     if (f >= 0 && f < F) {
-      unsigned u = ((unsigned)f * 2654435761u) >> 24;
+      const int64_t tf = (int64_t)b * F + f;
+      const int key = ROWKEY ? (int)tf : (int)f;
+      unsigned u = ((unsigned)key * 2654435761u) >> 24;
       for (;;) {  // <= 256 keys in 256 slots: terminates
-        const int old = atomicCAS(&s_key[u], -1, (int)f);
-        if (old == -1 || old == (int)f) break;
+        const int old = atomicCAS(&s_key[u], -1, key);
+        if (old == -1 || old == key) break;
         u = (u + 1) & (HT - 1);
       }
       h = (int)u;
       rank = atomicAdd(&s_n[h], 1);
-      const int64_t tf = (int64_t)b * F + f;
       raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, gd, feat + tf * 3 * D, D, eps, c);
     }
   }
@@ -160,7 +153,7 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
   const int pos = wg_compact(occ, s_cnt, nocc);
   if (occ) s_list[pos] = tid;
   __syncthreads();
-  // the pixel's terms go to its position in slot order, so a slot's terms are contiguous rows;
+  // the sample's terms go to its position in slot order, so a slot's terms are contiguous rows;
   // pass q holds terms [c0, c1) (one pass of all S terms unless kSplit)
   for (int q = 0; q < (kSplit ? 2 : 1); ++q) {
     const int c0 = kSplit && q ? 6 : 0, c1 = kSplit && !q ? 6 : S;
@@ -190,7 +183,7 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
       const int slot = s_list[i];
       const int ns = s_n[slot];
       const int o = s_off[slot];
-      const int64_t row = (int64_t)b * F + s_key[slot];
+      const int64_t row = ROWKEY ? (int64_t)s_key[slot] : (int64_t)b * F + s_key[slot];
       if (VTX && j < ncorner) {
         T vx = (T)0, vy = (T)0;
         for (int r = 0; r < ns; ++r) {  // independent reads: pipelined
@@ -210,6 +203,24 @@ __device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra,
         atomicAdd(grad_feat + row * 3 * D + (jj - 6), v);
     }
   }
+}
+
+// One workgroup per 16x16 tile of a view's pixels (rasterization_cuda.cu:238-402 per pixel).
+template <typename T, int DMAX, bool VTX = false>
+__device__ __forceinline__ void raster_bwd_tile_body(const RasterBwdArgs<T> &ra, int d, int n,
+                                                     int ntl) {
+  const int H = ra.H, W = ra.W;
+  const int tid = threadIdx.x;
+  const int ntx = (W + kTile - 1) / kTile;
+  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (d % 8 is the XCD: callers keep
+  // it so), so XCD x gets the contiguous band of tiles [x n/8, (x+1) n/8): neighbouring tiles
+  // (which share faces) share one L2
+  if ((n & 7) == 0 && !ablate(ra.dbg, (1 << 17))) d = (d & 7) * (n >> 3) + (d >> 3);
+  const int b = d / ntl, tl = d - b * ntl;
+  const int px = (tl % ntx) * kTile + (tid & 15);
+  const int py = (tl / ntx) * kTile + (tid >> 4);
+  const int64_t p = px < W && py < H ? ((int64_t)b * H + py) * W + px : -1;
+  raster_bwd_group<T, DMAX, VTX, false>(ra, p, b);
 }
 
 }  // namespace kd

@@ -300,3 +300,47 @@ def test_forward_dense_soups(dt, size):
     ofi, od, oa0, oa1 = f3.deftet_forward_raw(px, rr, fvz, fvi, bbox, knum)
     for a, b in zip(raw, (ofi, od, oa0, oa1)):
         np.testing.assert_array_equal(a, b)
+
+
+# --------------------------------------------------------------------------------------------
+# the backward C-ABI entry directly (kd_dt_bwd: compacted sample groups), every feature-count
+# template (DMAX 3 / 4 / 8) and the per-sample atomic kernel past 8 features, across views
+# --------------------------------------------------------------------------------------------
+def _c_backward(go, fidx, w, fvi, feat):
+    from kaolin_amd import _lib
+    B, P, K = fidx.shape
+    F, D = fvi.shape[1], feat.shape[-1]
+    sfx = 'f32' if fvi.dtype == torch.float32 else 'f64'
+    gfvi, gfeat = torch.full_like(fvi, 7.), torch.full_like(feat, 7.)  # overwritten (zeroed)
+    _lib.call(f'kd_deftet_sparse_render_backward_{sfx}', B, P, F, K, D, go.data_ptr(),
+              fidx.data_ptr(), w.data_ptr(), fvi.data_ptr(), feat.data_ptr(), 1e-8,
+              gfvi.data_ptr(), gfeat.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    return N(gfvi), N(gfeat)
+
+
+@pytest.mark.parametrize('dt', [np.float32, np.float64])
+@pytest.mark.parametrize('D', [1, 2, 4, 5, 9])
+def test_backward_entry_vs_oracle(dt, D):
+    from kaolin_amd import _C
+    B, knum = 3, 40
+    px, rr, fvz, fvi, _ = soup(B, 2500, 600, dt, 50 + D, nan_faces=3)
+    feat = np.random.default_rng(D).standard_normal((B, 2500, 3, D)).astype(dt)
+    interp, fidx, w = _C.render.mesh.deftet_sparse_render_forward(
+        T(px), T(rr), T(fvz), T(fvi), T(feat), knum, 1e-8)
+    go = np.random.default_rng(7 + D).random(tuple(interp.shape)).astype(dt)
+    gfvi, gfeat = _c_backward(T(go), fidx, w, T(fvi), T(feat))
+    ofvi, ofeat = oracle.rasterize_backward(go, N(fidx), N(w), fvi, feat, 1e-8)
+    np.testing.assert_allclose(gfvi, ofvi, **grad_tol(dt))
+    np.testing.assert_allclose(gfeat, ofeat, **grad_tol(dt))
+
+
+def test_backward_entry_empty():
+    """No occupied sample: the gradients are zeros (buffers preset to 7 are cleared)."""
+    K, F, P = 4, 10, 33
+    fidx = torch.full((2, P, K), -1, dtype=torch.long, device=DEV)
+    w = torch.zeros((2, P, K, 3), device=DEV)
+    go = torch.rand((2, P, K, 3), device=DEV)
+    fvi, feat = torch.rand((2, F, 3, 2), device=DEV), torch.rand((2, F, 3, 3), device=DEV)
+    gfvi, gfeat = _c_backward(go, fidx, w, fvi, feat)
+    assert (gfvi == 0).all() and (gfeat == 0).all()
