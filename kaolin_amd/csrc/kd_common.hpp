@@ -40,7 +40,8 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       16384 return at the start of the raster / soft pass-A tile kernels (dispatch cost),
 //       1 << 24 the fused forward without its soft phase (the raster phase's instruction counts),
 //       1 << 25 the DefTet backward as the raster tile kernel over the P x knum samples,
-//       1 << 27 kd_dt_bwd: the sample compaction only (no per-face sums).
+//       1 << 27 kd_dt_bwd: the sample compaction only (no per-face sums),
+//       1 << 26 kd_dt_fwd: the LDS rank form for every pixel (not only past the wave form).
 #if KD_DIAG
 int debug_flags();
 #else

@@ -129,24 +129,27 @@ __device__ __forceinline__ bool dt_face_weights(T ax, T ay, T bx, T by, T cx, T 
                                                 T z2, T x0, T y0, T dmin, T dmax, T eps, T &w0,
                                                 T &w1, T &depth);
 
-// The reference's per-face test (deftet_cuda.cu:114-160): half-open box of the corner min / max,
-// eps-normalised barycentrics (copysignf of the float eps, also for fp64 data), all >= 0, depth
-// in [min, max).
+// The reference's per-face test (deftet_cuda.cu:114-160): half-open box of the corner min / max
+// (or the caller's face_bboxes), eps-normalised barycentrics (copysignf of the float eps, also for
+// fp64 data), all >= 0, depth in [min, max).  (Reading kd_dt_bin's box table and the depths for
+// every candidate instead measured 192 -> 198 us: more bytes per candidate than the min / max.)
 template <typename T>
-__device__ __forceinline__ bool dt_face_test(const T *v, const T *z, const T *bbox, T x0, T y0,
+__device__ __forceinline__ bool dt_face_test(const T *v, const T *z, const T *box, T x0, T y0,
                                              T dmin, T dmax, T eps, T &w0, T &w1, T &depth) {
   const T ax = v[0], ay = v[1], bx = v[2], by = v[3], cx = v[4], cy = v[5];
   T xmin, xmax, ymin, ymax;
-  if (bbox) {
-    xmin = bbox[0];
-    ymin = bbox[1];
-    xmax = bbox[2];
-    ymax = bbox[3];
+  if (box) {
+    xmin = box[0];
+    ymin = box[1];
+    xmax = box[2];
+    ymax = box[3];
   } else {
-    xmin = nmin3(ax, bx, cx);
-    xmax = nmax3(ax, bx, cx);
-    ymin = nmin3(ay, by, cy);
-    ymax = nmax3(ay, by, cy);
+    // listed faces have no NaN corner (kd_dt_bin drops NaN boxes), so the plain min / max equal
+    // the NaN-propagating ones here (and +-0 compare equal): v_min3 / v_max3, no branches
+    xmin = fmin(fmin(ax, bx), cx);
+    xmax = fmax(fmax(ax, bx), cx);
+    ymin = fmin(fmin(ay, by), cy);
+    ymax = fmax(fmax(ay, by), cy);
   }
   if (!(x0 >= xmin && x0 < xmax && y0 >= ymin && y0 < ymax)) return false;
   return dt_face_weights<T>(ax, ay, bx, by, cx, cy, z[0], z[1], z[2], x0, y0, dmin, dmax, eps, w0,
@@ -203,6 +206,85 @@ constexpr int kDtWaves = 4;  // pixels per workgroup
 template <typename T>
 __host__ __device__ constexpr size_t dt_wave_lds(int C) {  // depth, w0, w1, face, face rank
   return (size_t)C * (3 * sizeof(T) + 2 * sizeof(int));
+}
+
+// The pixel's outputs when its hits fit the wave without the first-K cut (nh <= 64, and nh <= K
+// unless op form).  Lanes form (hit i, group g) pairs: NI >= nh lanes a group, G = 64 / NI
+// groups; lane (i, g) compares hit i with hits j = g, g + G, ... and the groups' counts are summed
+// by lane shuffles, so a rank costs nh / G comparisons instead of nh.  The same comparisons as the
+// LDS form below (bit-identical outputs).
+template <typename T>
+__device__ __forceinline__ void dt_pixel_out_wave(const DtArgs<T> &a, int b, int64_t row, int nh,
+                                                  const T *dep, const T *lw0, const T *lw1,
+                                                  const int *fid) {
+  const int lane = threadIdx.x & 63;
+  const int K = a.K;
+  const int lg = nh <= 1 ? 0 : 32 - __builtin_clz((unsigned)(nh - 1));  // NI = 2^lg >= nh
+  const int NI = 1 << lg, G = kWave >> lg;
+  const int i = lane & (NI - 1), g = lane >> lg;
+  const bool has = i < nh;
+  T di = (T)0;
+  int fi = INT_MAX;
+  if (has) {
+    di = dep[i];
+    fi = fid[i];
+  }
+  int r = 0;
+  if (a.depth) {  // op form: slot = face rank among the hits (deftet_cuda.cu:166-180)
+    if (has) {
+#pragma unroll 4
+      for (int j = g; j < nh; j += G) r += fid[j] < fi ? 1 : 0;
+    }
+  } else {  // depth descending, then face index (deftet.py:300-303, stable order)
+    if (has) {
+#pragma unroll 4
+      for (int j = g; j < nh; j += G) {
+        const T dj = dep[j];
+        r += (dj > di || (dj == di && fid[j] < fi)) ? 1 : 0;
+      }
+    }
+  }
+  for (int s = NI; s < kWave; s <<= 1) r += __shfl_xor(r, s);
+  const bool st = has && g == 0;
+  const int n = min(nh, K);
+  if (a.depth) {  // unsorted; the empty slots keep -1 / -inf / 0 / 0 (deftet.cpp:88-94)
+    if (st && r < K) {
+      a.face_idx[row + r] = fi;
+      a.depth[row + r] = di;
+      a.w0[row + r] = lw0[i];
+      a.w1[row + r] = lw1[i];
+    }
+    for (int s = n + lane; s < K; s += kWave) {
+      a.face_idx[row + s] = -1;
+      a.depth[row + s] = (T)-INFINITY;
+      a.w0[row + s] = (T)0;
+      a.w1[row + s] = (T)0;
+    }
+    return;
+  }
+  const int D = a.D;
+  if (st) {
+    const T *feat = a.feat + (int64_t)b * a.F * 3 * D;
+    const T w0 = lw0[i], w1 = lw1[i];
+    const T w2 = (T)1 - (w0 + w1);  // deftet.py:304
+    const int64_t o = row + r;
+    a.face_idx[o] = fi;
+    a.weights[3 * o] = w0;
+    a.weights[3 * o + 1] = w1;
+    a.weights[3 * o + 2] = w2;
+    const T *cf = feat + (int64_t)fi * 3 * D;
+    T *out = a.interp + o * D;
+    for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
+      out[d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+  }
+  for (int s = n + lane; s < K; s += kWave) {
+    const int64_t o = row + s;
+    a.face_idx[o] = -1;
+    a.weights[3 * o] = (T)0;
+    a.weights[3 * o + 1] = (T)0;
+    a.weights[3 * o + 2] = (T)0;
+    for (int d = 0; d < D; ++d) a.interp[o * D + d] = (T)0;
+  }
 }
 
 // One wave per pixel.  The pixel's cell list is walked 64 faces at a time (lane = face, the
@@ -274,9 +356,13 @@ __device__ void dt_pixel_wave(const DtArgs<T> &a, int b, int64_t p, char *wave_l
     nh = walk(lo + 1, true);  // exactly K hits: faces <= the K-th smallest
   }
   wave_lds_sync();
+  const int64_t row = pp * K;
+  if (nh <= kWave && (a.depth || nh <= K) && !ablate(a.dbg, 1 << 26)) {
+    dt_pixel_out_wave<T>(a, b, row, nh, dep, lw0, lw1, fid);
+    return;
+  }
   // the reference keeps the first K hits by face index: mark the others (face rank >= K)
   int *frank = fid + C;
-  const int64_t row = pp * K;
   if (a.depth) {
     // op form: slot = face rank among the hits (the reference kernel's insertion order,
     // deftet_cuda.cu:166-180), unsorted; the empty slots keep -1 / -inf / 0 / 0
