@@ -242,7 +242,10 @@ __device__ __forceinline__ void tex_seg_sum16(const bool take[4], T v[N]) {
 // background of an image loss) add nothing and are skipped.  The uv gradient is per sample.
 template <typename T, int MODE>
 __global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) {
-  constexpr int kLds = 32768 / sizeof(T);
+  // 20 KB of texel sums: eight workgroups per CU (with s_red, under 160 KB / 8), and C3's block
+  // footprints still fit (32 KB: five per CU, 121.7 -> 113.4 us; 8 KB sends blocks to the
+  // global-atomic fallback, 148 us)
+  constexpr int kLds = 20416 / sizeof(T);
   __shared__ T s_acc[kLds];
   __shared__ int s_red[8];
   const int b = blockIdx.y;
