@@ -201,7 +201,7 @@ struct DtArgs {
   long long *tbuf;    // diagnostics (flag 64): candidate / hit / fallback / flush counters
 };
 
-constexpr int kDtWaves = 4;  // pixels per workgroup
+constexpr int kDtWaves = 1;  // pixels per workgroup: one wave (finer dispatch of uneven pixels)
 
 template <typename T>
 __host__ __device__ constexpr size_t dt_wave_lds(int C) {  // depth, w0, w1, face, face rank
