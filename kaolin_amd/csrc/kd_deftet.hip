@@ -315,13 +315,16 @@ __device__ void dt_pixel_wave(const DtArgs<T> &a, int b, int64_t p, char *wave_l
   // walk: hits with face < limit are appended (limit = F: all)
   auto walk = [&](int limit, bool store) {
     int num = 0;
+    int fn = lane < nl ? list[lane] : 0;  // the next step's list entry, loaded a step ahead
     for (int j0 = 0; j0 < nl; j0 += kWave) {
       const int j = j0 + lane;
       bool hit = false;
       T w0 = 0, w1 = 0, depth = 0;
       int f = 0;
+      const int fc = fn;
+      if (j + kWave < nl) fn = list[j + kWave];
       if (j < nl) {
-        f = list[j];
+        f = fc;
         if (f < limit)
           hit = dt_face_test<T>(fvi + (int64_t)f * 6, fvz + (int64_t)f * 3,
                                 bbox ? bbox + (int64_t)f * 4 : nullptr, x0, y0, dmin, dmax, eps,
