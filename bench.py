@@ -16,7 +16,9 @@ runs it eagerly); the all-reduce stays an eager RCCL call.  Every kernel of the 
 every replay.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3] [--dtype f32|f64]
-For N > 1 launch with torch.distributed.run (see README / the driver contract).
+For N > 1 the driver launches it with torch.distributed.run; without WORLD_SIZE in the
+environment `--gpus N` starts the N ranks itself (the same torch.distributed.run command, as a
+child process, before any GPU call).
 """
 import argparse
 import json
@@ -217,11 +219,15 @@ class Workload:
         for p in self.params:
             p.grad = None
 
+    def exchange(self):
+        """The step's one collective: the sum over ranks of the shared vertex gradient."""
+        if not self.soup:
+            distributed.allreduce_grads_([self.vertices.grad])
+
     def eager_step(self):
         self.clear()
         face_idx = self.forward_backward()
-        if not self.soup:
-            distributed.allreduce_grads_([self.vertices.grad])
+        self.exchange()
         return face_idx
 
     def inputs(self):
@@ -249,7 +255,7 @@ def make_step(wl, use_graph):
     return wl.eager_step, 'eager'
 
 
-def timed(step, steps, warmup, dev, world):
+def timed(step, steps, warmup, dev, world, wl=None):
     """W untimed steps, then exactly K steps between barrier + synchronize on both sides; the
     wall time is the max over ranks (nothing else is enqueued in that region).  Then K more steps,
     each bracketed by HIP events on the current stream (the replay, and for a GraphedStep at N > 1
@@ -269,14 +275,20 @@ def timed(step, steps, warmup, dev, world):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     # the per-step event pass (not part of the timed region)
-    split = isinstance(step, distributed.GraphedStep) and world > 1
+    graphed = isinstance(step, distributed.GraphedStep)
+    split = world > 1 and (graphed or wl is not None)
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
     for e in ev:
         e[0].record()
-        if split:
+        if split and graphed:
             step.replay()
             e[1].record()
             step.exchange()
+        elif split:  # the eager step in its two parts: the render, then the all-reduce
+            wl.clear()
+            wl.forward_backward()
+            e[1].record()
+            wl.exchange()
         else:
             step()
         e[2].record()
@@ -342,6 +354,37 @@ def load_pmc(path, config, dtype, lists, views):
     return out, os.path.relpath(path, ROOT)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(n, argv, port):
+    """The torch.distributed.run command that starts `n` ranks of this script on one node (the
+    driver's own form of the N > 1 launch; rendezvous on 127.0.0.1)."""
+    return [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+            '--master-addr', '127.0.0.1', '--master-port', str(port),
+            os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(n, argv):
+    """`python bench.py --gpus N` without WORLD_SIZE: launch N ranks (one per GPU; with
+    KD_BENCH_BACKEND=gloo they may share one) as a child torch.distributed.run and return its
+    exit status.  Nothing here initialises the GPU: torch.cuda.device_count() does not on this
+    stack, and no HIP call is made before the children exit."""
+    backend = os.environ.get('KD_BENCH_BACKEND', 'nccl')
+    visible = torch.cuda.device_count()
+    if backend == 'nccl' and visible < n:
+        print(f'[bench] --gpus {n}: only {visible} GPU(s) visible (RCCL needs one per rank)',
+              file=sys.stderr)
+        return 2
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')  # dmabuf IPC (RCCL peer buffers)
+    return subprocess.call(launcher_cmd(n, argv, free_port()), env=env)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -382,6 +425,10 @@ def main():
     ap.add_argument('--pmc', default=None,
                     help='PMC traffic summary (default profiles/r05, r04, r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        # one process per GPU: started here, before anything touches the GPU (this process only
+        # waits for them and exits with their status)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     # KD_BENCH_BACKEND=gloo rehearses the multi-rank path on a single GPU (ranks share cuda:0;
     # RCCL refuses two ranks on one device).  The default is RCCL ("nccl").
@@ -413,7 +460,8 @@ def main():
         if wl.perturb:  # the workload's coverage before the mesh moves
             covered0 = int((wl.eager_step() >= 0).sum().item())
         step, launch = make_step(wl, use_graph)
-        elapsed, evt = timed(step, args.steps, args.warmup, dev, world)
+        elapsed, evt = timed(step, args.steps, args.warmup, dev, world,
+                             wl if step == wl.eager_step else None)
     ms_per_step = elapsed * 1e3 / args.steps
     step_median = _median_over_ranks(evt['step_ms'], dev, world)
     ar_median = _median_over_ranks(evt['allreduce_ms'], dev, world) if world > 1 else None
@@ -513,11 +561,11 @@ def main():
                     'busy': 'SQ_ACTIVE_INST_VALU (quad-cycles, summed over waves) x 4 / (SIMDs x '
                             'clock): the cycles the SIMDs measured executing VALU instructions',
                     'source': f'{pmc_src}: {e["device_kernel"]}, SQ_INSTS_VALU_* per launch'}
-        # the bound is the larger of the roof fractions (the HBM figures stay the contract's
-        # achieved / peak / frac)
+        # the contract's bound is "hbm" | "mfma": this path has no MFMA work, so "hbm" with the
+        # byte fraction; `limiter` names the larger of the roof fractions (VALU issue here)
         vf = max(valu.get('frac') or 0, valu.get('busy_frac') or 0) if valu else 0
-        bound = 'valu' if valu and hbm_frac is not None and vf > hbm_frac else 'hbm'
-        roofline = {'kernel': dom, 'bound': bound,
+        limiter = 'valu_issue' if valu and hbm_frac is not None and vf > hbm_frac else 'hbm'
+        roofline = {'kernel': dom, 'bound': 'hbm', 'limiter': limiter,
                     'achieved': None if achieved is None else round(achieved, 1),
                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                     'frac': None if hbm_frac is None else round(hbm_frac, 4),

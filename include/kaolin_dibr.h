@@ -88,12 +88,23 @@ int kd_set_tile_split(int split);
 int kd_set_coarse_tile(int px);
 
 /* Tile cost history of dibr_rasterization's fp32 forward (a tuning hook; 1 by default).  The
- * one-launch forward records each 16x16 tile's duration in a library-owned device buffer (one
- * per device, 2 MB, kept for the process), and the next call of the same shape dispatches its
- * tiles heaviest-first by those durations instead of by their coarse bins' face counts (a
- * silhouette tile's soft-mask work shows only after its raster phase).  Results never depend
- * on it; 0 turns it off. */
+ * one-launch forward records each 16x16 tile's duration in a CALLER-OWNED device buffer (one per
+ * device, attached with kd_tile_history_attach), and the next call of the same shape dispatches
+ * its tiles heaviest-first by those durations instead of by their coarse bins' face counts (a
+ * silhouette tile's soft-mask work shows only after its raster phase).  Results never depend on
+ * it; 0 turns it off, and so does attaching no buffer. */
 int kd_set_tile_history(int on);
+
+/* Bytes of one device's tile history buffer (2 MB). */
+size_t kd_tile_history_bytes(void);
+
+/* Attach a caller-owned device buffer of >= kd_tile_history_bytes() bytes as the tile history of
+ * the device `stream` belongs to (NULL detaches).  The library never allocates or frees it and
+ * keeps only its address: the caller keeps it alive while any call or captured graph on that
+ * device may use it (kaolin_amd._C allocates one per device from the PyTorch caching allocator
+ * and holds it for the process).  Every stream, thread and graph of the device shares it; the
+ * library zeroes it on the stream when the call's shape changes outside a capture. */
+int kd_tile_history_attach(void *stream, void *device_buffer, size_t bytes);
 
 /* Pool limits (a test and tuning hook; both 1 by default).  The workspaces hold two bounded
  * pools whose layout depends only on the call's sizes: the coarse bins (16 entries per face row)

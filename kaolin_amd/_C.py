@@ -444,8 +444,13 @@ def dibr_rasterization_forward_fused(height, width, face_vertices_z, face_vertic
     face_idx = torch.empty((B, height, width), device=dev, dtype=torch.long)
     weights = torch.empty((B, height, width, 3), **opts)
     soft = torch.empty((B, height, width), **opts)
+    if with_lists and iou_gt is not None:
+        raise ValueError(f'{fn}: the close-face lists (with_lists) and the fused mask_iou '
+                         f'(iou_gt) cannot be combined')
     nb = int(_lib.load().kd_dibr_workspace_size(B, height, width, F, knum,
                                                 1 if fvi.dtype == torch.float64 else 0))
+    if fvi.dtype == torch.float32:
+        _lib.tile_history_buffer(dev)  # the caller-owned tile history (kd_tile_history_attach)
     ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
     if iou_gt is not None:
         _check_size(fn, 'gt_mask', iou_gt, (B, height, width))
@@ -522,6 +527,8 @@ def dibr_rasterization_forward_vertices(height, width, vertices, faces, camera_p
     soft = torch.empty((B, height, width), **opts)
     nb = int(_lib.load().kd_dibr_workspace_size(B, height, width, F, knum,
                                                 1 if vertices.dtype == torch.float64 else 0))
+    if vertices.dtype == torch.float32:
+        _lib.tile_history_buffer(dev)
     ws = torch.empty((max(nb, 1),), dtype=torch.uint8, device=dev)
     _lib.call(f'kd_dibr_rasterization_forward_vertices_{sfx}', B, height, width, Bv, V, F, D,
               _ptr(vertices), _ptr(faces), _ptr(camera_proj), _ptr(camera_transform), _ptr(feat),

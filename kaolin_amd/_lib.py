@@ -143,6 +143,10 @@ def load():
             lib.kd_set_coarse_tile.restype = c_int
             lib.kd_set_tile_history.argtypes = [c_int]
             lib.kd_set_tile_history.restype = c_int
+            lib.kd_tile_history_bytes.argtypes = []
+            lib.kd_tile_history_bytes.restype = c_size
+            lib.kd_tile_history_attach.argtypes = [c_p, c_p, c_size]
+            lib.kd_tile_history_attach.restype = c_int
             lib.kd_prepare_vertices_ranges.argtypes = [c_p, c_i64, ctypes.c_int32, c_p]
             lib.kd_prepare_vertices_ranges.restype = c_i64
             # diagnostic build only (A/B of kernel variants under the test suite): KD_DEBUG_FLAGS
@@ -219,6 +223,36 @@ def set_tile_history(on=True):
     (kd_set_tile_history, a tuning hook; on by default).  Results never depend on it."""
     if load().kd_set_tile_history(1 if on else 0) != KD_OK:
         raise RuntimeError(load().kd_last_error().decode(errors='replace'))
+
+
+_history = {}  # device index -> the caller-owned tile history buffer (kd_tile_history_attach)
+
+
+def tile_history_buffer(dev):
+    """The tile history buffer attached for `dev` (a torch.device), allocating and attaching it
+    on first use -- caller-owned memory from the caching allocator, held for the process so that
+    captured graphs keep a valid address.  None inside a stream capture before one exists (no
+    allocation there; that call runs without history)."""
+    import torch
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    buf = _history.get(idx)
+    if buf is not None:
+        return buf
+    if torch.cuda.is_current_stream_capturing():
+        return None
+    lib = load()
+    with _lock:
+        buf = _history.get(idx)
+        if buf is None:
+            nb = int(lib.kd_tile_history_bytes())
+            d = torch.device('cuda', idx)
+            buf = torch.zeros((nb,), dtype=torch.uint8, device=d)
+            rc = lib.kd_tile_history_attach(torch.cuda.current_stream(d).cuda_stream,
+                                            buf.data_ptr(), nb)
+            if rc != KD_OK:
+                raise RuntimeError(lib.kd_last_error().decode(errors='replace'))
+            _history[idx] = buf
+    return buf
 
 
 def debug_set(flags):

@@ -50,47 +50,45 @@ int device_cus(hipStream_t stream) {
 std::atomic<int> g_hist{1};
 namespace {
 struct HistSlot {
-  unsigned short *buf = nullptr;
+  unsigned short *buf = nullptr;  // the caller's buffer (kd_tile_history_attach), not owned
   long long tag = -1;
 };
 HistSlot g_hist_slots[kMaxDevices];
 std::mutex g_hist_mu;
 }  // namespace
-// One buffer per device for the whole process: streams, threads and captured graphs of that
-// device share it.  Sharing can only degrade the dispatch order (tile_order reads
-// each entry once, so any history gives a permutation of the tiles), never a result.
+// One caller-owned buffer per device (kd_tile_history_attach): streams, threads and captured
+// graphs of that device share it.  Sharing can only degrade the dispatch order
+// (tile_order reads each entry once, so any history gives a permutation of the tiles), never a
+// result.  The library allocates nothing here: without an attached buffer there is no history.
 unsigned short *tile_history(int64_t n, long long tag, hipStream_t stream) {
   if (!g_hist.load() || n <= 0 || n > kTileHistCap) return nullptr;
   const int dev = stream_device(stream);  // the device the launches will run on
   if (dev < 0 || dev >= kMaxDevices) return nullptr;
   std::lock_guard<std::mutex> lk(g_hist_mu);
   HistSlot &h = g_hist_slots[dev];
-  if (h.buf && h.tag == tag) return h.buf;  // the common case: no allocation, no capture query
-  // a first allocation or a new shape: only outside a stream capture (no allocation inside one,
-  // and a captured zero fill would clear the history on every replay)
+  if (!h.buf) return nullptr;
+  if (h.tag == tag) return h.buf;  // the common case: no fill, no capture query
+  // a new shape: only outside a stream capture (a captured zero fill would clear the history on
+  // every replay)
   hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(stream, &st) != hipSuccess || st != hipStreamCaptureStatusNone)
     return nullptr;
-  if (!h.buf) {
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess) return nullptr;
-    void *p = nullptr;
-    // allocated on the stream's device (a device guard around hipMalloc), whatever is current
-    const bool switched = cur != dev && hipSetDevice(dev) == hipSuccess;
-    const hipError_t ea = (cur == dev || switched)
-                              ? hipMalloc(&p, sizeof(unsigned short) * (size_t)kTileHistCap)
-                              : hipErrorInvalidDevice;
-    if (switched) (void)hipSetDevice(cur);
-    if (ea != hipSuccess) {
-      (void)hipGetLastError();  // (no history: the caller's own launch checks stay clean)
-      return nullptr;
-    }
-    h.buf = (unsigned short *)p;
-    h.tag = -1;
-  }
   if (zero_words(h.buf, sizeof(unsigned short) * (size_t)n, stream) != hipSuccess) return nullptr;
   h.tag = tag;
   return h.buf;
+}
+int tile_history_attach(hipStream_t stream, void *buf, size_t bytes) {
+  const int dev = stream_device(stream);
+  if (dev < 0 || dev >= kMaxDevices)
+    return set_error(KD_ERR_INVALID_ARGUMENT, "tile history: device %d out of range", dev);
+  if (buf && bytes < sizeof(unsigned short) * (size_t)kTileHistCap)
+    return set_error(KD_ERR_INVALID_ARGUMENT, "tile history: %zu bytes < %zu", bytes,
+                     sizeof(unsigned short) * (size_t)kTileHistCap);
+  std::lock_guard<std::mutex> lk(g_hist_mu);
+  HistSlot &h = g_hist_slots[dev];
+  h.buf = (unsigned short *)buf;
+  h.tag = -1;  // zeroed by the next forward of any shape
+  return KD_OK;
 }
 std::atomic<long long *> g_tbuf{nullptr};
 std::atomic<float> g_lim_bins{1.f}, g_lim_pairs{1.f};
@@ -188,6 +186,12 @@ int kd_set_tile_history(int on) {
     return kd::set_error(KD_ERR_INVALID_ARGUMENT, "tile history must be 0 or 1 (got %d)", on);
   kd::g_hist.store(on);
   return KD_OK;
+}
+
+size_t kd_tile_history_bytes(void) { return sizeof(unsigned short) * (size_t)kd::kTileHistCap; }
+
+int kd_tile_history_attach(void *stream, void *device_buffer, size_t bytes) {
+  return kd::tile_history_attach((hipStream_t)stream, device_buffer, bytes);
 }
 
 int kd_set_pool_limits(double bins, double pairs) {

@@ -58,12 +58,14 @@ int coarse_tile_hook();
 int stream_device(hipStream_t stream);
 // compute units of the stream's device (cached per device on first use; 256 when unknown)
 int device_cus(hipStream_t stream);
-// Tile cost history of the fused fp32 DIB-R forward (kd_set_tile_history): a library-owned
-// device buffer of kTileHistCap ushort entries per device, never freed (captured graphs keep
-// its address), zeroed on the stream when `tag` (the call's shape) changes outside a capture.
-// nullptr: history off, too many entries, or a new shape inside a stream capture.
+// Tile cost history of the fused fp32 DIB-R forward (kd_set_tile_history): a caller-owned
+// device buffer of kTileHistCap ushort entries per device (kd_tile_history_attach; the caller
+// keeps it alive while captured graphs use it), zeroed on the stream when `tag` (the call's
+// shape) changes outside a capture.  nullptr: history off, no buffer attached for the stream's
+// device, too many entries, or a new shape inside a stream capture.
 constexpr int64_t kTileHistCap = 1 << 20;
 unsigned short *tile_history(int64_t n, long long tag, hipStream_t stream);
+int tile_history_attach(hipStream_t stream, void *buf, size_t bytes);
 long long *debug_tile_buffer();  // kd_debug_buffer (flag 64), else nullptr
 
 // Per-workgroup duration (wall clock, 100 MHz ticks) for diagnostics: written by thread 0 when
@@ -72,16 +74,16 @@ struct TileClock {
   long long *buf;
   long long t0;
   int64_t idx;
-  __device__ TileClock(long long *b, int slot)
+  __device__ __forceinline__ TileClock(long long *b, int slot)
       : buf(KD_DIAG ? b : nullptr), t0(KD_DIAG && b ? wall_clock64() : 0),
         idx((int64_t)slot * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x +
             blockIdx.x) {}
-  __device__ ~TileClock() {
-    if (buf && threadIdx.x == 0) buf[idx] = wall_clock64() - t0;
+  __device__ __forceinline__ ~TileClock() {
+    if (KD_DIAG && buf && threadIdx.x == 0) buf[idx] = wall_clock64() - t0;
   }
   // diagnostics: also the start time, in `slot` (dispatch slot order)
-  __device__ void start_to(int slot) const {
-    if (buf && threadIdx.x == 0)
+  __device__ __forceinline__ void start_to(int slot) const {
+    if (KD_DIAG && buf && threadIdx.x == 0)
       buf[(int64_t)slot * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
           t0;
   }

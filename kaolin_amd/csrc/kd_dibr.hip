@@ -110,6 +110,7 @@ static int dibr_fwd(int B, int H, int W, int64_t F, int D, const T *fvz, int64_t
     return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
   KD_CHECK_ARG(!iou.gt || (iou.loss && iou.stats && iou.acc), "mask_iou: NULL output");
   KD_CHECK_ARG(!prob == !cidx && !prob == !ctype, "close lists: give all three outputs or none");
+  KD_CHECK_ARG(!prob || F < (1ll << 28), "close lists: more than 2^28 faces per view");
   KD_CHECK_ARG(!iou.gt || (K <= kFuseSlots && pool_limit_pairs() >= 1.f &&
                             !(test_forms() & KD_FORM_SOFT_SPLIT)),
                "fused mask_iou needs knum <= 32 (the one-launch soft mask)");

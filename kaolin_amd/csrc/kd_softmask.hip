@@ -241,13 +241,12 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
       gsv = grad_soft[p];
       sov = soft[p];
     }
-    // a listed pixel needs its rows read unless every term of its row is exactly zero: soft 0
-    // (every probability 0, e.g. no close face at all: most uncovered pixels), soft 1 (the
-    // factor 1 - soft) or a zero incoming gradient -- with both finite (a NaN or inf must reach
-    // the gradients as in the reference).  This replaces a read of each uncovered pixel's first
-    // slot (a cache line per pixel) before the compaction.
-    const bool zero_terms = (sov == (T)0 || sov == (T)1 || gsv == (T)0) && isfinite(sov) &&
-                            isfinite(gsv);
+    // a listed pixel needs its rows read unless every term of its row is exactly zero: soft 1
+    // (the factor 1 - soft) or a zero incoming gradient -- with both finite (a NaN or inf must
+    // reach the gradients as in the reference).  soft 0 is NOT such a case: it only says that
+    // every 1 - prob rounded to 1 (dibr_soft_mask_cuda.cu:174-181), and a probability of ~2^-25
+    // still gives the nonzero terms dLdz * geometry of dibr_soft_mask_cuda.cu:283-348.
+    const bool zero_terms = (sov == (T)1 || gsv == (T)0) && isfinite(sov) && isfinite(gsv);
     const bool live = in && fi < 0 && !zero_terms;
     int n;
     const int pos = wg_compact(live, s_cnt, n);  // (its barriers also order the table reset)

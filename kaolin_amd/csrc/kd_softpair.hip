@@ -1279,8 +1279,8 @@ static void ovf_bwd_launch(const SoftArgs<T> &a, const SoftPairBuf<T> &pb, hipSt
 // lists from the streaming walk (the split form), then the lists writer over the records.
 template <typename T>
 static int lists_after_one_launch(const SoftArgs<T> &a, SoftPairBuf<T> &pb, hipStream_t stream) {
+  // (F < 2^28 was checked before the first launch: dibr_fwd, soft_pairs_launch)
   if (pool_may_overflow(a.K)) ovf_fwd_launch<T, false>(a, pb, stream);
-  KD_CHECK_ARG(a.fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
   SoftArgs<T> al = a;  // (the backward's zero fills were the one launch's side job)
   al.nzero0 = al.nzero1 = 0;
   al.soft = nullptr;  // (and the soft mask)
@@ -1294,6 +1294,9 @@ template <typename T>
 int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce,
                       hipStream_t stream) {
   const FaceSet<T> &fs = a.fs;
+  // the close lists pack (face << 3 | type) into an int: checked before any launch, so a refused
+  // call writes no output
+  KD_CHECK_ARG(!a.prob || fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
   a.fs.dbg = debug_flags();
   a.fs.tbuf = debug_tile_buffer();
   // one launch for the whole soft mask (knum <= 32); with the close-face lists (the op form,
@@ -1335,7 +1338,6 @@ int soft_pairs_launch(SoftArgs<T> &a, SoftPairBuf<T> &pb, bool grad, bool reduce
   if (reduce && a.soft) {
     ProfScope prof(K_SOFT_REDUCE, stream);
     if (a.prob) {  // soft mask + the close lists, row-coalesced (dynamic LDS past 64 KB)
-      KD_CHECK_ARG(fs.F < (1ll << 28), "close lists: more than 2^28 faces per view");
       const size_t dyn = ((sizeof(T) + sizeof(int)) * (kReduceSlots + 1) + sizeof(int)) * kBlock / 2;
       if (dyn > 64 * 1024) {  // (34 KB fp32, 51 KB fp64: within the default limit)
         const hipError_t ea = hipFuncSetAttribute((const void *)kd_soft_lists<T>,

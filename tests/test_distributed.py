@@ -361,3 +361,16 @@ def test_bench_workload_sharded_world2():
     assert np.abs(ref).sum() > 0
     for _, g in res:
         np.testing.assert_allclose(g, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_bench_launcher_cmd():
+    """bench.py --gpus N without WORLD_SIZE starts its N ranks with the driver's own launch form
+    (torch.distributed.run, one node, rendezvous on 127.0.0.1) and passes its arguments on."""
+    import bench
+    cmd = bench.launcher_cmd(4, ['--gpus', '4', '--steps', '5'], 29555)
+    assert cmd[1:4] == ['-m', 'torch.distributed.run', '--nnodes=1']
+    assert '--nproc-per-node=4' in cmd
+    i = cmd.index('--master-addr')
+    assert cmd[i + 1] == '127.0.0.1' and cmd[i + 2:i + 4] == ['--master-port', '29555']
+    assert cmd[-5].endswith('bench.py') and cmd[-4:] == ['--gpus', '4', '--steps', '5']
+    assert 0 < bench.free_port() < 65536

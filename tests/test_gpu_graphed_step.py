@@ -186,3 +186,26 @@ def test_graphed_step_two_ranks(tmp_path):
     r1 = torch.load(tmp_path / 'rank1.pt', weights_only=True)
     for k in ('gv', 'gf'):
         torch.testing.assert_close(r0[k], r1[k], rtol=0, atol=0)
+
+
+def test_bench_starts_its_own_ranks():
+    """`bench.py --gpus 2` without WORLD_SIZE launches its two ranks itself: with
+    the gloo backend both share this box's one GPU; the JSON line reports n_gpus 2 and the
+    all-reduce's own time."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT')}
+    env['KD_BENCH_BACKEND'] = 'gloo'
+    r = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2',
+                        '--views-per-gpu', '1', '--steps', '3', '--warmup', '1', '--no-weak',
+                        '--config', 'c2'], capture_output=True, text=True, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [x for x in r.stdout.splitlines() if x.startswith('{')][-1]
+    out = json.loads(line)
+    assert out['n_gpus'] == 2
+    assert out['config']['global_batch'] == 2
+    assert out['allreduce_us'] is not None and out['allreduce_us'] > 0

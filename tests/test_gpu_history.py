@@ -1,6 +1,7 @@
 """GPU: the tile cost history of the fused fp32 DIB-R forward (kd_set_tile_history).
 
-Each call of the one-launch forward records its tiles' durations in a library-owned buffer, and
+Each call of the one-launch forward records its tiles' durations in a caller-owned buffer
+(kd_tile_history_attach; kaolin_amd._C attaches one per device from the caching allocator), and
 the next call of the same shape dispatches its tiles heaviest-first by them (tile_order) instead
 of by the coarse bins' face counts.  Only the dispatch order changes, so the outputs must be
 bit-identical to a call without history -- also when the history comes from another mesh of the
@@ -67,6 +68,32 @@ def test_history_ragged_vs_oracle(split, hw):
     _run(h, w, v, True)
     out = _run(h, w, v, True)
     _check_view(h, w, 0, out)
+
+
+def test_history_buffer_is_the_callers():
+    """the forward records into the buffer the caller attached (the library allocates nothing),
+    and with the buffer detached (no history) the outputs are the same"""
+    from kaolin_amd import _lib, workloads
+    h = w = 256
+    v = workloads.sphere_views(100, 51, h, w, 2, DEV)
+    buf = _lib.tile_history_buffer(torch.device(DEV))
+    out = _run(h, w, v, True)
+    torch.cuda.synchronize()
+    assert buf.numel() == _lib.load().kd_tile_history_bytes()
+    assert int((buf != 0).sum().item()) > 0, 'the forward did not record into the attached buffer'
+    lib = _lib.load()
+    stream = torch.cuda.current_stream(buf.device).cuda_stream
+    assert lib.kd_tile_history_attach(stream, None, 0) == 0
+    try:
+        buf.zero_()
+        none = _run(h, w, v, True)
+        torch.cuda.synchronize()
+        assert int((buf != 0).sum().item()) == 0, 'a detached buffer was written'
+    finally:
+        assert lib.kd_tile_history_attach(stream, buf.data_ptr(), buf.numel()) == 0
+    _same(none, out)
+    # too small a buffer is refused
+    assert lib.kd_tile_history_attach(stream, buf.data_ptr(), 16) != 0
 
 
 @pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,

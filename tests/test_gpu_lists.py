@@ -145,3 +145,26 @@ def test_close_lists_fused_matches_composition(dname):
     tol = 1e-4 if dname == 'f32' else 1e-9
     for a, b in zip(out[True][3:], out[False][3:]):
         np.testing.assert_allclose(a, b, rtol=tol, atol=tol * 0.1 * np.abs(b).max())
+
+
+def test_op_backward_soft_zero_rows_keep_their_terms():
+    """soft == 0 only says that every 1 - prob rounded to 1; with boxlen 0.05 and
+    sigmainv 30000 many rows hold probabilities of ~1e-30..3e-8 under a soft mask of exactly 0,
+    and their terms dLdz * geometry (dibr_soft_mask_cuda.cu:283-348) are nonzero.  The incoming
+    gradient is nonzero on those pixels only, so a backward that skipped them would return 0."""
+    from kaolin_amd import _C
+    fvi, face_idx = _view(100, 51, 256, 2, torch.float32, elevation=0.7)
+    sig, box, K, M = 30000., 0.05, 30, 1000.
+    soft, _, prob, cidx, ctype = _C.render.mesh.dibr_soft_mask_forward_fused(
+        fvi, face_idx, sig, box, K, M, with_lists=True, want_grad=False)
+    zero_rows = (soft == 0) & (prob[..., 0] > 0) & (face_idx < 0)
+    assert int(zero_rows.sum()) > 100, 'the case needs soft == 0 rows with probabilities'
+    gs = zero_rows.to(torch.float32)
+    sfvi = (fvi * M).contiguous()
+    ref = oracle.soft_mask_backward(N(gs), N(soft), N(face_idx), N(prob), N(cidx), N(ctype),
+                                    N(sfvi), sig, M)
+    gop = _C.render.mesh.dibr_soft_mask_backward_cuda(gs, soft, face_idx, prob, cidx, ctype,
+                                                      sfvi, sig, M)
+    torch.cuda.synchronize()
+    assert np.abs(ref).max() > 0
+    np.testing.assert_allclose(N(gop), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
