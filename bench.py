@@ -614,8 +614,8 @@ def main():
                    'faces': wl.F, 'height': H, 'width': W, 'views_per_gpu': n,
                    'global_batch': total,
                    'parallelism': f'view-sharded x{world}' +
-                                  (' + RCCL vertex-grad all-reduce'
-                                   if world > 1 and not soup else ''),
+                                  ((' + RCCL' if backend == 'nccl' else f' + {backend}') +
+                                   ' vertex-grad all-reduce' if world > 1 and not soup else ''),
                    'launch': launch,
                    'vertex_path': {'compose': 'prepare_vertices + dibr_rasterization',
                                    'node': 'dibr_rasterization_from_vertices (projection in the '
