@@ -463,6 +463,27 @@ int kd_prepare_vertices_backward_f64(int batch, int vertex_batch, int64_t num_ve
                                      const int64_t *adj_offsets, const int32_t *adj,
                                      const int32_t *adj_ranges, int64_t num_ranges,
                                      double *grad_vertices, void *stream);
+/* The same backward for grad_fvi alone (grad_fvc and grad_normals zero: the DIB-R training
+ * step, where face_vertices_z and the normals only select faces), from the vertices instead of
+ * fvc: each corner's camera-space point is recomputed per view with the forward's arithmetic (the
+ * bits of fvc), so only the corner's grad_fvi is gathered per (entry, view).  Same result, bit
+ * for bit, as kd_prepare_vertices_backward_* with the forward's fvc. */
+int kd_prepare_vertices_backward_vertices_f32(int batch, int vertex_batch, int64_t num_vertices,
+                                              int64_t num_faces, const float *vertices,
+                                              const int64_t *faces, const float *camera_proj,
+                                              const float *camera_transform,
+                                              const float *grad_fvi, const int64_t *adj_offsets,
+                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              int64_t num_ranges, float *grad_vertices,
+                                              void *stream);
+int kd_prepare_vertices_backward_vertices_f64(int batch, int vertex_batch, int64_t num_vertices,
+                                              int64_t num_faces, const double *vertices,
+                                              const int64_t *faces, const double *camera_proj,
+                                              const double *camera_transform,
+                                              const double *grad_fvi, const int64_t *adj_offsets,
+                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              int64_t num_ranges, double *grad_vertices,
+                                              void *stream);
 /* Host function (host memory): workgroup entry ranges of the prepare_vertices backward from the
  * CSR offsets (V + 1): greedy, whole vertices, at most `cap` (<= 256) entries per range unless one
  * vertex alone has more.  ranges_out holds at least V + 2 values; returns the range count. */

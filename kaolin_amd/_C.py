@@ -390,6 +390,24 @@ def prepare_vertices_backward(faces, camera_proj, camera_transform, fvc, grad_fv
     return g
 
 
+def prepare_vertices_backward_from_vertices(vertices, faces, camera_proj, camera_transform,
+                                            grad_fvi, adjacency):
+    """The vertex gradient (Bv, V, 3) from grad_fvi alone, each corner's camera-space point
+    recomputed from the vertices (kd_prepare_vertices_backward_vertices): the same bits as
+    prepare_vertices_backward(..., fvc, None, grad_fvi, None, ...)."""
+    dev = vertices.device
+    Bv, V = vertices.shape[:2]
+    B, F = grad_fvi.shape[:2]
+    sfx = _sfx(vertices, 'prepare_vertices_backward')
+    offsets, adj, ranges = adjacency
+    g = torch.empty((Bv, V, 3), device=dev, dtype=vertices.dtype)
+    _lib.call(f'kd_prepare_vertices_backward_vertices_{sfx}', B, Bv, V, F,
+              _ptr(vertices.contiguous()), _ptr(faces), _ptr(camera_proj),
+              _ptr(camera_transform), _ptr(grad_fvi.contiguous()), _ptr(offsets), _ptr(adj),
+              _ptr(ranges), ranges.numel() - 1, _ptr(g), _stream(dev))
+    return g
+
+
 # -------------------------------------------------------------------------------------------
 # dibr_rasterization fused (kd_dibr.hip)
 # -------------------------------------------------------------------------------------------
@@ -865,6 +883,7 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     dibr_rasterization_backward_vertices=dibr_rasterization_backward_vertices,
     prepare_vertices_forward=prepare_vertices_forward,
     prepare_vertices_backward=prepare_vertices_backward,
+    prepare_vertices_backward_from_vertices=prepare_vertices_backward_from_vertices,
     texture_mapping_forward=texture_mapping_forward,
     texture_mapping_backward=texture_mapping_backward,
     rast_interpolate=rast_interpolate,

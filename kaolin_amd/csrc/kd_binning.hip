@@ -22,7 +22,7 @@ size_t bin_workspace_bytes(int B, int H, int W, int64_t N, int64_t max_per_view,
   const int64_t nchunk = (max_per_view + chunk - 1) / chunk;
   size_t s = 0;
   s += align_up(sizeof(Span) * (size_t)N);
-  s += align_up(sizeof(int) * (size_t)B * (size_t)(nchunk > 0 ? nchunk : 1) * g.nct());
+  s += 2 * align_up(sizeof(int) * (size_t)B * (size_t)(nchunk > 0 ? nchunk : 1) * g.nct());
   s += align_up(sizeof(int) * (size_t)B * g.nct());
   s += align_up(sizeof(int) * (size_t)B * g.nct());
   s += align_up(sizeof(int) * (size_t)kBinEntriesPerFace * (size_t)(N > 0 ? N : 1));
@@ -41,7 +41,13 @@ BinBuffers bin_carve(void *ws, size_t &off, int B, int H, int W, int64_t N,
   bb.spans = (Span *)(base + off);
   off += align_up(sizeof(Span) * (size_t)N);
   bb.counts = (int *)(base + off);
-  off += align_up(sizeof(int) * (size_t)B * (size_t)(bb.nchunk > 0 ? bb.nchunk : 1) * bb.g.nct());
+  // (sized like bin_workspace_bytes: for the smaller chunk)
+  const size_t ncsz = align_up(sizeof(int) * (size_t)B *
+                               (size_t)std::max<int64_t>((max_per_view + kChunk / 2 - 1) / (kChunk / 2), 1) *
+                               bb.g.nct());
+  off += ncsz;
+  bb.offs = (int *)(base + off);
+  off += ncsz;
   bb.totals = (int *)(base + off);
   off += align_up(sizeof(int) * (size_t)B * bb.g.nct());
   bb.base = (int *)(base + off);
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 }
 
 // One wave per (coarse tile, view, set), four per workgroup: exclusive scan of counts[b][c][*]
-// over the chunks (contiguous: tile-major).  Lane l owns the contiguous run of chunks
+// over the chunks (contiguous: tile-major), written to offs[b][*][c].  Lane l owns the contiguous run of chunks
 // [l*per, l*per + per), held in registers; the run sums are scanned with DPP (wave_incl_scan).
 // No LDS, no barriers: every wave's loads are in flight at once and the grid is one round on the
 // chip.
@@ -202,7 +208,10 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
   const int b = blockIdx.y, lane = threadIdx.x & (kWave - 1);
   const int n = bb.nchunk;
   const int per = (n + kWave - 1) / kWave;
-  int *base = bb.counts + ((int64_t)b * nct + c) * n;
+  const int *base = bb.counts + ((int64_t)b * nct + c) * n;
+  // the offsets go out chunk-major (offs[b][j][c]): the four waves of a workgroup write 16
+  // contiguous bytes per chunk, and every scatter workgroup then reads one contiguous row
+  int *outp = bb.offs + (int64_t)b * n * nct + c;
   constexpr int kMaxPer = 16;  // register-held run (n <= 1024 chunks = 262k faces per view)
   int v[kMaxPer];
   int local = 0;
@@ -228,7 +237,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
     for (int k = 0; k < kMaxPer; ++k) {
       const int j = lane * per + k;
       if (k < per && j < n) {
-        base[j] = run;
+        outp[(int64_t)j * nct] = run;
         run += v[k];
       }
     }
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
       const int j = lane * per + k;
       if (j < n) {
         const int x = base[j];
-        base[j] = run;
+        outp[(int64_t)j * nct] = run;
         run += x;
       }
     }
@@ -264,9 +273,9 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
   for (int k = tid; k < nct * kStride; k += kBlock) s_mask[k] = 0u;
-  {  // this chunk's exclusive offsets in every tile's bin (strided reads, once)
-    const int *offs = bb.counts + (int64_t)b * nct * bb.nchunk + chunk;
-    for (int c = tid; c < nct; c += kBlock) s_offs[c] = offs[(int64_t)c * bb.nchunk];
+  {  // this chunk's exclusive offsets in every tile's bin (kd_bin_scan's chunk-major row)
+    const int *offs = bb.offs + ((int64_t)b * bb.nchunk + chunk) * nct;
+    for (int c = tid; c < nct; c += kBlock) s_offs[c] = offs[c];
   }
   int64_t lo, hi;
   view_range(fs, b, lo, hi);

@@ -15,7 +15,8 @@
 //                     bins in the view's region (CSR; the chunk-0 workgroup stores the bases).
 // Layout in the workspace (N = rows of the face arrays):
 //   spans  [N]           Span (8 B)
-//   counts [B][nct][nchunk] int32, tile-major (turned into exclusive offsets by the scan)
+//   counts [B][nct][nchunk] int32, tile-major (read by the scan)
+//   offs   [B][nchunk][nct] int32, the scan's exclusive offsets, chunk-major (read by the scatter)
 //   totals [B][nct]      int32
 //   base   [B][nct]      int32 start of bin (b, c) inside view b's region, -1 = overflowed
 //   bins   [xper * N]    int32 local face index; view b owns the region [xper*lo, xper*hi) of
@@ -39,7 +40,9 @@ constexpr int kBinEntriesPerFace = 16;
 
 struct BinBuffers {
   Span *spans;
-  int *counts;
+  int *counts;     // [B][nct][nchunk] per-chunk counts, tile-major (kd_bin_count -> kd_bin_scan)
+  int *offs;       // [B][nchunk][nct] the chunks' exclusive offsets in each bin, chunk-major
+                   // (kd_bin_scan -> kd_bin_scatter: one contiguous row per scatter workgroup)
   int *totals;
   int *base;       // [B][nct]: start of bin (b, c) in view b's region, -1 = overflowed
   int *bins;

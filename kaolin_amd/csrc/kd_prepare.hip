@@ -83,6 +83,21 @@ __device__ __forceinline__ void corner_grad(const T c[3][3], int k, const T proj
   }
 }
 
+// corner_grad with only the projection's incoming gradient (grad_fvc = grad_nrm = NULL): the
+// same operations in the same order on the corner's own camera-space point, so the same bits.
+template <typename T>
+__device__ __forceinline__ void corner_grad_gi(const T ck[3], const T proj[3], T gi0, T gi1,
+                                               T g[3]) {
+  g[0] = (T)0;
+  g[1] = (T)0;
+  g[2] = (T)0;
+  const T pz = ck[2] * proj[2];
+  const T x = ck[0] * proj[0] / pz, y = ck[1] * proj[1] / pz;
+  g[0] += gi0 * proj[0] / pz;
+  g[1] += gi1 * proj[1] / pz;
+  g[2] -= (gi0 * x + gi1 * y) / ck[2];
+}
+
 // One thread per incident (face, corner) entry of the CSR (entries grouped by vertex) and vertex
 // batch: the corner's gradient, transformed back to world space, summed over the views it
 // covers.  Workgroup k takes the entries [blocks[k], blocks[k+1]): whole vertices, at most 256
@@ -90,7 +105,12 @@ __device__ __forceinline__ void corner_grad(const T c[3][3], int k, const T proj
 // rounds, each thread summing its own).  A vertex's entries are summed in LDS and stored once --
 // no memset, no global atomics.  The workgroups past the last range (blockIdx.x >= nblk) write
 // the zero gradient of vertices without incident faces.
-template <typename T>
+//
+// FROM_V (the DIB-R node's backward: grad_fvi only): the corner's camera-space point is
+// recomputed from the vertex per view (cam_point, the forward's own arithmetic: the bits of fvc)
+// instead of gathering the face's 9 camera coordinates from fvc for every (entry, view) -- the
+// entry's vertex is loaded once, the view loop gathers only the corner's 8-byte grad_fvi.
+template <typename T, bool FROM_V = false>
 __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T *fvc,
                                                          const T *gfvc, const T *gfvi,
                                                          const T *gnrm, const int64_t *adj_off,
@@ -121,6 +141,22 @@ __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T 
     const int k = fc - (int)f * 3;
     v = a.faces[fc];  // (F, 3) row-major: entry fc = 3 f + k (one vertex per multi-round range)
     const int b0 = a.Bv == 1 ? 0 : bv, b1 = a.Bv == 1 ? a.B : bv + 1;
+    if constexpr (FROM_V) {
+      const T *pv = a.vertices + ((int64_t)bv * a.V + v) * 3;  // (bv = 0 when Bv == 1)
+      const T p[3] = {pv[0], pv[1], pv[2]};
+      for (int b = b0; b < b1; ++b) {
+        const int64_t row = (int64_t)b * a.F + f;
+        const T *tf = a.tf + (int64_t)b * 12;
+        T ck[3], g[3];
+        cam_point<T>(tf, p, ck);
+        const T *gi = gfvi + row * 6 + k * 2;
+        corner_grad_gi<T>(ck, a.proj, gi[0], gi[1], g);
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          g3[q] += tf[q * 3 + 0] * g[0] + tf[q * 3 + 1] * g[1] + tf[q * 3 + 2] * g[2];
+      }
+      continue;
+    }
     for (int b = b0; b < b1; ++b) {
       const int64_t row = (int64_t)b * a.F + f;
       T c[3][3];
@@ -200,7 +236,9 @@ template <typename T>
 static int prep_bwd(int B, int Bv, int64_t V, int64_t F, const int64_t *faces, const T *proj,
                     const T *tf, const T *fvc, const T *gfvc, const T *gfvi, const T *gnrm,
                     const int64_t *adj_off, const int32_t *adj, const int32_t *blocks,
-                    int64_t nblk, T *gvert, void *stream) {
+                    int64_t nblk, T *gvert, void *stream, const T *vert = nullptr) {
+  KD_CHECK_ARG(!vert || (!gfvc && !gnrm && gfvi),
+               "from vertices: only the grad_fvi form (grad_fvc and grad_normals NULL)");
   KD_CHECK_ARG(B >= 0 && V >= 0 && F >= 0, "negative size");
   KD_CHECK_ARG(Bv == 1 || Bv == B, "vertex batch must be 1 or the view count");
   KD_CHECK_ARG(F * 3 < (1ll << 31), "too many faces");
@@ -214,12 +252,17 @@ static int prep_bwd(int B, int Bv, int64_t V, int64_t F, const int64_t *faces, c
   KD_CHECK_ARG(adj_off && adj && blocks && nblk >= 1, "vertex adjacency and its ranges required");
   const int64_t nz = (V + kBlock - 1) / kBlock;
   KD_CHECK_ARG(nblk + nz < (1ll << 31), "too many faces");
-  PrepArgs<T> a{B, Bv, V, F, nullptr, faces, proj, tf};
+  PrepArgs<T> a{B, Bv, V, F, vert, faces, proj, tf};
   {
     ProfScope prof(K_PREPARE_BWD, (hipStream_t)stream);
-    hipLaunchKernelGGL(kd_prepare_bwd<T>, dim3((unsigned)(nblk + nz), Bv), dim3(kBlock), 0,
-                       (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj_off, adj, blocks,
-                       (int)nblk, gvert);
+    if (vert)
+      hipLaunchKernelGGL((kd_prepare_bwd<T, true>), dim3((unsigned)(nblk + nz), Bv), dim3(kBlock),
+                         0, (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj_off, adj, blocks,
+                         (int)nblk, gvert);
+    else
+      hipLaunchKernelGGL((kd_prepare_bwd<T, false>), dim3((unsigned)(nblk + nz), Bv),
+                         dim3(kBlock), 0, (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj_off,
+                         adj, blocks, (int)nblk, gvert);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "prepare bwd: %s", hipGetErrorString(e));
@@ -267,6 +310,33 @@ int kd_prepare_vertices_backward_f64(int B, int Bv, int64_t V, int64_t F, const 
   return prep_bwd<double>(B, Bv, V, F, faces, camera_proj, camera_transform, fvc, grad_fvc,
                           grad_fvi, grad_normals, adj_offsets, adj, adj_ranges, num_ranges,
                           grad_vertices, stream);
+}
+
+int kd_prepare_vertices_backward_vertices_f32(int B, int Bv, int64_t V, int64_t F,
+                                              const float *vertices, const int64_t *faces,
+                                              const float *camera_proj,
+                                              const float *camera_transform,
+                                              const float *grad_fvi, const int64_t *adj_offsets,
+                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              int64_t num_ranges, float *grad_vertices,
+                                              void *stream) {
+  KD_CHECK_ARG(vertices, "vertices is NULL");
+  return prep_bwd<float>(B, Bv, V, F, faces, camera_proj, camera_transform, nullptr, nullptr,
+                         grad_fvi, nullptr, adj_offsets, adj, adj_ranges, num_ranges,
+                         grad_vertices, stream, vertices);
+}
+int kd_prepare_vertices_backward_vertices_f64(int B, int Bv, int64_t V, int64_t F,
+                                              const double *vertices, const int64_t *faces,
+                                              const double *camera_proj,
+                                              const double *camera_transform,
+                                              const double *grad_fvi, const int64_t *adj_offsets,
+                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              int64_t num_ranges, double *grad_vertices,
+                                              void *stream) {
+  KD_CHECK_ARG(vertices, "vertices is NULL");
+  return prep_bwd<double>(B, Bv, V, F, faces, camera_proj, camera_transform, nullptr, nullptr,
+                          grad_fvi, nullptr, adj_offsets, adj, adj_ranges, num_ranges,
+                          grad_vertices, stream, vertices);
 }
 
 // Host: workgroup entry ranges of the backward from the CSR offsets (host memory, V + 1 values):

@@ -237,6 +237,10 @@ def dibr_rasterization(height, width, face_vertices_z, face_vertices_image, face
 # gather kernel (the faster form, measured below); True = the face -> vertex step inside the
 # DIB-R backward kernel (kd_dibr_rasterization_backward_vertices).
 FUSED_VERTEX_BACKWARD = False
+# The gather kernel from the vertices (kd_prepare_vertices_backward_vertices: each corner's
+# camera-space point recomputed per view, only grad_fvi gathered) rather than from the forward's
+# fvc (kd_prepare_vertices_backward): the same bits.
+PREPARE_BWD_FROM_VERTICES = True
 
 
 class DibrRenderHip(Function):
@@ -271,7 +275,7 @@ class DibrRenderHip(Function):
                 grad_buffers=(gfvi_buf, gfeat_buf) if want_grad else None)
         ctx.save_for_backward(face_idx, weights, soft, fvi, fvc, face_features, faces,
                               camera_proj.contiguous(), camera_transform.contiguous(),
-                              ws if want_grad else None)
+                              ws if want_grad else None, vertices)
         ctx.bufs = (gfvi_buf, gfeat_buf)
         ctx.fused_vtx = fused_vtx
         from .utils import _adjacency
@@ -288,7 +292,7 @@ class DibrRenderHip(Function):
         if not (need_v or need_feat) or (grad_interp is None and grad_soft is None):
             return (None,) * 12
         (face_idx, weights, soft, fvi, fvc, feat, faces, proj, tf,
-         workspace) = ctx.saved_tensors
+         workspace, vertices) = ctx.saved_tensors
         eps, multiplier, boxlen, sigmainv, knum = ctx.params
         # the forward zeroed one set of gradient buffers: the first backward fills them, a second
         # one (retained graph) gets fresh buffers zeroed by the backward itself
@@ -307,8 +311,12 @@ class DibrRenderHip(Function):
             if need_v:
                 from .utils import _adjacency
                 adj = ctx.adj if ctx.adj is not None else _adjacency(faces, ctx.vshape[1])
-                gvert = _C.prepare_vertices_backward(faces, proj, tf, fvc, None, gfvi, None, adj,
-                                                     ctx.vshape[0], ctx.vshape[1])
+                if PREPARE_BWD_FROM_VERTICES:
+                    gvert = _C.prepare_vertices_backward_from_vertices(vertices, faces, proj, tf,
+                                                                       gfvi, adj)
+                else:
+                    gvert = _C.prepare_vertices_backward(faces, proj, tf, fvc, None, gfvi, None,
+                                                         adj, ctx.vshape[0], ctx.vshape[1])
         return (gvert if need_v else None, None, None, None, gfeat if need_feat else None, None,
                 None, None, None, None, None, None)
 

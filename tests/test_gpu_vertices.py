@@ -170,3 +170,28 @@ def test_from_vertices_forward_outputs_match_prepare(dname):
         assert torch.equal(fvc, c2) and torch.equal(fvi, i2) and torch.equal(nrm, n2)
         ri, rs, rf = dibr_rasterization(h, h, c2[..., 2], i2, feats, n2[..., 2])
         assert torch.equal(interp, ri) and torch.equal(soft, rs) and torch.equal(face_idx, rf)
+
+
+@pytest.mark.parametrize('dname', ['f32', 'f64'])
+@pytest.mark.parametrize('shared', [True, False])
+def test_prepare_backward_from_vertices_bit_identical(dname, shared, vertex_backward):
+    """kd_prepare_vertices_backward_vertices (the node's gather backward, each corner's
+    camera-space point recomputed from the vertex per view) gives the bits of
+    kd_prepare_vertices_backward over the forward's fvc, for a random grad_fvi (C3 mesh, 3
+    views, shared and per-view vertices)"""
+    if vertex_backward != 'gather':
+        pytest.skip('a prepare-kernel test (one backward form suffices)')
+    from kaolin_amd import _C
+    from kaolin_amd.render.mesh.utils import _adjacency
+    dt = TORCH_DTYPES[dname]
+    B = 3
+    v, faces, proj, cam, _ = _scene(250, 101, B, dt, shared=shared)
+    fvc, fvi, _ = _C.prepare_vertices_forward(v, faces, proj, cam)
+    g = torch.Generator().manual_seed(7)
+    gfvi = (torch.rand(fvi.shape, generator=g, dtype=torch.float64) - 0.5).to(DEV, dt)
+    adj = _adjacency(faces, v.shape[1])
+    ref = _C.prepare_vertices_backward(faces, proj, cam, fvc, None, gfvi, None, adj,
+                                       v.shape[0], v.shape[1])
+    new = _C.prepare_vertices_backward_from_vertices(v, faces, proj, cam, gfvi, adj)
+    torch.cuda.synchronize()
+    assert torch.equal(new, ref)
