@@ -398,9 +398,13 @@ struct SoftPairsLDS {
 //
 // The pair math of records [i0, i1) of the tile whose records start at `base` (tile column tx,
 // row ty): distance type and probability, bit-identical to the reference (kd_softdist.hpp).
+//
+// pt (nullable; split tiles): the part's LDS probability table [slot][q - q0] (row stride ptw),
+// so that the product reads each pixel's probabilities in slot order from LDS.
 template <typename T>
 __device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
-                                                int64_t base, int tx, int ty, int i0, int i1) {
+                                                int64_t base, int tx, int ty, int i0, int i1,
+                                                T *pt = nullptr, int q0 = 0, int ptw = 0) {
   const FaceSet<T> &fs = a.fs;
   const float M = fs.M;
   const SoftPairRec *rec = pb.rec + base;
@@ -417,6 +421,7 @@ __device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const Soft
     soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
     sp[i] = prob;
     pb.rec[base + i].type = (uint8_t)et;
+    if (pt) pt[(int)r.slot * ptw + ((int)r.q - q0)] = prob;
     // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
   }
 }
@@ -564,9 +569,9 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
           const int take = min(cnt, max(K - slot, 0));
           const uint64_t sel = take < cnt ? lowest_bits(hits, take) : hits;
           const long long w0 = now_clk();
-          if (mine)
+          if (mine)  // (split tiles: no record table -- the pair math fills a probability table)
             soft_chunk_write(L, w, sel, c, lo, slot, S.pm[w], S.off[w], S.row[w], &S.nrec,
-                             pb.rec + S.base, S.ridx, tile_q, tile_q);
+                             pb.rec + S.base, nullptr, tile_q, tile_q);
           if (CLK) {
             cyc[1] += now_clk() - w0;
             cyc[4] += mine ? 1 : 0;
@@ -694,7 +699,14 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     // pair math over this tile's records (record order: coalesced reads; diag 32: none)
     const int tx = tl % pb.ntx, ty = tl / pb.ntx;
     const T *sp = pb.sprob + base;
-    pair_math_range<T>(a, pb, base, tx, ty, 0, n);
+    // split tiles (a part owns kBlock / SPLIT pixels): the record table's LDS holds the part's
+    // probabilities by (slot, pixel) instead -- the product then needs no global reads
+    constexpr int kPtw = kBlock / SPLIT;
+    static_assert(SPLIT == 1 || sizeof(T) * kFuseSlots * kPtw <= sizeof(S.ridx),
+                  "split tiles: the probability table must fit the record table's LDS");
+    T *pt = SPLIT > 1 ? reinterpret_cast<T *>(&S.ridx[0][0]) : nullptr;
+    const int q0 = part * kPtw;
+    pair_math_range<T>(a, pb, base, tx, ty, 0, n, pt, q0, kPtw);
     __syncthreads();  // the workgroup's probabilities are visible to it
     if (KD_DIAG && fs.tbuf && tid == 0)  // diagnostics: end of the pair math
       fs.tbuf[6ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
@@ -707,7 +719,10 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       for (int s0 = 0; s0 < my_kid; s0 += U8) {
         T pv[U8];
 #pragma unroll
-        for (int u = 0; u < U8; ++u) pv[u] = s0 + u < my_kid ? sp[S.ridx[s0 + u][rq]] : (T)0;
+        for (int u = 0; u < U8; ++u)
+          pv[u] = s0 + u < my_kid ? (SPLIT > 1 ? pt[(s0 + u) * kPtw + (rq - q0)]
+                                               : sp[S.ridx[s0 + u][rq]])
+                                  : (T)0;
 #pragma unroll
         for (int u = 0; u < U8; ++u)
           if (s0 + u < my_kid) prod = (T)((double)prod * (1.0 - (double)pv[u]));

@@ -176,9 +176,10 @@ def test_from_vertices_forward_outputs_match_prepare(dname):
 @pytest.mark.parametrize('shared', [True, False])
 def test_prepare_backward_from_vertices_bit_identical(dname, shared, vertex_backward):
     """kd_prepare_vertices_backward_vertices (the node's gather backward, each corner's
-    camera-space point recomputed from the vertex per view) gives the bits of
-    kd_prepare_vertices_backward over the forward's fvc, for a random grad_fvi (C3 mesh, 3
-    views, shared and per-view vertices)"""
+    camera-space point recomputed from the vertex per view: the bits of fvc) equals
+    kd_prepare_vertices_backward over the forward's fvc for a random grad_fvi (C3 mesh, 3 views,
+    shared and per-view vertices) -- to the summation order of a vertex's entries, which both
+    kernels add in LDS with float atomics (their order is not fixed)"""
     if vertex_backward != 'gather':
         pytest.skip('a prepare-kernel test (one backward form suffices)')
     from kaolin_amd import _C
@@ -194,4 +195,5 @@ def test_prepare_backward_from_vertices_bit_identical(dname, shared, vertex_back
                                        v.shape[0], v.shape[1])
     new = _C.prepare_vertices_backward_from_vertices(v, faces, proj, cam, gfvi, adj)
     torch.cuda.synchronize()
-    assert torch.equal(new, ref)
+    tol = 1e-5 if dname == 'f32' else 1e-12
+    torch.testing.assert_close(new, ref, rtol=tol, atol=tol * ref.abs().max().item())
