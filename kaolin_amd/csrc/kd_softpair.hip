@@ -401,7 +401,10 @@ struct SoftPairsLDS {
 //
 // pt (nullable; split tiles): the part's LDS probability table [slot][q - q0] (row stride ptw),
 // so that the product reads each pixel's probabilities in slot order from LDS.
-template <typename T>
+// R records per thread and pass, their record and corner loads issued together (R = 2 for the
+// split tiles of small batches, whose heavy tiles run alone at the end of the launch: the loop is
+// bound by its two dependent loads per record there; at 8 views it is VALU-bound and R = 1).
+template <typename T, int R = 1>
 __device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                 int64_t base, int tx, int ty, int i0, int i1,
                                                 T *pt = nullptr, int q0 = 0, int ptw = 0) {
@@ -409,20 +412,32 @@ __device__ __forceinline__ void pair_math_range(const SoftArgs<T> &a, const Soft
   const float M = fs.M;
   const SoftPairRec *rec = pb.rec + base;
   T *sp = pb.sprob + base;
-  for (int i = i0 + (int)threadIdx.x; i < i1 && !ablate(fs.dbg, 32); i += kBlock) {
-    const SoftPairRec r = rec[i];
-    T v[6];
-    load_corners(fs, (int64_t)r.row, v);
-    int px, py;
-    tile_pixel(tx, ty, r.q, px, py);
-    const T x0 = (T)px_cx(M, fs.W, px), y0 = (T)px_cy(M, fs.H, py);
-    int et = 0;
-    T prob = (T)0;
-    soft_face_dist<T>(x0, y0, v, M, a.sigmainv, et, prob);
-    sp[i] = prob;
-    pb.rec[base + i].type = (uint8_t)et;
-    if (pt) pt[(int)r.slot * ptw + ((int)r.q - q0)] = prob;
-    // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
+  for (int i = i0 + (int)threadIdx.x; i < i1 && !ablate(fs.dbg, 32); i += R * kBlock) {
+    SoftPairRec r[R];
+    bool ok[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      ok[u] = u == 0 || i + u * kBlock < i1;
+      r[u] = rec[ok[u] ? i + u * kBlock : i];
+    }
+    T v[R][6];
+#pragma unroll
+    for (int u = 0; u < R; ++u) load_corners(fs, (int64_t)r[u].row, v[u]);
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (!ok[u]) break;
+      int px, py;
+      tile_pixel(tx, ty, r[u].q, px, py);
+      const T x0 = (T)px_cx(M, fs.W, px), y0 = (T)px_cy(M, fs.H, py);
+      int et = 0;
+      T prob = (T)0;
+      soft_face_dist<T>(x0, y0, v[u], M, a.sigmainv, et, prob);
+      const int ii = i + u * kBlock;
+      sp[ii] = prob;
+      pb.rec[base + ii].type = (uint8_t)et;
+      if (pt) pt[(int)r[u].slot * ptw + ((int)r[u].q - q0)] = prob;
+      // (no backward coefficients here: kd_soft_bwd_items computes them from the record)
+    }
   }
 }
 
@@ -679,16 +694,23 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
     pb.ntile[tile] = ovf ? -1 : n;  // -1: kd_soft_ovf_fwd streams the tile (lists included)
     pb.tbase[tile] = n > 0 ? base : 0;
   }
-  if (n > 0) {  // work items of the math and backward passes
-    const int nch = (n + kBlock - 1) / kBlock;
-    if (tid == 0) {
-      S.ibase = atomicAdd(&pb.counters[0], nch);
-      if (!FUSED) pb.tiles[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
-    }
+  // work items of the math and backward passes: nch items reserved with one device atomic.
+  // FUSED: the reservation's latency overlaps the pair math (thread 0 keeps the returned base in
+  // a register; the items are written after the product)
+  const int nch = (n + kBlock - 1) / kBlock;
+  int ibase = 0;
+  if (n > 0 && tid == 0) ibase = atomicAdd(&pb.counters[0], nch);
+  auto write_items = [&]() {
+    if (n <= 0) return;
+    if (tid == 0) S.ibase = ibase;
     __syncthreads();
     for (int c = tid; c < nch; c += kBlock)
       pb.items[S.ibase + c] =
           PairItem{base + (int64_t)c * kBlock, (int32_t)tile, min(kBlock, n - c * kBlock)};
+  };
+  if constexpr (!FUSED) {
+    if (n > 0 && tid == 0) pb.tiles[atomicAdd(&pb.counters[1], 1)] = (int32_t)tile;
+    write_items();
   }
   if constexpr (FUSED) {
     zero_side_job(a);
@@ -706,7 +728,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
                   "split tiles: the probability table must fit the record table's LDS");
     T *pt = SPLIT > 1 ? reinterpret_cast<T *>(&S.ridx[0][0]) : nullptr;
     const int q0 = part * kPtw;
-    pair_math_range<T>(a, pb, base, tx, ty, 0, n, pt, q0, kPtw);
+    pair_math_range<T, SPLIT == 1 ? 1 : 2>(a, pb, base, tx, ty, 0, n, pt, q0, kPtw);
     __syncthreads();  // the workgroup's probabilities are visible to it
     if (KD_DIAG && fs.tbuf && tid == 0)  // diagnostics: end of the pair math
       fs.tbuf[6ll * gridDim.x * gridDim.y + (int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
@@ -730,6 +752,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
       sval = (T)(1.0 - (double)prod);
       a.soft[p] = sval;
     }
+    write_items();
     iou_tile_terms<T>(a, b, tl, p, t.inimg && owner, sval, S.iou);
   }
 }
