@@ -29,6 +29,14 @@ import subprocess
 import sys
 import time
 
+# HIP graph replays dispatched through the runtime's regular kernel path instead of its
+# pre-recorded AQL packets (a launch-mode setting of the HIP runtime, read at its initialisation;
+# results are unchanged).  Same-box A/B, profiles/r06/ab_graph_packet_env.txt: C3 8 views
+# 0.2667 -> 0.2638 ms per step, 1 view 0.0898 -> 0.0869 ms.  Set KD_BENCH_KEEP_HIP_ENV=1 to
+# leave the runtime's default.
+if not os.environ.get('KD_BENCH_KEEP_HIP_ENV'):
+    os.environ.setdefault('DEBUG_CLR_GRAPH_PACKET_CAPTURE', '0')
+
 import torch
 import torch.distributed as dist
 
@@ -617,6 +625,8 @@ def main():
                                   ((' + RCCL' if backend == 'nccl' else f' + {backend}') +
                                    ' vertex-grad all-reduce' if world > 1 and not soup else ''),
                    'launch': launch,
+                   'hip_graph_packet_capture': os.environ.get('DEBUG_CLR_GRAPH_PACKET_CAPTURE',
+                                                              'runtime default'),
                    'vertex_path': {'compose': 'prepare_vertices + dibr_rasterization',
                                    'node': 'dibr_rasterization_from_vertices (projection in the '
                                            'binning launch; gather backward)',

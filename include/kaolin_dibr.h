@@ -467,13 +467,16 @@ int kd_prepare_vertices_backward_f64(int batch, int vertex_batch, int64_t num_ve
  * step, where face_vertices_z and the normals only select faces), from the vertices instead of
  * fvc: each corner's camera-space point is recomputed per view with the forward's arithmetic (the
  * bits of fvc), so only the corner's grad_fvi is gathered per (entry, view).  Same result, bit
- * for bit, as kd_prepare_vertices_backward_* with the forward's fvc. */
+ * for bit, as kd_prepare_vertices_backward_* with the forward's fvc (up to the order of the
+ * LDS sums of a vertex's entries).  adj_vertex (3F) int32: the vertex of each CSR entry (the
+ * chain entry -> face row -> vertex becomes one load). */
 int kd_prepare_vertices_backward_vertices_f32(int batch, int vertex_batch, int64_t num_vertices,
                                               int64_t num_faces, const float *vertices,
                                               const int64_t *faces, const float *camera_proj,
                                               const float *camera_transform,
                                               const float *grad_fvi, const int64_t *adj_offsets,
-                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              const int32_t *adj, const int32_t *adj_vertex,
+                                              const int32_t *adj_ranges,
                                               int64_t num_ranges, float *grad_vertices,
                                               void *stream);
 int kd_prepare_vertices_backward_vertices_f64(int batch, int vertex_batch, int64_t num_vertices,
@@ -481,7 +484,8 @@ int kd_prepare_vertices_backward_vertices_f64(int batch, int vertex_batch, int64
                                               const int64_t *faces, const double *camera_proj,
                                               const double *camera_transform,
                                               const double *grad_fvi, const int64_t *adj_offsets,
-                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              const int32_t *adj, const int32_t *adj_vertex,
+                                              const int32_t *adj_ranges,
                                               int64_t num_ranges, double *grad_vertices,
                                               void *stream);
 /* Host function (host memory): workgroup entry ranges of the prepare_vertices backward from the

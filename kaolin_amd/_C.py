@@ -331,7 +331,8 @@ def vertex_face_adjacency(faces, num_vertices):
     """CSR of each vertex's incident (face, corner) entries f * 3 + corner, grouped by vertex
     (stable order), and the backward's workgroup entry ranges (whole vertices, <= 256 entries;
     kd_prepare_vertices_ranges).  Returns (offsets (V+1) int64, adj (3F) int32, ranges (R+1)
-    int32) on the faces' device.  Built once per topology (one device->host copy of offsets)."""
+    int32, vertex of each entry (3F) int32) on the faces' device.  Built once per topology (one
+    device->host copy of offsets)."""
     import numpy as np
     flat = faces.reshape(-1)
     order = torch.argsort(flat, stable=True)
@@ -345,7 +346,7 @@ def vertex_face_adjacency(faces, num_vertices):
     if n < 0:
         raise RuntimeError('vertex_face_adjacency: kd_prepare_vertices_ranges failed')
     ranges = torch.from_numpy(rng[:n + 1].copy()).to(faces.device)
-    return offsets, order.to(torch.int32), ranges
+    return offsets, order.to(torch.int32), ranges, flat[order].to(torch.int32)
 
 
 def prepare_vertices_forward(vertices, faces, camera_proj, camera_transform):
@@ -381,7 +382,7 @@ def prepare_vertices_backward(faces, camera_proj, camera_transform, fvc, grad_fv
     dev = fvc.device
     B, F = fvc.shape[:2]
     sfx = _sfx(fvc, 'prepare_vertices_backward')
-    offsets, adj, ranges = adjacency
+    offsets, adj, ranges = adjacency[:3]
     g = torch.empty((vertex_batch, num_vertices, 3), device=dev, dtype=fvc.dtype)
     _lib.call(f'kd_prepare_vertices_backward_{sfx}', B, vertex_batch, num_vertices, F,
               _ptr(faces), _ptr(camera_proj), _ptr(camera_transform), _ptr(fvc),
@@ -399,12 +400,12 @@ def prepare_vertices_backward_from_vertices(vertices, faces, camera_proj, camera
     Bv, V = vertices.shape[:2]
     B, F = grad_fvi.shape[:2]
     sfx = _sfx(vertices, 'prepare_vertices_backward')
-    offsets, adj, ranges = adjacency
+    offsets, adj, ranges, vid = adjacency
     g = torch.empty((Bv, V, 3), device=dev, dtype=vertices.dtype)
     _lib.call(f'kd_prepare_vertices_backward_vertices_{sfx}', B, Bv, V, F,
               _ptr(vertices.contiguous()), _ptr(faces), _ptr(camera_proj),
               _ptr(camera_transform), _ptr(grad_fvi.contiguous()), _ptr(offsets), _ptr(adj),
-              _ptr(ranges), ranges.numel() - 1, _ptr(g), _stream(dev))
+              _ptr(vid), _ptr(ranges), ranges.numel() - 1, _ptr(g), _stream(dev))
     return g
 
 

@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T 
                                                          const T *gnrm, const int64_t *adj_off,
                                                          const int32_t *adj,
                                                          const int32_t *blocks, int nblk,
-                                                         T *gvert) {
+                                                         T *gvert, const int32_t *adj_v = nullptr) {
   __shared__ T s_acc[kBlock][3];
   __shared__ int64_t s_vid[kBlock];
   __shared__ int s_scan[4];
@@ -139,7 +139,9 @@ __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T 
     const int32_t fc = adj[e];
     const int64_t f = fc / 3;
     const int k = fc - (int)f * 3;
-    v = a.faces[fc];  // (F, 3) row-major: entry fc = 3 f + k (one vertex per multi-round range)
+    // (F, 3) row-major: entry fc = 3 f + k (one vertex per multi-round range); FROM_V reads the
+    // entry's vertex directly (adj_v) instead of through the face row
+    v = FROM_V ? (int64_t)adj_v[e] : a.faces[fc];
     const int b0 = a.Bv == 1 ? 0 : bv, b1 = a.Bv == 1 ? a.B : bv + 1;
     if constexpr (FROM_V) {
       const T *pv = a.vertices + ((int64_t)bv * a.V + v) * 3;  // (bv = 0 when Bv == 1)
@@ -236,9 +238,11 @@ template <typename T>
 static int prep_bwd(int B, int Bv, int64_t V, int64_t F, const int64_t *faces, const T *proj,
                     const T *tf, const T *fvc, const T *gfvc, const T *gfvi, const T *gnrm,
                     const int64_t *adj_off, const int32_t *adj, const int32_t *blocks,
-                    int64_t nblk, T *gvert, void *stream, const T *vert = nullptr) {
-  KD_CHECK_ARG(!vert || (!gfvc && !gnrm && gfvi),
-               "from vertices: only the grad_fvi form (grad_fvc and grad_normals NULL)");
+                    int64_t nblk, T *gvert, void *stream, const T *vert = nullptr,
+                    const int32_t *adj_v = nullptr) {
+  KD_CHECK_ARG(!vert || (!gfvc && !gnrm && gfvi && adj_v),
+               "from vertices: only the grad_fvi form (grad_fvc and grad_normals NULL), with "
+               "adj_vertex");
   KD_CHECK_ARG(B >= 0 && V >= 0 && F >= 0, "negative size");
   KD_CHECK_ARG(Bv == 1 || Bv == B, "vertex batch must be 1 or the view count");
   KD_CHECK_ARG(F * 3 < (1ll << 31), "too many faces");
@@ -258,7 +262,7 @@ static int prep_bwd(int B, int Bv, int64_t V, int64_t F, const int64_t *faces, c
     if (vert)
       hipLaunchKernelGGL((kd_prepare_bwd<T, true>), dim3((unsigned)(nblk + nz), Bv), dim3(kBlock),
                          0, (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj_off, adj, blocks,
-                         (int)nblk, gvert);
+                         (int)nblk, gvert, adj_v);
     else
       hipLaunchKernelGGL((kd_prepare_bwd<T, false>), dim3((unsigned)(nblk + nz), Bv),
                          dim3(kBlock), 0, (hipStream_t)stream, a, fvc, gfvc, gfvi, gnrm, adj_off,
@@ -317,26 +321,28 @@ int kd_prepare_vertices_backward_vertices_f32(int B, int Bv, int64_t V, int64_t 
                                               const float *camera_proj,
                                               const float *camera_transform,
                                               const float *grad_fvi, const int64_t *adj_offsets,
-                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              const int32_t *adj, const int32_t *adj_vertex,
+                                              const int32_t *adj_ranges,
                                               int64_t num_ranges, float *grad_vertices,
                                               void *stream) {
   KD_CHECK_ARG(vertices, "vertices is NULL");
   return prep_bwd<float>(B, Bv, V, F, faces, camera_proj, camera_transform, nullptr, nullptr,
                          grad_fvi, nullptr, adj_offsets, adj, adj_ranges, num_ranges,
-                         grad_vertices, stream, vertices);
+                         grad_vertices, stream, vertices, adj_vertex);
 }
 int kd_prepare_vertices_backward_vertices_f64(int B, int Bv, int64_t V, int64_t F,
                                               const double *vertices, const int64_t *faces,
                                               const double *camera_proj,
                                               const double *camera_transform,
                                               const double *grad_fvi, const int64_t *adj_offsets,
-                                              const int32_t *adj, const int32_t *adj_ranges,
+                                              const int32_t *adj, const int32_t *adj_vertex,
+                                              const int32_t *adj_ranges,
                                               int64_t num_ranges, double *grad_vertices,
                                               void *stream) {
   KD_CHECK_ARG(vertices, "vertices is NULL");
   return prep_bwd<double>(B, Bv, V, F, faces, camera_proj, camera_transform, nullptr, nullptr,
                           grad_fvi, nullptr, adj_offsets, adj, adj_ranges, num_ranges,
-                          grad_vertices, stream, vertices);
+                          grad_vertices, stream, vertices, adj_vertex);
 }
 
 // Host: workgroup entry ranges of the backward from the CSR offsets (host memory, V + 1 values):
