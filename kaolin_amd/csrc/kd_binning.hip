@@ -169,7 +169,8 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
           bin_count_face<T>(jobs.fs[z0 + z], jobs.bb[z0 + z], jobs.k[z0 + z], i, v, s_cnt[z],
                             &n[2]);
       }
-      if (z0 == 0 && i0 < hi) {  // (workgroup-uniform)
+      if (z0 == 0 && i0 < hi && !ablate(fs.dbg, 1 << 30)) {  // (workgroup-uniform; diagnostics:
+                                                              // 1 << 30 skips the outputs)
         const int rows = (int)min((int64_t)kBlock, hi - i0);
         __syncthreads();
         lds_to_global<T>(jobs.prep.fvc + i0 * 9, s_pc, rows * 9);

@@ -131,7 +131,15 @@ __global__ __launch_bounds__(kBlock) void kd_prepare_bwd(PrepArgs<T> a, const T 
     }
     return;
   }
-  const int64_t e0 = blocks[blockIdx.x], e1 = blocks[blockIdx.x + 1];
+  // XCD-aware: workgroups are dealt to the 8 XCDs round-robin (blockIdx % 8), so XCD x takes the
+  // contiguous band of ranges [x q + min(x, r), ...) (nblk = 8 q + r): neighbouring vertices,
+  // whose faces' corner rows (in every view) overlap, share one L2
+  int rb = blockIdx.x;
+  if (nblk >= 64) {
+    const int x = rb & 7, j = rb >> 3, q = nblk >> 3, r = nblk & 7;
+    rb = x * q + min(x, r) + j;
+  }
+  const int64_t e0 = blocks[rb], e1 = blocks[rb + 1];
   const bool valid = e0 + threadIdx.x < e1;
   int64_t v = -1;
   T g3[3] = {0, 0, 0};

@@ -455,7 +455,8 @@ template <typename T, bool FUSED, int SPLIT = 1, bool CLK = false>
 __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const SoftPairBuf<T> &pb,
                                                 int b, int tl, int nbin, SoftPairsLDS<FUSED> &S,
                                                 int part = 0, const uint64_t *uncm = nullptr,
-                                                long long *clk = nullptr) {
+                                                long long *clk = nullptr,
+                                                int bbase = kNoBinBase) {
   static_assert(SPLIT == 1 || FUSED, "split tiles: the fused soft mask only");
   TileLists &L = S.L;
   const FaceSet<T> &fs = a.fs;
@@ -466,6 +467,7 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
   const int nview = (int)(hi - lo);
   TileGeom t = SPLIT == 1 ? tile_geom(H, W, tl) : tile_geom_part<SPLIT>(H, W, tl, part);
   t.nbin = nbin;
+  t.bbase = bbase;
   const int tile_q = t.sub * kWave + lane;  // the pixel's index in the 16x16 tile frame
   if (KD_DIAG && fs.tbuf && tid == 0 && nbin >= 0)  // diagnostics: (view, tile, bin) of the slot
     fs.tbuf[(int64_t)blockIdx.y * gridDim.x + blockIdx.x] =
@@ -803,6 +805,17 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
   }
   int b, tl, nbin, part;
   tile_of_block_split<SPLIT>(ra.bb, ra.fs.H, ra.fs.W, b, tl, part, nbin, ra.fs.dbg);
+  // the soft mask's coarse bin (same geometry as the raster's): its base and face count loaded
+  // now, in flight during the raster phase, instead of as the soft walk's first round trip
+  int s_nb, s_base;
+  {
+    const BinGeom &g = a.bb.g;
+    const int ntx = (a.fs.W + kTile - 1) / kTile;
+    const int ct = (((tl / ntx) * kTile) >> g.sh) * g.nctx + (((tl % ntx) * kTile) >> g.sh);
+    const int64_t bc = (int64_t)b * g.nct() + ct;
+    s_base = a.bb.base[bc];
+    s_nb = a.bb.totals[bc];
+  }
   if (DIAG && a.fs.tbuf && threadIdx.x == 0) {
     const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
     a.fs.tbuf[slot] = ((long long)nbin << 32) | (long long)(b * pb.ntiles + tl);
@@ -820,8 +833,8 @@ __global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<flo
         wall_clock64();
   if (!ablate(a.fs.dbg, 1 << 24))  // diagnostics: the raster phase alone (instruction counts)
     soft_pairs_tile<float, true, SPLIT, DIAG>(
-        a, pb, b, tl, -1, U.s, part, uncm,
-        DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr);
+        a, pb, b, tl, s_nb, U.s, part, uncm,
+        DIAG && a.fs.tbuf ? a.fs.tbuf + 16ll * gridDim.x * gridDim.y : nullptr, s_base);
   // tile history (kd_set_tile_history): the last wave to finish stores the workgroup's duration
   // as a quarter-octave bucket (1..63; 0 = none) for the next same-shape call's dispatch order
   if (ra.bb.hist && (threadIdx.x & (kWave - 1)) == 0 &&

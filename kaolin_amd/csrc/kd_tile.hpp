@@ -36,7 +36,10 @@ struct TileGeom {
   int SX0, SX1, SY0, SY1;      // this wave's sub-list filter
   int sub;                     // this wave's 8x8 sub-tile in the 16x16 tile frame (0..3)
   int role;                    // split tiles: which of the sub-tile's waves this is (0 owns pixels)
+  int bbase;                   // the coarse bin's base when already loaded (with nbin), else
+                               // kNoBinBase: tile_rounds loads it
 };
+constexpr int kNoBinBase = INT_MIN;
 
 // (view, fine tile) of dispatch slot d of n tile slots: the bins' heaviest-first order
 // (tile_order) when the bins were built, else slot order.
@@ -100,6 +103,7 @@ __device__ __forceinline__ TileGeom tile_geom(int H, int W, int tile) {
   t.SY1 = t.WY1;
   t.sub = w;
   t.role = 0;
+  t.bbase = kNoBinBase;
   return t;
 }
 __device__ __forceinline__ TileGeom tile_geom(int H, int W) { return tile_geom(H, W, blockIdx.x); }
@@ -144,6 +148,7 @@ __device__ __forceinline__ TileGeom tile_geom_part(int H, int W, int tile, int p
   t.SY1 = t.WY1;
   t.sub = s;
   t.role = w / NS;
+  t.bbase = kNoBinBase;
   return t;
 }
 
@@ -240,7 +245,13 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
   int n;
-  const int *bin = bin_list(bb, b, ct, lo, nview, t.nbin, n);
+  const int *bin;
+  if (t.bbase != kNoBinBase && t.nbin >= 0) {  // (bin_list with its loads done by the caller)
+    n = t.bbase < 0 ? nview : t.nbin;
+    bin = t.bbase < 0 ? nullptr : bb.bins + (int64_t)bb.xper * lo + t.bbase;
+  } else {
+    bin = bin_list(bb, b, ct, lo, nview, t.nbin, n);
+  }
   int cnt = 0;
   // kPrefetch chunks of bin entries and their spans are loaded up front (two dependent
   // round trips per kPrefetch * 256 entries instead of per 256)
