@@ -95,6 +95,11 @@ int kd_set_coarse_tile(int px);
  * it; 0 turns it off, and so does attaching no buffer. */
 int kd_set_tile_history(int on);
 
+/* The device a stream belongs to (the null stream: the calling thread's current device) -- the
+ * device whose per-device state (tile history, CU count) a call on that stream uses -- and, when
+ * compute_units is not NULL, that device's CU count as the launchers see it.  Support. */
+int kd_stream_device(void *stream, int *compute_units);
+
 /* Bytes of one device's tile history buffer (2 MB). */
 size_t kd_tile_history_bytes(void);
 

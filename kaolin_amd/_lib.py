@@ -145,6 +145,8 @@ def load():
             lib.kd_set_coarse_tile.restype = c_int
             lib.kd_set_tile_history.argtypes = [c_int]
             lib.kd_set_tile_history.restype = c_int
+            lib.kd_stream_device.argtypes = [c_p, c_p]
+            lib.kd_stream_device.restype = c_int
             lib.kd_tile_history_bytes.argtypes = []
             lib.kd_tile_history_bytes.restype = c_size
             lib.kd_tile_history_attach.argtypes = [c_p, c_p, c_size]

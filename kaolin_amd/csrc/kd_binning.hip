@@ -200,12 +200,16 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
 // [l*per, l*per + per), held in registers; the run sums are scanned with DPP (wave_incl_scan).
 // No LDS, no barriers: every wave's loads are in flight at once and the grid is one round on the
 // chip.
+// (up to 16 waves per workgroup: the chunk-major offsets of 16 consecutive tiles are 64
+// contiguous bytes per chunk row -- at 8 views 7.8 -> 7.0 us; small batches keep 4 waves, 16
+// would leave too few workgroups: 1 view 6.7 -> 8.0 us)
+constexpr int kScanWaves = 16;
 template <typename T>
-__global__ __launch_bounds__(kBlock) void kd_bin_scan(BinJobs<T> jobs) {
+__global__ __launch_bounds__(kScanWaves * kWave) void kd_bin_scan(BinJobs<T> jobs) {
   const BinBuffers &bb = jobs.bb[blockIdx.z];
   const int nct = bb.g.nct();
   const int wv = threadIdx.x >> 6;
-  const int c = blockIdx.x * (kBlock / kWave) + wv;
+  const int c = blockIdx.x * (int)(blockDim.x >> 6) + wv;
   const int b = blockIdx.y, lane = threadIdx.x & (kWave - 1);
   const int n = bb.nchunk;
   const int per = (n + kWave - 1) / kWave;
@@ -464,7 +468,8 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
     return hipSuccess;
   }
   const dim3 grid_c(bb.nchunk, fs.B, njobs);
-  const dim3 grid_t((bb.g.nct() + kBlock / kWave - 1) / (kBlock / kWave), fs.B, njobs);
+  const int scan_waves = fs.B >= 4 ? kScanWaves : kBlock / kWave;
+  const dim3 grid_t((bb.g.nct() + scan_waves - 1) / scan_waves, fs.B, njobs);
   const bool two = bb.chunk == 2 * kBlock;
   // both sets in one workgroup when they share the corners (dibr_rasterization's raster and soft
   // boxes), the corners loaded once: measured slower at C3 (24.6 vs 19.8 us at 8 views, 11.7 vs
@@ -498,7 +503,7 @@ static hipError_t bin_jobs(const BinJobs<T> &jobs_in, int njobs, hipStream_t str
   }
   {
     ProfScope prof(K_BIN_SCAN, stream);
-    hipLaunchKernelGGL(kd_bin_scan<T>, grid_t, dim3(kBlock), 0, stream, jobs);
+    hipLaunchKernelGGL(kd_bin_scan<T>, grid_t, dim3(scan_waves * kWave), 0, stream, jobs);
   }
   {  // + one column of workgroups for the tile order (kd_bin_scatter, tile_order)
     // chunk-bit masks per coarse tile: up to 64 KB of dynamic LDS at 1024 coarse tiles (a

@@ -188,6 +188,11 @@ int kd_set_tile_history(int on) {
   return KD_OK;
 }
 
+int kd_stream_device(void *stream, int *compute_units) {
+  if (compute_units) *compute_units = kd::device_cus((hipStream_t)stream);
+  return kd::stream_device((hipStream_t)stream);
+}
+
 size_t kd_tile_history_bytes(void) { return sizeof(unsigned short) * (size_t)kd::kTileHistCap; }
 
 int kd_tile_history_attach(void *stream, void *device_buffer, size_t bytes) {

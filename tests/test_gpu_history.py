@@ -124,3 +124,19 @@ def test_history_on_a_device_other_than_the_current_one():
     for x, y in zip(other[:3], ref[:3]):
         assert torch.equal(x, y)
     torch.testing.assert_close(other[3], ref[3], rtol=1e-4, atol=1e-5 * ref[3].abs().max().item())
+
+
+def test_stream_device_resolution():
+    """per-device state is keyed by the stream's device -- the null stream resolves to
+    the current device, a stream to its own device, and the CU count is that device's"""
+    import ctypes
+    from kaolin_amd import _lib
+    lib = _lib.load()
+    cus = ctypes.c_int(0)
+    assert lib.kd_stream_device(None, ctypes.byref(cus)) == torch.cuda.current_device()
+    assert cus.value == torch.cuda.get_device_properties(0).multi_processor_count
+    s = torch.cuda.Stream(device=0)
+    assert lib.kd_stream_device(s.cuda_stream, None) == 0
+    if torch.cuda.device_count() > 1:
+        s1 = torch.cuda.Stream(device=1)
+        assert lib.kd_stream_device(s1.cuda_stream, None) == 1
