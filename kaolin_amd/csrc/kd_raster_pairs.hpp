@@ -93,9 +93,10 @@ template <typename T>
 struct RasterPairsLDS {
   TileLists L;
   T geo[9][kCap];        // ax ay bx by cx cy (scaled), az bz cz
-  // raster_cull_coefs (kd_binning), face frame.  fp64: read from global memory in pass A
-  // instead (8 KB less LDS: five workgroups per CU instead of four)
-  float4 cull[2][sizeof(T) == 8 ? 1 : kCap];
+  // raster_cull_coefs (kd_binning), face frame: read from global memory in pass A (fp64 since
+  // round 3: five workgroups per CU instead of four; fp32 since round 6 -- with the soft phase's
+  // lane permutes, 8 KB less LDS makes the fused forward's 7 workgroups per CU instead of 6)
+  float4 cull[2][1];
   unsigned short pair[4][kRasterPairCap];  // (q << 8) | sub-list entry
   unsigned long long key[4][64];
   unsigned long long zx[sizeof(T) == 8 ? 4 : 1][64];  // fp64: ordered exact maximum depth
@@ -119,7 +120,6 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   constexpr bool kF64 = sizeof(T) == 8;
   TileLists &L = S.L;
   auto &s_geo = S.geo;
-  auto &s_cull = S.cull;
   auto &s_pair = S.pair;
   auto &s_key = S.key;
   auto &s_nan = S.nan;
@@ -152,10 +152,6 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     s_geo[6][k] = zz[0];
     s_geo[7][k] = zz[a.fvz_cs];
     s_geo[8][k] = zz[2 * a.fvz_cs];
-    if constexpr (!kF64) {
-      s_cull[0][k] = a.bb.cull[2 * fi];
-      s_cull[1][k] = a.bb.cull[2 * fi + 1];
-    }
   };
   // CLK: per-wave cycle counts of the phases (wave 0's are written out): [0] pass A row
   // intervals + transpose + scan, [1] pair placement, [2] pass B, [4] chunks, [5] candidate
@@ -264,14 +260,8 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
         // face frame -> this sub-tile: columns shift by WX0 - span.x0, rows by the centre offset
         const float xo = (float)(ox - sp.x0);
         const float dref = ysb - px_cy(M, H, sp.y0);
-        float4 cl, ch;
-        if constexpr (kF64) {
-          cl = a.bb.cull[2 * (lo + L.f[k])];
-          ch = a.bb.cull[2 * (lo + L.f[k]) + 1];
-        } else {
-          cl = s_cull[0][k];
-          ch = s_cull[1][k];
-        }
+        const float4 cl = a.bb.cull[2 * (lo + L.f[k])];
+        const float4 ch = a.bb.cull[2 * (lo + L.f[k]) + 1];
         const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
         // only the rows of the face's own span (a lane's loop: the wave runs the longest span,
         // not all 8 rows); drow[r] is recomputed from sy (px_cy's first factor: the same bits)

@@ -171,9 +171,12 @@ __device__ __forceinline__ uint64_t chunk_select(const TileLists &L, int nsub, i
 // The record writes of one chunk for a selection `sel` (pixel lane: its faces of the chunk),
 // slots from my_kid on (advanced).  tile_q: the pixel's thread index in the 16x16 tile frame (the
 // record's q); ridx_q: its column of the (slot, pixel) record table.
+// The face lanes' pixel masks, first records and face rows reach the pixel lanes through lane
+// permutes (ds_bpermute: no LDS allocation -- 4 KB less per workgroup than staging them, which
+// lets a seventh workgroup onto a CU); the permute loop runs wave-uniform, so every source lane
+// is active.
 __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uint64_t sel, int c,
-                                                 int64_t lo, int &my_kid, uint64_t *s_pm,
-                                                 int *s_off, int *s_row, int *s_nrec,
+                                                 int64_t lo, int &my_kid, int *s_nrec,
                                                  SoftPairRec *rec,
                                                  unsigned short (*s_ridx)[kBlock], int tile_q,
                                                  int ridx_q) {
@@ -186,22 +189,19 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
   if (tot == 0) return;
   int base = 0;
   if (lane == 0) base = atomicAdd(s_nrec, tot);
-  // the face lane's row (its entry of the chunk), staged with its mask and first record so that
-  // a pixel lane needs one LDS round trip per selected face
+  // the face lane's row (its entry of the chunk) and first record
   const int row = cnt ? (int)(lo + L.f[L.sub[ls][c * kWave + lane]]) : 0;
   base = __builtin_amdgcn_readfirstlane(base);
-  s_pm[lane] = pm;
-  s_off[lane] = base + incl - cnt;
-  s_row[lane] = row;
-  wave_lds_sync();
-  // pixel lanes: write own records, slots ascending with the face index, four selected faces per
-  // step with every LDS read issued before the first store; a record is one 8-byte store
+  const int first = base + incl - cnt;
+  const int pml = (int)(uint32_t)pm, pmh = (int)(uint32_t)(pm >> 32);
+  // pixel lanes: write own records, slots ascending with the face index, two selected faces per
+  // step with every permute issued before the first store; a record is one 8-byte store
   const uint64_t below = (1ull << lane) - 1ull;
   unsigned long long *rec8 = reinterpret_cast<unsigned long long *>(rec);
   const unsigned long long qbits = (unsigned long long)(uint8_t)tile_q << 48;
   int slot = my_kid;
-  for (uint64_t m = sel; m;) {
-    constexpr int U = 4;
+  for (uint64_t m = sel; __ballot(m != 0ull);) {
+    constexpr int U = 2;
     int jj[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -212,10 +212,11 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
     uint64_t pmu[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = jj[u] < 0 ? 0 : jj[u];
-      off[u] = s_off[j];
-      rw[u] = s_row[j];
-      pmu[u] = s_pm[j];
+      const int a = (jj[u] < 0 ? 0 : jj[u]) << 2;  // (byte address of the source lane)
+      off[u] = __builtin_amdgcn_ds_bpermute(a, first);
+      rw[u] = __builtin_amdgcn_ds_bpermute(a, row);
+      pmu[u] = (uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, pml) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, pmh) << 32);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -227,7 +228,8 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
         if (s_ridx) s_ridx[slot + u][ridx_q] = (unsigned short)ri;  // (slot, pixel) -> record
       }
     }
-    slot += (jj[0] >= 0) + (jj[1] >= 0) + (jj[2] >= 0) + (jj[3] >= 0);
+#pragma unroll
+    for (int u = 0; u < U; ++u) slot += jj[u] >= 0;
   }
   my_kid = slot;
   wave_lds_sync();
@@ -235,13 +237,11 @@ __device__ __forceinline__ void soft_chunk_write(const TileLists &L, int ls, uin
 
 __device__ __forceinline__ void soft_chunk_records(const TileLists &L, int nsub, int c, bool unc,
                                                    int K, const TileGeom &t, int64_t lo,
-                                                   int &my_kid, uint64_t *s_pm, int *s_off,
-                                                   int *s_row, int *s_nrec, SoftPairRec *rec,
+                                                   int &my_kid, int *s_nrec, SoftPairRec *rec,
                                                    unsigned short (*s_ridx)[kBlock] = nullptr) {
   const int tile_q = threadIdx.x;
   const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
-  soft_chunk_write(L, threadIdx.x >> 6, sel, c, lo, my_kid, s_pm, s_off, s_row, s_nrec, rec,
-                   s_ridx, tile_q, tile_q);
+  soft_chunk_write(L, threadIdx.x >> 6, sel, c, lo, my_kid, s_nrec, rec, s_ridx, tile_q, tile_q);
 }
 
 // The streaming form of one chunk (a tile without records): the pixel lane visits the same
@@ -382,9 +382,6 @@ template <bool FUSED>
 struct SoftPairsLDS {
   unsigned short ridx[FUSED ? kFuseSlots : 1][kBlock];
   TileLists L;
-  uint64_t pm[4][kWave];
-  int off[4][kWave];   // soft_chunk_write: a chunk face's first record
-  int row[4][kWave];   // ... and its face row
   int64_t base;
   int nrec, ibase, box[4];
   double iou[8];  // iou_tile_terms
@@ -552,13 +549,12 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
               cyc[4] += 1;
               const uint64_t sel = chunk_select(L, nsub, c, unc, K, t, my_kid);
               const long long w0 = now_clk();
-              soft_chunk_write(L, w, sel, c, lo, my_kid, S.pm[w], S.off[w], S.row[w], &S.nrec,
-                               pb.rec + S.base, FUSED ? S.ridx : nullptr, tid, tid);
+              soft_chunk_write(L, w, sel, c, lo, my_kid, &S.nrec, pb.rec + S.base,
+                               FUSED ? S.ridx : nullptr, tid, tid);
               cyc[1] += now_clk() - w0;
             } else {
-              soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, S.pm[w], S.off[w], S.row[w],
-                                 &S.nrec,
-                                 pb.rec + S.base, FUSED ? S.ridx : nullptr);
+              soft_chunk_records(L, nsub, c, unc, K, t, lo, my_kid, &S.nrec, pb.rec + S.base,
+                                 FUSED ? S.ridx : nullptr);
             }
           }
         }
@@ -587,8 +583,8 @@ __device__ __forceinline__ void soft_pairs_tile(const SoftArgs<T> &a, const Soft
           const uint64_t sel = take < cnt ? lowest_bits(hits, take) : hits;
           const long long w0 = now_clk();
           if (mine)  // (split tiles: no record table -- the pair math fills a probability table)
-            soft_chunk_write(L, w, sel, c, lo, slot, S.pm[w], S.off[w], S.row[w], &S.nrec,
-                             pb.rec + S.base, nullptr, tile_q, tile_q);
+            soft_chunk_write(L, w, sel, c, lo, slot, &S.nrec, pb.rec + S.base, nullptr, tile_q,
+                             tile_q);
           if (CLK) {
             cyc[1] += now_clk() - w0;
             cyc[4] += mine ? 1 : 0;
