@@ -431,7 +431,7 @@ def main():
                          'step\'s own gradient, inside the timed step (1 GPU; tile history A/B '
                          'under motion)')
     ap.add_argument('--pmc', default=None,
-                    help='PMC traffic summary (default profiles/r05, r04, r03 or r02/pmc_traffic_<config>.json)')
+                    help='PMC traffic summary (default profiles/r06, r05, r04, r03 or r02/pmc_traffic_<config>.json)')
     args = ap.parse_args()
     if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
         # one process per GPU: started here, before anything touches the GPU (this process only
@@ -513,7 +513,7 @@ def main():
     # the step's count projects the mesh (dibr_rasterization_from_vertices, kd_bin_count PREP)
     prep = (V, wl.F, n) if (not soup and args.vertex_path != 'compose' and not args.iou) else None
     pmc, pmc_src = {}, None
-    for rnd in ([args.pmc] if args.pmc else ['r05', 'r04', 'r03', 'r02']):  # the newest committed summary
+    for rnd in ([args.pmc] if args.pmc else ['r06', 'r05', 'r04', 'r03', 'r02']):  # the newest committed summary
         pmc_path = rnd if args.pmc else os.path.join(ROOT, 'profiles', rnd,
                                                        f'pmc_traffic_{args.config}.json')
         pmc, pmc_src = load_pmc(pmc_path, args.config, args.dtype, args.lists, n)
