@@ -115,6 +115,10 @@ def algorithmic_bytes(kernel, P, F, Fv, D, K, lists, pairs=None, V=0, esize=4, f
         return F * (6 + 3 * D) * e
     if kernel == 'kd_prepare_fwd':     # vertices + faces in; fvc, fvi, normals out
         return V * 3 * e + F * (9 + 6 + 3) * e
+    if kernel == 'kd_prepare_bwd' and prep:  # from the vertices (the node's backward): grad_fvi,
+        # the vertices and the CSR (entry, vertex) pairs in, vertex grads out
+        Vm, Fm, nv = prep
+        return F * 6 * e + Vm * 3 * e * 2 + Fm * 3 * (4 + 4)
     if kernel == 'kd_prepare_bwd':     # fvc + grad_fvi in, vertex grads out
         return F * (9 + 6) * e + V * 3 * e
     if pairs is None:
