@@ -305,6 +305,23 @@ int kd_dibr_rasterization_forward_f64(int batch, int height, int width, int64_t 
  * (B, H, W, knum), cidx (B, H, W, knum) int64 (-1 = empty), ctype (B, H, W, knum) uint8, read
  * by kd_dibr_soft_mask_backward_* (with kd_rasterize_backward_* for the raster part).  No
  * workspace backward (want_grad 0). */
+/* dibr_soft_mask's backward (as kd_dibr_soft_mask_backward_*) over the close-face lists that
+ * kd_dibr_rasterization_forward_lists_* wrote, given that forward's workspace (ws, wsb as it was
+ * called with): its per-pixel row lengths let the rows without listed faces be skipped exactly,
+ * without reading them.  fvi_scaled = face_vertices_image * multiplier.  Replaces the soft half
+ * of the reference composition's backward (dibr.py:57-73 -> dibr_soft_mask.cpp:110-183). */
+int kd_dibr_rasterization_soft_backward_lists_f32(
+    int batch, int height, int width, int64_t num_faces, int knum, const float *grad_soft,
+    const float *soft_mask, const int64_t *face_idx, const float *close_prob,
+    const int64_t *close_idx, const uint8_t *close_type, const float *fvi_scaled,
+    float sigmainv, float multiplier, float *grad_fvi, const void *workspace,
+    size_t workspace_bytes, void *stream);
+int kd_dibr_rasterization_soft_backward_lists_f64(
+    int batch, int height, int width, int64_t num_faces, int knum, const double *grad_soft,
+    const double *soft_mask, const int64_t *face_idx, const double *close_prob,
+    const int64_t *close_idx, const uint8_t *close_type, const double *fvi_scaled,
+    float sigmainv, float multiplier, double *grad_fvi, const void *workspace,
+    size_t workspace_bytes, void *stream);
 int kd_dibr_rasterization_forward_lists_f32(
     int batch, int height, int width, int64_t num_faces, int feat_dim, const float *fvz,
     int64_t fvz_face_stride, int64_t fvz_corner_stride, const float *fvi, const float *feat,

@@ -558,6 +558,24 @@ def dibr_rasterization_forward_vertices(height, width, vertices, faces, camera_p
     return fvc, fvi, nrm, interp, face_idx, weights, soft, ws
 
 
+def dibr_soft_mask_backward_lists_ws(grad_soft, soft, face_idx, close_prob, close_idx,
+                                     close_type, fvi_scaled, sigmainv, multiplier, workspace):
+    """dibr_soft_mask_backward_cuda over the lists of dibr_rasterization_forward_fused(...,
+    with_lists=True), given that call's workspace: the rows without listed faces are skipped
+    exactly (kd_dibr_rasterization_soft_backward_lists)."""
+    fn = 'dibr_soft_mask_backward'
+    dev = _check_same_gpu(fn, grad_soft=grad_soft, soft=soft, close_prob=close_prob)
+    B, H, W, K = close_prob.shape
+    F = fvi_scaled.shape[1]
+    sfx = _sfx(fvi_scaled, fn)
+    g = torch.empty_like(fvi_scaled)
+    _lib.call(f'kd_dibr_rasterization_soft_backward_lists_{sfx}', B, H, W, F, K,
+              _ptr(grad_soft.contiguous()), _ptr(soft), _ptr(face_idx), _ptr(close_prob),
+              _ptr(close_idx), _ptr(close_type), _ptr(fvi_scaled), float(sigmainv),
+              float(multiplier), _ptr(g), _ptr(workspace), workspace.numel(), _stream(dev))
+    return g
+
+
 def dibr_rasterization_backward_fused(grad_interp, grad_soft, face_idx, weights, soft,
                                       face_vertices_image, face_features, eps, multiplier,
                                       boxlen, sigmainv, knum, workspace, need_feat=True,
@@ -881,6 +899,7 @@ render = types.SimpleNamespace(mesh=types.SimpleNamespace(
     dibr_rasterization_forward_fused=dibr_rasterization_forward_fused,
     dibr_rasterization_forward_vertices=dibr_rasterization_forward_vertices,
     dibr_rasterization_backward_fused=dibr_rasterization_backward_fused,
+    dibr_soft_mask_backward_lists_ws=dibr_soft_mask_backward_lists_ws,
     dibr_rasterization_backward_vertices=dibr_rasterization_backward_vertices,
     prepare_vertices_forward=prepare_vertices_forward,
     prepare_vertices_backward=prepare_vertices_backward,

@@ -72,6 +72,9 @@ _SIGS = {
                                     c_p, c_p],
     'kd_prepare_vertices_backward': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p, c_p, c_p,
                                      c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
+    'kd_dibr_rasterization_soft_backward_lists': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p,
+                                                  c_p, c_p, c_p, c_p, c_p, c_float, c_float, c_p,
+                                                  c_p, c_size, c_p],
     'kd_prepare_vertices_backward_vertices': [c_int, c_int, c_i64, c_i64, c_p, c_p, c_p, c_p,
                                               c_p, c_p, c_p, c_p, c_p, c_i64, c_p, c_p],
     'kd_dibr_soft_mask_backward_binned': [c_int, c_int, c_int, c_i64, c_int, c_p, c_p, c_p, c_p,

@@ -387,6 +387,52 @@ int kd_dibr_rasterization_forward_lists_f64(
                           face_idx, weights, soft, 0, nullptr, nullptr, ws, wsb, stream,
                           IouIo<double>{}, nullptr, prob, cidx, ctype);
 }
+}  // extern "C"
+
+namespace kd {
+template <typename T>
+int soft_backward(int B, int H, int W, int64_t F, int K, const T *grad_soft, const T *soft,
+                  const int64_t *face_idx, const T *prob, const int64_t *cidx,
+                  const uint8_t *ctype, const T *fvi, float sigmainv, float M, T *grad_fvi,
+                  hipStream_t stream, const int32_t *row_n);
+
+// dibr_soft_mask's backward over the close-face lists of kd_dibr_rasterization_forward_lists_*,
+// with that forward's workspace: its per-pixel row lengths let the lists backward skip the rows
+// without listed faces exactly (their terms are all zero), without reading them.
+template <typename T>
+static int soft_bwd_lists_ws(int B, int H, int W, int64_t F, int K, const T *gs, const T *soft,
+                             const int64_t *fidx, const T *prob, const int64_t *cidx,
+                             const uint8_t *ctype, const T *fvi_scaled, float sigmainv, float M,
+                             T *gfvi, const void *ws, size_t wsb, void *stream) {
+  KD_CHECK_ARG(B >= 0 && H >= 0 && W >= 0 && F >= 0 && K >= 1, "negative size");
+  const size_t need = dibr_workspace_bytes(B, H, W, F, K, sizeof(T));
+  if (wsb < need || (need && !ws))
+    return set_error(KD_ERR_WORKSPACE, "workspace too small: %zu < %zu", wsb, need);
+  const int32_t *row_n =
+      (B && H && W) ? dibr_carve<T>(const_cast<void *>(ws), B, H, W, F, K).pb.npix : nullptr;
+  return soft_backward<T>(B, H, W, F, K, gs, soft, fidx, prob, cidx, ctype, fvi_scaled, sigmainv,
+                          M, gfvi, (hipStream_t)stream, row_n);
+}
+}  // namespace kd
+
+extern "C" {
+
+int kd_dibr_rasterization_soft_backward_lists_f32(
+    int B, int H, int W, int64_t F, int knum, const float *grad_soft, const float *soft,
+    const int64_t *face_idx, const float *prob, const int64_t *cidx, const uint8_t *ctype,
+    const float *fvi_scaled, float sigmainv, float M, float *grad_fvi, const void *ws,
+    size_t wsb, void *stream) {
+  return soft_bwd_lists_ws<float>(B, H, W, F, knum, grad_soft, soft, face_idx, prob, cidx, ctype,
+                                  fvi_scaled, sigmainv, M, grad_fvi, ws, wsb, stream);
+}
+int kd_dibr_rasterization_soft_backward_lists_f64(
+    int B, int H, int W, int64_t F, int knum, const double *grad_soft, const double *soft,
+    const int64_t *face_idx, const double *prob, const int64_t *cidx, const uint8_t *ctype,
+    const double *fvi_scaled, float sigmainv, float M, double *grad_fvi, const void *ws,
+    size_t wsb, void *stream) {
+  return soft_bwd_lists_ws<double>(B, H, W, F, knum, grad_soft, soft, face_idx, prob, cidx,
+                                   ctype, fvi_scaled, sigmainv, M, grad_fvi, ws, wsb, stream);
+}
 int kd_dibr_rasterization_forward_vertices_f32(
     int B, int H, int W, int vertex_batch, int64_t V, int64_t F, int D, const float *vertices,
     const int64_t *faces, const float *camera_proj, const float *camera_transform,

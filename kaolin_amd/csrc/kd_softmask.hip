@@ -180,7 +180,8 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
     int B, int H, int W, int64_t F, int K, const T *__restrict__ grad_soft,
     const T *__restrict__ soft, const int64_t *__restrict__ face_idx, const T *__restrict__ prob,
     const int64_t *__restrict__ cidx, const uint8_t *__restrict__ ctype,
-    const T *__restrict__ fvi, float sigmainv, float M, T *grad_fvi, int dbg) {
+    const T *__restrict__ fvi, float sigmainv, float M, T *grad_fvi, int dbg,
+    const int32_t *__restrict__ row_n) {
   __shared__ int64_t s_pix[kBlock];  // listed pixel: image index | tile pixel << 48
   __shared__ double s_sp[kBlock];    // its s_p
   __shared__ int s_cnt[kBlock / kWave];
@@ -246,7 +247,10 @@ __global__ __launch_bounds__(kBlock) void kd_soft_bwd_lists(
     // reach the gradients as in the reference).  soft 0 is NOT such a case: it only says that
     // every 1 - prob rounded to 1 (dibr_soft_mask_cuda.cu:174-181), and a probability of ~2^-25
     // still gives the nonzero terms dLdz * geometry of dibr_soft_mask_cuda.cu:283-348.
-    const bool zero_terms = (sov == (T)1 || gsv == (T)0) && isfinite(sov) && isfinite(gsv);
+    // row_n (nullable; the fused lists forward's row lengths, kd_dibr_rasterization_forward_lists):
+    // a row without listed faces has no terms at all -- known without reading it
+    const bool zero_terms = ((sov == (T)1 || gsv == (T)0) && isfinite(sov) && isfinite(gsv)) ||
+                            (row_n && in && row_n[p] == 0);
     const bool live = in && fi < 0 && !zero_terms;
     int n;
     const int pos = wg_compact(live, s_cnt, n);  // (its barriers also order the table reset)
@@ -355,7 +359,7 @@ template <typename T>
 int soft_backward(int B, int H, int W, int64_t F, int K, const T *grad_soft, const T *soft,
                   const int64_t *face_idx, const T *prob, const int64_t *cidx,
                   const uint8_t *ctype, const T *fvi, float sigmainv, float M, T *grad_fvi,
-                  hipStream_t stream) {
+                  hipStream_t stream, const int32_t *row_n = nullptr) {
   const int64_t nf = (int64_t)B * F;
   if (nf > 0) {  // (a kernel, not a memset node: see zero_buffers)
     const int rc = zero_buffers<T>(grad_fvi, nf * 6, (T *)nullptr, 0, stream);
@@ -379,12 +383,21 @@ int soft_backward(int B, int H, int W, int64_t F, int K, const T *grad_soft, con
     if (!atomic_form)
       hipLaunchKernelGGL(kd_soft_bwd_lists<T>, dim3(tgrid), dim3(kBlock), 0, stream, B, H, W, F,
                          K, grad_soft, soft, face_idx, prob, cidx, ctype, fvi, sigmainv, M,
-                         grad_fvi, debug_flags());
+                         grad_fvi, debug_flags(), row_n);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return set_error(KD_ERR_LAUNCH, "soft bwd: %s", hipGetErrorString(e));
   return KD_OK;
 }
+
+template int soft_backward<float>(int, int, int, int64_t, int, const float *, const float *,
+                                  const int64_t *, const float *, const int64_t *,
+                                  const uint8_t *, const float *, float, float, float *,
+                                  hipStream_t, const int32_t *);
+template int soft_backward<double>(int, int, int, int64_t, int, const double *, const double *,
+                                   const int64_t *, const double *, const int64_t *,
+                                   const uint8_t *, const double *, float, float, double *,
+                                   hipStream_t, const int32_t *);
 
 template <typename T>
 FaceSet<T> fused_faceset(int B, int H, int W, int64_t F, const T *fvi, double M, double boxlen) {

@@ -306,6 +306,7 @@ __global__ __launch_bounds__(kBlock) void kd_soft_ovf_fwd(SoftArgs<T> a, SoftPai
     if (__syncthreads_or(unc))
       tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg, done);
     if (unc && my_kid > 0 && a.soft) a.soft[p] = (T)(1.0 - (double)prod);
+    if (!FUSED && a.prob && t.inimg) pb.npix[p] = my_kid;  // (the lists' row lengths)
     if (!FUSED && a.prob && t.inimg)
       for (int s = my_kid; s < K; ++s) {  // the -1 / 0 / 0 padding (kd_soft_lists skips the tile)
         a.prob[p * K + s] = (T)0;

@@ -159,13 +159,14 @@ class DibrRasterizationListsHip(Function):
                 face_normals_z, sigmainv, boxlen, knum, multiplier, eps):
         face_vertices_image = face_vertices_image.contiguous()
         face_features = face_features.contiguous()
-        interp, face_idx, weights, soft, _, prob, cidx, ctype = \
+        interp, face_idx, weights, soft, ws, prob, cidx, ctype = \
             _C.render.mesh.dibr_rasterization_forward_fused(
                 height, width, face_vertices_z, face_vertices_image, face_features,
                 face_normals_z, sigmainv, boxlen, knum, multiplier, eps, want_grad=False,
                 with_lists=True)
+        # (the workspace's per-pixel row lengths let the lists backward skip empty rows)
         ctx.save_for_backward(face_idx, weights, soft, face_vertices_image, face_features, prob,
-                              cidx, ctype)
+                              cidx, ctype, ws)
         ctx.params = (eps, multiplier, sigmainv)
         ctx.mark_non_differentiable(face_idx)
         ctx.set_materialize_grads(False)
@@ -176,16 +177,16 @@ class DibrRasterizationListsHip(Function):
         need_fvi, need_feat = ctx.needs_input_grad[3], ctx.needs_input_grad[4]
         if not (need_fvi or need_feat) or (grad_interp is None and grad_soft is None):
             return (None,) * 11
-        face_idx, weights, soft, fvi, feat, prob, cidx, ctype = ctx.saved_tensors
+        face_idx, weights, soft, fvi, feat, prob, cidx, ctype, ws = ctx.saved_tensors
         eps, multiplier, sigmainv = ctx.params
         gfvi = gfeat = None
         if grad_interp is not None:
             gfvi, gfeat = _C.render.mesh.rasterize_backward_autograd(
                 grad_interp.contiguous(), face_idx, weights, fvi, feat, eps, need_feat=need_feat)
         if grad_soft is not None and need_fvi:
-            gs = _C.render.mesh.dibr_soft_mask_backward_cuda(
+            gs = _C.render.mesh.dibr_soft_mask_backward_lists_ws(
                 grad_soft.contiguous(), soft, face_idx, prob, cidx, ctype,
-                (fvi * multiplier).contiguous(), sigmainv, multiplier)
+                (fvi * multiplier).contiguous(), sigmainv, multiplier, ws)
             gfvi = gs if gfvi is None else gfvi + gs
         return (None, None, None, gfvi if need_fvi else None, gfeat if need_feat else None, None,
                 None, None, None, None, None)

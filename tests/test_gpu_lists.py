@@ -168,3 +168,37 @@ def test_op_backward_soft_zero_rows_keep_their_terms():
     torch.cuda.synchronize()
     assert np.abs(ref).max() > 0
     np.testing.assert_allclose(N(gop), ref, rtol=1e-4, atol=1e-5 * np.abs(ref).max())
+
+
+def test_fused_lists_backward_keeps_soft_zero_rows():
+    """The fused lists path's backward skips only the rows without listed faces (the forward's
+    row lengths; kd_dibr_rasterization_soft_backward_lists): on soft == 0 rows with
+    probabilities (boxlen 0.05, sigmainv 30000) its gradient equals the op-form backward's,
+    which reads every row."""
+    from kaolin_amd import _C, workloads
+    v = workloads.sphere_views(100, 51, 256, 256, 2, DEV, elevation=0.7)
+    sig, box, K, M = 30000., 0.05, 30, 1000.
+    out = _C.render.mesh.dibr_rasterization_forward_fused(
+        256, 256, v['fvz'], v['fvi'], v['feats'], v['normals_z'], sig, box, K, M, 1e-8,
+        want_grad=False, with_lists=True)
+    _, face_idx, _, soft, ws, prob, cidx, ctype = out
+    zero_rows = (soft == 0) & (prob[..., 0] > 0) & (face_idx < 0)
+    assert int(zero_rows.sum()) > 100
+    g = torch.Generator().manual_seed(11)
+    gs = torch.rand(soft.shape, generator=g).to(DEV) * (zero_rows | (soft < 1)).float()
+    sfvi = (v['fvi'] * M).contiguous()
+    ref = _C.render.mesh.dibr_soft_mask_backward_cuda(gs, soft, face_idx, prob, cidx, ctype, sfvi,
+                                                      sig, M)
+    new = _C.render.mesh.dibr_soft_mask_backward_lists_ws(gs, soft, face_idx, prob, cidx, ctype,
+                                                          sfvi, sig, M, ws)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(N(new), N(ref), rtol=1e-4, atol=1e-5 * N(ref).__abs__().max())
+    # and on the soft == 0 rows alone
+    gz = zero_rows.float()
+    ref = _C.render.mesh.dibr_soft_mask_backward_cuda(gz, soft, face_idx, prob, cidx, ctype, sfvi,
+                                                      sig, M)
+    new = _C.render.mesh.dibr_soft_mask_backward_lists_ws(gz, soft, face_idx, prob, cidx, ctype,
+                                                          sfvi, sig, M, ws)
+    torch.cuda.synchronize()
+    assert N(ref).__abs__().max() > 0
+    np.testing.assert_allclose(N(new), N(ref), rtol=1e-4, atol=1e-5 * N(ref).__abs__().max())
