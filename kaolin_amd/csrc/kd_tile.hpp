@@ -364,22 +364,26 @@ __device__ __forceinline__ uint32_t lane_xor(uint32_t x) {
     a = r[1];  // even rows: the odd rows' values
     b = r[0];  // odd rows: the even rows' values
     hi = (lane & 16) != 0;
-  } else if constexpr (SH == 8) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xf, 0xf, false);  // row_ror:8
+  } else if constexpr (SH == 8) {  // (every source lane exists: bound_ctrl, no `old` to set up)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xf, 0xf, true);  // row_ror:8
   } else if constexpr (SH == 4) {
-    a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xf, 0xf, false);  // row_shl:4
-    b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
-    hi = (lane & 4) != 0;
+    // banks 0 and 2 of each row (lanes with bit 2 clear) read row_shl:4, banks 1 and 3 row_shr:4
+    // into the same register (bank_mask): no select
+    const int t = __builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xf, 0x5, false);  // row_shl:4
+    return (uint32_t)__builtin_amdgcn_update_dpp(t, (int)x, 0x114, 0xf, 0xa, false);  // row_shr:4
   } else if constexpr (SH == 2) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, false);  // [2,3,0,1]
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x4e, 0xf, 0xf, true);  // [2,3,0,1]
   } else {
     static_assert(SH == 1, "lane_xor: SH in {1, 2, 4, 8, 16, 32}");
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, false);  // [1,0,3,2]
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xb1, 0xf, 0xf, true);  // [1,0,3,2]
   }
   asm volatile("" : "+v"(a), "+v"(b));
   return hi ? b : a;
 }
 
+// One block-swap stage of the transpose in the form of the reference text (a lane-dependent
+// branch per stage: both sides run under partial EXEC); wave_transpose64_blocks keeps it as the
+// check of wave_transpose64 (tools/micro/transpose_check.hip).
 template <int SH>
 __device__ __forceinline__ uint64_t transpose_step(uint64_t x, uint64_t mlo) {
   const int lane = threadIdx.x & 63;
@@ -389,15 +393,70 @@ __device__ __forceinline__ uint64_t transpose_step(uint64_t x, uint64_t mlo) {
   return (lane & SH) ? ((x & ~mlo) | ((y & ~mlo) >> SH)) : ((x & mlo) | ((y & mlo) << SH));
 }
 
-// 64x64 bit-matrix transpose across a wave: lane l bit j -> lane j bit l (block swaps).
-// Every lane of the wave must be active.
-__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
+__device__ __forceinline__ uint64_t wave_transpose64_blocks(uint64_t x) {
   x = transpose_step<32>(x, 0x00000000ffffffffull);
   x = transpose_step<16>(x, 0x0000ffff0000ffffull);
   x = transpose_step<8>(x, 0x00ff00ff00ff00ffull);
   x = transpose_step<4>(x, 0x0f0f0f0f0f0f0f0full);
   x = transpose_step<2>(x, 0x3333333333333333ull);
   x = transpose_step<1>(x, 0x5555555555555555ull);
+  return x;
+}
+
+// Stage SH <= 8 without a branch, on each 32-bit half: a lane with bit SH clear keeps its low
+// SH-bit parts (m) and takes its partner's low parts moved up; a lane with the bit set keeps the
+// high parts and takes the partner's high parts moved down.  So every lane SENDS its half rotated
+// by its own parity (clear: right by SH, its high parts land on the low places; set: left by SH)
+// and merges the received word under its keep mask with one bit-field insert.
+template <int SH>
+__device__ __forceinline__ uint32_t transpose_half(uint32_t h, uint32_t keep, uint32_t rot) {
+  const uint32_t s = __builtin_amdgcn_alignbit(h, h, rot);  // rotate right
+  return (h & keep) | (lane_xor<SH>(s) & ~keep);  // v_bfi_b32
+}
+
+// lane: the lane id, opaque to the compiler (wave_transpose64), so that the per-lane masks are
+// recomputed at each use (three instructions a stage) rather than hoisted into eight VGPRs
+template <int SH>
+__device__ __forceinline__ uint64_t transpose_step_rot(uint64_t x, uint32_t m, uint32_t lane) {
+  const uint32_t neg = (uint32_t)((int)(lane << (31 - __builtin_ctz(SH))) >> 31);  // 0 / ~0
+  const uint32_t keep = m ^ neg;
+  const uint32_t rot = (neg & (uint32_t)(32 - SH)) | (~neg & (uint32_t)SH);
+  const uint32_t lo = transpose_half<SH>((uint32_t)x, keep, rot);
+  const uint32_t hi = transpose_half<SH>((uint32_t)(x >> 32), keep, rot);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// 64x64 bit-matrix transpose across a wave: lane l bit j -> lane j bit l.  Every lane of the
+// wave must be active.  The stages are the block swaps of wave_transpose64_blocks, written for
+// gfx950's lane movers so that no stage branches:
+//   32: one v_permlane32_swap of the two halves (the low half's upper lanes <-> the high half's
+//       lower lanes is exactly the 32-bit block swap);
+//   16: the two 16-bit parts each lane keeps / sends packed into one word each (v_perm), one
+//       v_permlane16_swap of the packed words, unpacked by v_perm -- the same two selectors for
+//       every lane;
+//   8, 4, 2, 1: transpose_step_rot (rotate, DPP exchange, bit-field insert).
+__device__ __forceinline__ uint64_t wave_transpose64(uint64_t x) {
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap((uint32_t)x, (uint32_t)(x >> 32), false, false);
+    x = ((uint64_t)r[1] << 32) | r[0];
+  }
+  {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    const uint32_t a = __builtin_amdgcn_perm(hi, lo, 0x05040100u);  // low 16-bit parts
+    const uint32_t b = __builtin_amdgcn_perm(hi, lo, 0x07060302u);  // high 16-bit parts
+    const auto r = __builtin_amdgcn_permlane16_swap(a, b, false, false);
+    // even rows: a' = own low parts, b' = the partner's low parts; odd rows: a' = the partner's
+    // high parts, b' = own high parts -- both unpack as (a' part, b' part)
+    const uint32_t nlo = __builtin_amdgcn_perm(r[1], r[0], 0x05040100u);
+    const uint32_t nhi = __builtin_amdgcn_perm(r[1], r[0], 0x07060302u);
+    x = ((uint64_t)nhi << 32) | nlo;
+  }
+  uint32_t lane = threadIdx.x & 63;
+  asm volatile("" : "+v"(lane));
+  x = transpose_step_rot<8>(x, 0x00ff00ffu, lane);
+  x = transpose_step_rot<4>(x, 0x0f0f0f0fu, lane);
+  x = transpose_step_rot<2>(x, 0x33333333u, lane);
+  x = transpose_step_rot<1>(x, 0x55555555u, lane);
   return x;
 }
 
