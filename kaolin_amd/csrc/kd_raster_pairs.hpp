@@ -235,6 +235,24 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     }
     wave_lds_sync();
   };
+  // pass A's culling coefficients of the wave's first chunk of the batch, loaded as soon as the
+  // wave's sub-list is known (tile_rounds `pre`): their round trip overlaps the stage's instead
+  // of following the barrier
+  float p0 = 0.f, p1 = 0.f, p2 = 0.f, p3 = 0.f, p4 = 0.f, p5 = 0.f, p6 = 0.f, p7 = 0.f;
+  auto pre = [&](int nsub) {
+    const int j = t.role * kWave + lane;
+    wave_lds_sync();  // this wave's own sub-list stores
+    // (only entries of the sub-list: past nsub -- e.g. an empty sub-list -- L.sub holds stale
+    // or never-written bytes)
+    float4 cl = make_float4(0.f, 0.f, 0.f, 0.f), ch = cl;
+    if (j < nsub) {
+      const int64_t r = lo + L.f[L.sub[w][j]];
+      cl = a.bb.cull[2 * r];
+      ch = a.bb.cull[2 * r + 1];
+    }
+    p0 = cl.x; p1 = cl.y; p2 = cl.z; p3 = cl.w;
+    p4 = ch.x; p5 = ch.y; p6 = ch.z; p7 = ch.w;
+  };
   auto round = [&](int nsub, int) {
     if (ablate(fs.dbg, 1)) return;
     if (nsub == 0) return;
@@ -260,8 +278,15 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
         // face frame -> this sub-tile: columns shift by WX0 - span.x0, rows by the centre offset
         const float xo = (float)(ox - sp.x0);
         const float dref = ysb - px_cy(M, H, sp.y0);
-        const float4 cl = a.bb.cull[2 * (lo + L.f[k])];
-        const float4 ch = a.bb.cull[2 * (lo + L.f[k]) + 1];
+        // (the wave's first chunk: loaded by `pre` below, in flight with the stage's loads)
+        float4 cl, ch;
+        if (c == t.role) {
+          cl = make_float4(p0, p1, p2, p3);
+          ch = make_float4(p4, p5, p6, p7);
+        } else {
+          cl = a.bb.cull[2 * (lo + L.f[k])];
+          ch = a.bb.cull[2 * (lo + L.f[k]) + 1];
+        }
         const float l0 = cl.x - xo, l2 = cl.z - xo, h0 = ch.x - xo, h2 = ch.z - xo;
         // only the rows of the face's own span (a lane's loop: the wave runs the longest span,
         // not all 8 rows); drow[r] is recomputed from sy (px_cy's first factor: the same bits)
@@ -327,7 +352,7 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
     }
     if (total) test_batch(total);
   };
-  tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg);
+  tile_rounds(L, a.bb, (int)(hi - lo), b, lo, t, stage, round, fs.dbg, NeverDone(), pre);
   if (CLK && KD_DIAG && clk && threadIdx.x == 0) {
     const int64_t nb = (int64_t)gridDim.x * gridDim.y, slot = blockIdx.y * gridDim.x + blockIdx.x;
     clk[slot] = wall_clock64();

@@ -786,8 +786,11 @@ union DibrTileLDS {
 // SPLIT, views) grid, for batches too small to fill the chip with whole tiles: a heavy tile's
 // raster chunks, pass A chunks and pair math spread over SPLIT CUs.  The raster phase hands the
 // soft phase its uncovered pixels through `uncm` (the soft phase's waves need not own them).
+// 7 workgroups per CU (21.5 KB of LDS, <= 72 VGPRs: four of the values the raster walk keeps in
+// flight spill to 20 bytes of scratch; at 6 per CU, 78 VGPRs, the launch measured 124.7 against
+// 119.5 us at 8 views).
 template <bool DIAG, int SPLIT>
-__global__ __launch_bounds__(kBlock, 6) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
+__global__ __launch_bounds__(kBlock, 7) void kd_dibr_fwd_tiles(RasterFwdArgs<float> ra,
                                                               SoftArgs<float> a,
                                                               SoftPairBuf<float> pb) {
   __shared__ DibrTileLDS<float> U;

@@ -233,25 +233,55 @@ __device__ __forceinline__ SubSpans load_subspans(const TileLists &L, int nsub) 
 struct NeverDone {
   __device__ bool operator()() const { return false; }
 };
+struct NoPrefetch {
+  __device__ void operator()(int) const {}
+};
 
 // `done()` (evaluated by every thread; must return a workgroup-uniform value, e.g. through
 // __syncthreads_and) lets a caller stop the walk once later faces cannot matter any more.
+// `pre(nsub)` (per wave, before the batch's face data is staged): the wave's sub-list of the
+// batch is in L.sub[w] / L.nsub[w] (written by the wave itself), so a caller can issue the loads
+// its round needs per sub-list entry here, in flight together with the stage's loads.
 // nview: faces of view b (rows [lo, lo + nview)), walked in full when the bin overflowed.
-template <typename Stage, typename Round, typename Done = NeverDone>
+template <typename Stage, typename Round, typename Done = NeverDone, typename Pre = NoPrefetch>
 __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, int nview, int b,
                                             int64_t lo, const TileGeom &t, Stage stage,
-                                            Round round, int dbg = 0, Done done = Done()) {
+                                            Round round, int dbg = 0, Done done = Done(),
+                                            Pre pre = Pre()) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const BinGeom &g = bb.g;
   const int ct = (t.Y0 >> g.sh) * g.nctx + (t.X0 >> g.sh);
   int n;
   const int *bin;
-  if (t.bbase != kNoBinBase && t.nbin >= 0) {  // (bin_list with its loads done by the caller)
+  if (t.nbin == 0) {  // an empty bin never overflows: no header load
+    n = 0;
+    bin = nullptr;
+  } else if (t.bbase != kNoBinBase && t.nbin >= 0) {  // (bin_list with its loads done by the caller)
     n = t.bbase < 0 ? nview : t.nbin;
     bin = t.bbase < 0 ? nullptr : bb.bins + (int64_t)bb.xper * lo + t.bbase;
   } else {
     bin = bin_list(bb, b, ct, lo, nview, t.nbin, n);
   }
+  // one batch of cnt faces in L.f / L.span: sub-lists, the caller's prefetch, staging, its round
+  auto flush = [&](int cnt) {
+    __syncthreads();
+    int nsub = 0;
+    for (int k0 = 0; k0 < cnt; k0 += kWave) {
+      const int k = k0 + lane;
+      const bool ok =
+          t.wave_live && k < cnt && span_overlaps(L.span[k], t.SX0, t.SX1, t.SY0, t.SY1);
+      const uint64_t m = __ballot(ok);
+      if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
+      nsub += __popcll(m);
+    }
+    if (lane == 0) L.nsub[w] = nsub;
+    pre(nsub);
+    if (!ablate(dbg, 2))
+      for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
+    __syncthreads();
+    if (!ablate(dbg, 4)) round(nsub, cnt);
+    __syncthreads();
+  };
   int cnt = 0;
   // kPrefetch chunks of bin entries and their spans are loaded up front (two dependent
   // round trips per kPrefetch * 256 entries instead of per 256)
@@ -279,22 +309,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
       const int pos = wg_compact(ov, L.cnt, tot);
       // a batch holds at most kCap faces: flush first if this chunk would overflow it
       if (cnt + tot > kCap) {
-        __syncthreads();
-        if (!ablate(dbg, 2))
-          for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
-        int nsub = 0;
-        for (int k0 = 0; k0 < cnt; k0 += kWave) {
-          const int k = k0 + lane;
-          const bool ok =
-              t.wave_live && k < cnt && span_overlaps(L.span[k], t.SX0, t.SX1, t.SY0, t.SY1);
-          const uint64_t m = __ballot(ok);
-          if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
-          nsub += __popcll(m);
-        }
-        if (lane == 0) L.nsub[w] = nsub;
-        __syncthreads();
-        if (!ablate(dbg, 4)) round(nsub, cnt);
-        __syncthreads();
+        flush(cnt);
         cnt = 0;
         if (done()) return;
       }
@@ -305,24 +320,7 @@ __device__ __forceinline__ void tile_rounds(TileLists &L, const BinBuffers &bb, 
       cnt += tot;
     }
   }
-  if (cnt > 0) {
-    __syncthreads();
-    if (!ablate(dbg, 2))
-      for (int k = tid; k < cnt; k += kBlock) stage(k, lo + L.f[k]);
-    int nsub = 0;
-    for (int k0 = 0; k0 < cnt; k0 += kWave) {
-      const int k = k0 + lane;
-      const bool ok =
-          t.wave_live && k < cnt && span_overlaps(L.span[k], t.SX0, t.SX1, t.SY0, t.SY1);
-      const uint64_t m = __ballot(ok);
-      if (ok) L.sub[w][nsub + mbcnt(m)] = (unsigned char)k;
-      nsub += __popcll(m);
-    }
-    if (lane == 0) L.nsub[w] = nsub;
-    __syncthreads();
-    if (!ablate(dbg, 4)) round(nsub, cnt);
-    __syncthreads();
-  }
+  if (cnt > 0) flush(cnt);
 }
 
 // Orders LDS traffic between lanes of one wave (LDS ops of a wave complete in order; this keeps
