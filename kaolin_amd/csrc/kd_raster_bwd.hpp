@@ -24,7 +24,8 @@ struct RasterBwdArgs {
 // ------------------------------------------------------------------------------------------
 // Backward terms of one covered pixel (rasterization_cuda.cu:271-399) into out[]: out[0..5]
 // the 6 corner terms summed over the D features, out[6 + ii*DMAX + d] the feature terms
-// (register array, static indices only).
+// (register array, static indices only).  v: the 6 corner coordinates, c: the corner features
+// as [3][DMAX] (register arrays).
 // ------------------------------------------------------------------------------------------
 template <typename T, int DMAX>
 __device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], const T *g,
@@ -70,7 +71,7 @@ __device__ __forceinline__ void raster_bwd_pixel(const T *v, const T wts[3], con
 #pragma unroll
   for (int d = 0; d < DMAX; ++d) {
     if (d < D) {
-      const T c0 = c[d], c1 = c[D + d], c2 = c[2 * D + d];
+      const T c0 = c[d], c1 = c[DMAX + d], c2 = c[2 * DMAX + d];  // (c: [3][DMAX])
       const T dldI = sizeof(T) == 4 ? gd[d] * rkk : gd[d] / kk;
 #pragma unroll
       for (int j = 0; j < 6; ++j) out[j] += dldI * ((c1 - c0) * dw1[j] + (c2 - c0) * dw2[j]);
@@ -130,6 +131,16 @@ __device__ __forceinline__ void raster_bwd_group(const RasterBwdArgs<T> &ra, int
     for (int d = 0; d < DMAX; ++d) gd[d] = d < D ? grad[p * D + d] : (T)0;
     if (f >= 0 && f < F) {
       const int64_t tf = (int64_t)b * F + f;
+      // the face's corners and features first: their round trip overlaps the LDS hash insert
+      // below (the compiler keeps global loads after an LDS atomic loop)
+      T fv[6], fc[3 * DMAX];
+#pragma unroll
+      for (int j = 0; j < 6; ++j) fv[j] = fvi[tf * 6 + j];
+#pragma unroll
+      for (int ii = 0; ii < 3; ++ii)
+#pragma unroll
+        for (int d = 0; d < DMAX; ++d)
+          fc[ii * DMAX + d] = d < D ? feat[tf * 3 * D + ii * D + d] : (T)0;
       const int key = ROWKEY ? (int)tf : (int)f;
       unsigned u = ((unsigned)key * 2654435761u) >> 24;
       for (;;) {  // <= 256 keys in 256 slots: terminates
@@ -139,7 +150,7 @@ __device__ __forceinline__ void raster_bwd_group(const RasterBwdArgs<T> &ra, int
       }
       h = (int)u;
       rank = atomicAdd(&s_n[h], 1);
-      raster_bwd_pixel<T, DMAX>(fvi + tf * 6, wts, gd, feat + tf * 3 * D, D, eps, c);
+      raster_bwd_pixel<T, DMAX>(fv, wts, gd, fc, D, eps, c);
     }
   }
   __syncthreads();

@@ -315,6 +315,7 @@ struct SoftPairBuf {
                        // record cursor (all zeroed by kd_bin_count: n_clear = 6)
   unsigned long long *cursor;
   int64_t ntiles, npixels, cap, lim;  // lim: records a forward may use (kd_set_pool_limits)
+  int64_t icap;                        // entries of `items` (its allocation)
   int fixed;  // knum <= 32 and the whole pool usable: tile t owns records [t * 256 K, +256 K)
   int ntx;
 };

@@ -91,7 +91,8 @@ SoftPairBuf<T> soft_pair_carve(void *ws, size_t &off, int B, int H, int W, int K
   pb.ntile = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.items = (PairItem *)(base + off);
-  off += align_up(sizeof(PairItem) * (size_t)(pb.cap / kBlock + tiles));
+  pb.icap = pb.cap / kBlock + tiles;
+  off += align_up(sizeof(PairItem) * (size_t)pb.icap);
   pb.tiles = (int32_t *)(base + off);
   off += align_up(sizeof(int32_t) * (size_t)tiles);
   pb.ovf = (int32_t *)(base + off);
@@ -1149,6 +1150,12 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
   const FaceSet<T> &fs = a.fs;
   const int H = fs.H, W = fs.W;
   const int lane = threadIdx.x & (kWave - 1);
+  // the first pass's items are loaded with the item count, not after it (entries past the count
+  // are stale and dropped; the grid covers the items in about one pass)
+  PairItem first[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u)
+    first[u] = blk * R + u < pb.icap ? pb.items[blk * R + u] : PairItem{0, 0, 0};
   const int nitems = pb.counters[0];
   // R items per workgroup pass; their load chains (item -> record -> the pixel's gradient and
   // soft value, the face's corners) are issued together
@@ -1161,7 +1168,8 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
     PairItem item[R];
 #pragma unroll
     for (int u = 0; u < R; ++u) {
-      item[u] = it0 + u < nitems ? pb.items[it0 + u] : PairItem{0, 0, 0};
+      item[u] = it0 + u < nitems ? (it0 == blk * R ? first[u] : pb.items[it0 + u])
+                                 : PairItem{0, 0, 0};
       ok[u] = (int)threadIdx.x < item[u].n;
       if (ok[u]) r[u] = pb.rec[item[u].start + threadIdx.x];
     }
