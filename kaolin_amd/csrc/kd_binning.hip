@@ -278,9 +278,18 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
   const int b = blockIdx.y, chunk = blockIdx.x, tid = threadIdx.x;
   const int nct = bb.g.nct();
   for (int k = tid; k < nct * kStride; k += kBlock) s_mask[k] = 0u;
-  {  // this chunk's exclusive offsets in every tile's bin (kd_bin_scan's chunk-major row)
+  // this chunk's exclusive offsets in every tile's bin (kd_bin_scan's chunk-major row), the
+  // chunk's spans and (below) the view's totals: all loaded before any of them is waited for
+  // (one round trip; staging the offsets into LDS first made it two)
+  constexpr int kOffPer = kMaxCtiles / kBlock;
+  int ofv[kOffPer];
+  {
     const int *offs = bb.offs + ((int64_t)b * bb.nchunk + chunk) * nct;
-    for (int c = tid; c < nct; c += kBlock) s_offs[c] = offs[c];
+#pragma unroll
+    for (int k = 0; k < kOffPer; ++k) {
+      const int c = k * kBlock + tid;
+      ofv[k] = c < nct ? offs[c] : 0;
+    }
   }
   int64_t lo, hi;
   view_range(fs, b, lo, hi);
@@ -303,6 +312,11 @@ __global__ __launch_bounds__(kBlock, 7) void kd_bin_scatter(BinJobs<T> jobs) {
       const int c = tid * kPer + k;
       v[k] = c < nct ? tot[c] : 0;
       sum += v[k];
+    }
+#pragma unroll
+    for (int k = 0; k < kOffPer; ++k) {
+      const int c = k * kBlock + tid;
+      if (c < nct) s_offs[c] = ofv[k];
     }
     int all;
     int run = wg_exclusive_scan(sum, s_scan, all);
