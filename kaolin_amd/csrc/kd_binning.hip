@@ -160,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void kd_bin_count(BinJobs<T> jobs) {
       const FaceSet<T> &fs = jobs.fs[z0];
       if (i < hi) {
         T c[3][3], fi[6], n[3], v[6];
-        prep_face<T>(jobs.prep.a, i, c, fi, n);
+        prep_face_bf<T>(jobs.prep.a, b, i - lo, c, fi, n);  // (row i = view b's face i - lo)
 #pragma unroll
         for (int k = 0; k < 6; ++k) v[k] = fi[k] * fs.scale;  // load_corners' product
         if (z0 == 0) prep_stage<T>(c, fi, n, s_pc, s_pi, s_pn);
@@ -555,6 +555,9 @@ hipError_t bin_faces2(const FaceSet<T> &fs0, const BinBuffers &bb0, const FaceSe
   // both sets must describe the same views, faces and image (same chunking and tile grid)
   if (fs0.B != fs1.B || fs0.N != fs1.N || fs0.H != fs1.H || fs0.W != fs1.W ||
       bb0.nchunk != bb1.nchunk || bb0.g.nct() != bb1.g.nct())
+    return hipErrorInvalidValue;
+  // the projecting count takes view b's rows as [b F, (b + 1) F) (kd_bin_count PREP)
+  if (prep && prep->a.vertices && (fs0.first_idx || fs1.first_idx || fs0.F != prep->a.F))
     return hipErrorInvalidValue;
   BinJobs<T> jobs{};
   if (prep) jobs.prep = *prep;

@@ -38,13 +38,12 @@ __device__ __forceinline__ void cam_point(const T *tf, const T *p, T c[3]) {
   for (int j = 0; j < 3; ++j) c[j] = p[0] * tf[j] + p[1] * tf[3 + j] + p[2] * tf[6 + j] + tf[9 + j];
 }
 
-// Face row i (view i / F): camera-space corners c, image corners fi (x, y per corner) and the
-// unit normal n, exactly as the reference composition rounds them.
+// Face f of view b: camera-space corners c, image corners fi (x, y per corner) and the unit
+// normal n, exactly as the reference composition rounds them.  (A caller whose workgroup holds
+// one view passes it as b: no 64-bit division, and the view's transform is a uniform load.)
 template <typename T>
-__device__ __forceinline__ void prep_face(const PrepArgs<T> &a, int64_t i, T c[3][3], T fi[6],
-                                          T n[3]) {
-  const int b = (int)(i / a.F);
-  const int64_t f = i - (int64_t)b * a.F;
+__device__ __forceinline__ void prep_face_bf(const PrepArgs<T> &a, int b, int64_t f, T c[3][3],
+                                             T fi[6], T n[3]) {
   const T *vb = a.vertices + (a.Bv == 1 ? 0 : (int64_t)b * a.V * 3);
   const T *tf = a.tf + (int64_t)b * 12;
 #pragma unroll
@@ -66,6 +65,14 @@ __device__ __forceinline__ void prep_face(const PrepArgs<T> &a, int64_t i, T c[3
   n[0] = r[0] / len;
   n[1] = r[1] / len;
   n[2] = r[2] / len;
+}
+
+// Face row i (view i / F).
+template <typename T>
+__device__ __forceinline__ void prep_face(const PrepArgs<T> &a, int64_t i, T c[3][3], T fi[6],
+                                          T n[3]) {
+  const int b = (int)(i / a.F);
+  prep_face_bf<T>(a, b, i - (int64_t)b * a.F, c, fi, n);
 }
 
 // Copies n elements of T from LDS to global memory with the workgroup, 16-byte vectors when

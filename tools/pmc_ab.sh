@@ -15,5 +15,5 @@ for d in "$a" "$b"; do
   rc=$?
   if [ $rc -ne 0 ]; then tail -5 "$out/p1.log"; exit $rc; fi
   echo "== $name"
-  python3 "$root/tools/pmc_summary.py" "$out" | grep -A9 "dibr_fwd\|dibr_bwd"
+  python3 "$root/tools/pmc_summary.py" "$out" | grep -A9 "dibr_fwd\|dibr_bwd\|bin_count"
 done
