@@ -1214,7 +1214,32 @@ __device__ __forceinline__ void soft_bwd_items_body(const SoftArgs<T> &a, const 
       seg_scan_dpp<0x143, 0xc>(seg, g);  // row_bcast:31 -> rows 2, 3
       const int next_key = __shfl_down(key, 1);
       const bool tail = key >= 0 && (lane == kWave - 1 || next_key != key);
-      if (tail) {
+      if constexpr (!VTX && sizeof(T) == 4) {
+        // the run sums leave as whole face rows: tail r's term q goes to lane 6 r + q of a pass,
+        // so one atomic instruction adds ~10 faces' consecutive 24-byte rows.  Float atomics
+        // execute at the memory side, one request per 64-byte segment an instruction touches
+        // (MI355X_MICROARCH.md, Global float atomics): six one-term instructions made one
+        // request per tail and term.  (diagnostics 4096: no atomics)
+        const uint64_t tm = __ballot(tail);
+        const int nt = __popcll(tm);
+        const int rank = __popcll(tm & ((1ull << lane) - 1ull));
+        // lane r < nt learns the lane of the r-th tail (a push; the other lanes push to lane 63,
+        // which is a tail's destination only when every lane is a tail)
+        const int tail_lane = __builtin_amdgcn_ds_permute((tail ? rank : 63) << 2, lane);
+        for (int v0 = 0; v0 < 6 * nt && !ablate(fs.dbg, 4096); v0 += kWave) {
+          const int v = v0 + lane;
+          const int r = v / 6, q = v - 6 * r;
+          const int src = __builtin_amdgcn_ds_bpermute(min(r, kWave - 1) << 2, tail_lane) << 2;
+          const int kk = __builtin_amdgcn_ds_bpermute(src, key);
+          float x = 0.f;
+#pragma unroll
+          for (int j = 0; j < 6; ++j) {
+            const float gj = __int_as_float(__builtin_amdgcn_ds_bpermute(src, __float_as_int(g[j])));
+            x = q == j ? gj : x;
+          }
+          if (v < 6 * nt && x != 0.f) atomicAdd(a.grad_fvi + (int64_t)kk * 6 + q, x);
+        }
+      } else if (tail && !ablate(fs.dbg, 4096)) {  // (diagnostics 4096: no atomics)
         if constexpr (VTX) {
 #pragma unroll
           for (int k = 0; k < 3; ++k) vertex_add(a.vo, (int64_t)key, k, g[2 * k], g[2 * k + 1]);
