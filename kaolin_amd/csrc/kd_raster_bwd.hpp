@@ -142,7 +142,9 @@ __device__ __forceinline__ void raster_bwd_group(const RasterBwdArgs<T> &ra, int
         for (int d = 0; d < DMAX; ++d)
           fc[ii * DMAX + d] = d < D ? feat[tf * 3 * D + ii * D + d] : (T)0;
       const int key = ROWKEY ? (int)tf : (int)f;
-      unsigned u = ((unsigned)key * 2654435761u) >> 24;
+      // slot = the key's low bits (linear probing): neighbouring faces take neighbouring slots, so
+      // the slot-ordered flush below adds consecutive face rows in one atomic instruction
+      unsigned u = (unsigned)key & (HT - 1);
       for (;;) {  // <= 256 keys in 256 slots: terminates
         const int old = atomicCAS(&s_key[u], -1, key);
         if (old == -1 || old == key) break;
@@ -189,22 +191,41 @@ __device__ __forceinline__ void raster_bwd_group(const RasterBwdArgs<T> &ra, int
     const int ncorner = VTX && c0 == 0 ? 3 : 0;
     const int g0 = ncorner ? 6 : c0;
     const int SI = ncorner + (c1 - g0);
+    // !VTX: every slot's grad_fvi terms of the pass first, then its feature terms, so that an
+    // atomic instruction's lanes add consecutive slots' rows of one array (float atomics execute
+    // at the memory side, one request per 64-byte segment an instruction touches)
+    const int nA = VTX ? 0 : max(0, min(c1, 6) - g0);  // grad_fvi terms per slot
+    const int gB = max(g0, 6), nB = c1 - gB;            // feature terms per slot
     for (int idx = tid; idx < nocc * SI; idx += kBlock) {
-      const int i = idx / SI, j = idx - i * SI;
+      int i, jj;
+      if constexpr (VTX) {
+        i = idx / SI;
+        jj = idx - i * SI;  // (the item index j; the term below)
+      } else if (idx < nocc * nA) {
+        i = idx / nA;
+        jj = g0 + (idx - i * nA);
+      } else {
+        const int k2 = idx - nocc * nA;
+        i = k2 / nB;
+        jj = gB + (k2 - i * nB);
+      }
       const int slot = s_list[i];
       const int ns = s_n[slot];
       const int o = s_off[slot];
       const int64_t row = ROWKEY ? (int64_t)s_key[slot] : (int64_t)b * F + s_key[slot];
-      if (VTX && j < ncorner) {
-        T vx = (T)0, vy = (T)0;
-        for (int r = 0; r < ns; ++r) {  // independent reads: pipelined
-          vx += s_con[o + r][2 * j];
-          vy += s_con[o + r][2 * j + 1];
+      if constexpr (VTX) {
+        const int j = jj;
+        if (j < ncorner) {
+          T vx = (T)0, vy = (T)0;
+          for (int r = 0; r < ns; ++r) {  // independent reads: pipelined
+            vx += s_con[o + r][2 * j];
+            vy += s_con[o + r][2 * j + 1];
+          }
+          vertex_add(ra.vo, row, j, vx, vy);
+          continue;
         }
-        vertex_add(ra.vo, row, j, vx, vy);
-        continue;
+        jj = g0 + (j - ncorner);
       }
-      const int jj = g0 + (j - ncorner);
       T v = (T)0;
       for (int r = 0; r < ns; ++r) v += s_con[o + r][jj - c0];  // independent reads: pipelined
       if (v == (T)0 || ablate(dbg, 128)) continue;
