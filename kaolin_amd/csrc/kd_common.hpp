@@ -42,7 +42,8 @@ __host__ __device__ constexpr bool ablate(int flags, int bit) { return KD_DIAG &
 //       1 << 25 the DefTet backward as the raster tile kernel over the P x knum samples,
 //       1 << 27 kd_dt_bwd: the sample compaction only (no per-face sums),
 //       1 << 26 kd_dt_fwd: the LDS rank form for every pixel (not only past the wave form),
-//       128 / 4096 the raster backward's / the soft backward items' gradient atomics skipped.
+//       128 / 4096 the raster backward's / the soft backward items' gradient atomics skipped,
+//       1 << 28 kd_tex_bwd without its global atomics.
 #if KD_DIAG
 int debug_flags();
 #else

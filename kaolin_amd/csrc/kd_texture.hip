@@ -241,7 +241,7 @@ __device__ __forceinline__ void tex_seg_sum16(const bool take[4], T v[N]) {
 // the LDS buffer falls back to per-sample global atomics.  Zero incoming gradients (the masked
 // background of an image loss) add nothing and are skipped.  The uv gradient is per sample.
 template <typename T, int MODE>
-__global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) {
+__global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row, int dbg) {
   // 20 KB of texel sums: eight workgroups per CU (with s_red, under 160 KB / 8), and C3's block
   // footprints still fit (32 KB: five per CU, 121.7 -> 113.4 us; 8 KB sends blocks to the
   // global-atomic fallback, 148 us)
@@ -288,6 +288,7 @@ __global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) 
   if (lds) __syncthreads();
   auto add = [&](int c, int x, int y, T v) {
     if (x < 0 || x >= a.Wt || y < 0 || y >= a.Ht) return;
+    if (!lds && ablate(dbg, 1 << 28)) return;  // (diagnostics 1 << 28: no global atomics)
     if (lds)
       atomicAdd(&s_acc[((int64_t)c * bh + (y - ly)) * bw + (x - lx)], v);
     else
@@ -360,7 +361,7 @@ __global__ __launch_bounds__(kBlock) void kd_tex_bwd(TexArgs<T> a, int64_t row) 
     if (v == (T)0) continue;
     const int64_t c = i / (bw * bh), r = i - c * bw * bh;
     const int64_t y = ly + r / bw, x = lx + r % bw;
-    atomicAdd(gt + c * plane + y * a.Wt + x, v);
+    if (!ablate(dbg, 1 << 28)) atomicAdd(gt + c * plane + y * a.Wt + x, v);
   }
 }
 
@@ -772,10 +773,11 @@ static int tex_backward(int B, int64_t N, int C, int Ht, int Wt, const T *coords
   {
     ProfScope prof(K_TEX_BWD, stream);
     if (mode == KD_TEX_NEAREST)
-      hipLaunchKernelGGL((kd_tex_bwd<T, KD_TEX_NEAREST>), grid, dim3(kBlock), 0, stream, a, row);
+      hipLaunchKernelGGL((kd_tex_bwd<T, KD_TEX_NEAREST>), grid, dim3(kBlock), 0, stream, a, row,
+                         debug_flags());
     else
       hipLaunchKernelGGL((kd_tex_bwd<T, KD_TEX_BILINEAR>), grid, dim3(kBlock), 0, stream, a,
-                         row);
+                         row, debug_flags());
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess)
