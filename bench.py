@@ -400,8 +400,12 @@ def spawn_ranks(n, argv):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=3)
+    # defaults: a steady-state run (~25 ms timed at C3).  A run that starts from an idle GPU is
+    # ~8% slower over its first few ms (profiles/r06/bench_steps_sweep.txt: K = 20 / 100 / 400
+    # timed steps after 3 warmup steps gave 0.2537 / 0.2366 / 0.2323 ms per step), so 20 warmup
+    # steps and 100 timed ones; the driver's --steps / --warmup are used as given
+    ap.add_argument('--steps', type=int, default=100)
+    ap.add_argument('--warmup', type=int, default=20)
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS) + sorted(SOUP_CONFIGS))
     ap.add_argument('--dtype', default='f32', choices=sorted(DTYPES))
     ap.add_argument('--views-per-gpu', type=int, default=None,
