@@ -96,3 +96,21 @@ def test_c3_view_full_fwd_bwd_f64_vs_oracle(limits):
     finally:
         _lib.set_pool_limits(1.0, 1.0)
     _check_view(h, w, 0, out)
+
+
+def test_tiny_face_soup_single_record_runs_vs_oracle():
+    """Thousands of tiny scattered faces on a mostly empty image: a face is close to one or two
+    uncovered pixels, so most soft-backward runs are a single record and a wave's 64 lanes are
+    often all run ends -- the row-repacked atomics' case with no spare lane for the push
+    (kd_softpair.hip soft_bwd_items_body) -- forward and backward against the oracle."""
+    g = torch.Generator().manual_seed(21)
+    F, h, w = 4000, 96, 96
+    centre = torch.rand((1, F, 1, 2), generator=g) * 2 - 1
+    offs = (torch.rand((1, F, 3, 2), generator=g) - 0.5) * 0.03  # about one pixel across
+    v = dict(fvi=(centre + offs).to(DEV),
+             fvz=(-1 - torch.rand((1, F, 3), generator=g)).to(DEV),
+             feats=torch.rand((1, F, 3, 3), generator=g).to(DEV),
+             normals_z=torch.ones((1, F), device=DEV))
+    out = _fwd_bwd(h, w, v)
+    assert (out[5] < 1).any() and (out[6] >= 0).any()
+    _check_view(h, w, 0, out)
