@@ -208,6 +208,25 @@ __host__ __device__ constexpr size_t dt_wave_lds(int C) {  // depth, w0, w1, fac
   return (size_t)C * (3 * sizeof(T) + 2 * sizeof(int));
 }
 
+// A slot's three weights / two features as one store each (4-byte aligned rows of 12 / 8 bytes:
+// dwordx3 / dwordx2 instead of three / two dword stores)
+template <typename T>
+struct alignas(sizeof(T)) Vec3 {
+  T x, y, z;
+};
+template <typename T>
+struct alignas(sizeof(T)) Vec2 {
+  T x, y;
+};
+template <typename T>
+__device__ __forceinline__ void store3(T *p, T x, T y, T z) {
+  *reinterpret_cast<Vec3<T> *>(p) = Vec3<T>{x, y, z};
+}
+template <typename T>
+__device__ __forceinline__ void store2(T *p, T x, T y) {
+  *reinterpret_cast<Vec2<T> *>(p) = Vec2<T>{x, y};
+}
+
 // The pixel's outputs when its hits fit the wave without the first-K cut (nh <= 64, and nh <= K
 // unless op form).  Lanes form (hit i, group g) pairs: NI >= nh lanes a group, G = 64 / NI
 // groups; lane (i, g) compares hit i with hits j = g, g + G, ... and the groups' counts are summed
@@ -269,21 +288,24 @@ __device__ __forceinline__ void dt_pixel_out_wave(const DtArgs<T> &a, int b, int
     const T w2 = (T)1 - (w0 + w1);  // deftet.py:304
     const int64_t o = row + r;
     a.face_idx[o] = fi;
-    a.weights[3 * o] = w0;
-    a.weights[3 * o + 1] = w1;
-    a.weights[3 * o + 2] = w2;
+    store3(a.weights + 3 * o, w0, w1, w2);
     const T *cf = feat + (int64_t)fi * 3 * D;
     T *out = a.interp + o * D;
-    for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
-      out[d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+    if (D == 2) {  // (uv features: one 8-byte store)
+      store2(out, w0 * cf[0] + w1 * cf[2] + w2 * cf[4], w0 * cf[1] + w1 * cf[3] + w2 * cf[5]);
+    } else {
+      for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
+        out[d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+    }
   }
   for (int s = n + lane; s < K; s += kWave) {
     const int64_t o = row + s;
     a.face_idx[o] = -1;
-    a.weights[3 * o] = (T)0;
-    a.weights[3 * o + 1] = (T)0;
-    a.weights[3 * o + 2] = (T)0;
-    for (int d = 0; d < D; ++d) a.interp[o * D + d] = (T)0;
+    store3(a.weights + 3 * o, (T)0, (T)0, (T)0);
+    if (D == 2)
+      store2(a.interp + o * 2, (T)0, (T)0);
+    else
+      for (int d = 0; d < D; ++d) a.interp[o * D + d] = (T)0;
   }
 }
 
@@ -416,21 +438,24 @@ __device__ void dt_pixel_wave(const DtArgs<T> &a, int b, int64_t p, char *wave_l
     const T w2 = (T)1 - (w0 + w1);  // deftet.py:304
     const int64_t o = row + r;
     a.face_idx[o] = fi;
-    a.weights[3 * o] = w0;
-    a.weights[3 * o + 1] = w1;
-    a.weights[3 * o + 2] = w2;
+    store3(a.weights + 3 * o, w0, w1, w2);
     const T *cf = feat + (int64_t)fi * 3 * D;
     T *out = a.interp + o * D;
-    for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
-      out[d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+    if (D == 2) {  // (uv features: one 8-byte store)
+      store2(out, w0 * cf[0] + w1 * cf[2] + w2 * cf[4], w0 * cf[1] + w1 * cf[3] + w2 * cf[5]);
+    } else {
+      for (int d = 0; d < D; ++d)  // :312-313, the sum over the 3 corners in order
+        out[d] = w0 * cf[d] + w1 * cf[D + d] + w2 * cf[2 * D + d];
+    }
   }
   for (int s = n + lane; s < K; s += kWave) {
     const int64_t o = row + s;
     a.face_idx[o] = -1;
-    a.weights[3 * o] = (T)0;
-    a.weights[3 * o + 1] = (T)0;
-    a.weights[3 * o + 2] = (T)0;
-    for (int d = 0; d < D; ++d) a.interp[o * D + d] = (T)0;
+    store3(a.weights + 3 * o, (T)0, (T)0, (T)0);
+    if (D == 2)
+      store2(a.interp + o * 2, (T)0, (T)0);
+    else
+      for (int d = 0; d < D; ++d) a.interp[o * D + d] = (T)0;
   }
 }
 
