@@ -371,6 +371,25 @@ struct FaceSet {
   long long *tbuf;           // diagnostic per-tile clock buffer (nullptr in production)
 };
 
+// Three / two consecutive values of a row as one store (rows of 12 / 8 bytes at their element
+// alignment: a dwordx3-or-x2+x1 / dwordx2 store instead of three / two dword stores)
+template <typename T>
+struct alignas(sizeof(T)) Vec3 {
+  T x, y, z;
+};
+template <typename T>
+struct alignas(sizeof(T)) Vec2 {
+  T x, y;
+};
+template <typename T>
+__device__ __forceinline__ void store3(T *p, T x, T y, T z) {
+  *reinterpret_cast<Vec3<T> *>(p) = Vec3<T>{x, y, z};
+}
+template <typename T>
+__device__ __forceinline__ void store2(T *p, T x, T y) {
+  *reinterpret_cast<Vec2<T> *>(p) = Vec2<T>{x, y};
+}
+
 template <typename T>
 __device__ __forceinline__ void view_range(const FaceSet<T> &fs, int b, int64_t &lo,
                                            int64_t &hi) {

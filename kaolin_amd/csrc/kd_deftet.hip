@@ -208,25 +208,6 @@ __host__ __device__ constexpr size_t dt_wave_lds(int C) {  // depth, w0, w1, fac
   return (size_t)C * (3 * sizeof(T) + 2 * sizeof(int));
 }
 
-// A slot's three weights / two features as one store each (4-byte aligned rows of 12 / 8 bytes:
-// dwordx3 / dwordx2 instead of three / two dword stores)
-template <typename T>
-struct alignas(sizeof(T)) Vec3 {
-  T x, y, z;
-};
-template <typename T>
-struct alignas(sizeof(T)) Vec2 {
-  T x, y;
-};
-template <typename T>
-__device__ __forceinline__ void store3(T *p, T x, T y, T z) {
-  *reinterpret_cast<Vec3<T> *>(p) = Vec3<T>{x, y, z};
-}
-template <typename T>
-__device__ __forceinline__ void store2(T *p, T x, T y) {
-  *reinterpret_cast<Vec2<T> *>(p) = Vec2<T>{x, y};
-}
-
 // The pixel's outputs when its hits fit the wave without the first-K cut (nh <= 64, and nh <= K
 // unless op form).  Lanes form (hit i, group g) pairs: NI >= nh lanes a group, G = 64 / NI
 // groups; lane (i, g) compares hit i with hits j = g, g + G, ... and the groups' counts are summed

@@ -420,7 +420,16 @@ __device__ __forceinline__ void raster_pairs_tile(const RasterFwdArgs<T> &a, int
   if (uncm && best < 0) atomicOr(&uncm[t.sub], 1ull << lane);
   T *wo = a.weights + p * 3;
   T *io = a.interp + p * a.D;
-  if (best >= 0) {
+  if (a.D == 3 && (best < 0 || (fr_ok && !replay))) {  // one store per row (bw* stay 0: no face)
+    store3(wo, bw0, bw1, bw2);
+    T i0 = (T)0, i1 = (T)0, i2 = (T)0;
+    if (best >= 0) {
+      i0 = bw0 * fr[0][0] + bw1 * fr[1][0] + bw2 * fr[2][0];
+      i1 = bw0 * fr[0][1] + bw1 * fr[1][1] + bw2 * fr[2][1];
+      i2 = bw0 * fr[0][2] + bw1 * fr[1][2] + bw2 * fr[2][2];
+    }
+    store3(io, i0, i1, i2);
+  } else if (best >= 0) {
     wo[0] = bw0;
     wo[1] = bw1;
     wo[2] = bw2;
