@@ -28,22 +28,37 @@ __global__ __launch_bounds__(kBlock) void kd_rast_interp(int64_t P, int64_t HW, 
                                                          T *__restrict__ weights) {
   const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   if (p >= P) return;
-  const T u = rast[4 * p], v = rast[4 * p + 1], id = rast[4 * p + 3];
+  T u, v, id;
+  if (sizeof(T) == 4 && ((uintptr_t)rast & 15) == 0) {  // (the pixel's 16-byte row, one load)
+    const float4 r = reinterpret_cast<const float4 *>(rast)[p];
+    u = r.x;
+    v = r.y;
+    id = r.w;
+  } else {
+    u = rast[4 * p];
+    v = rast[4 * p + 1];
+    id = rast[4 * p + 3];
+  }
   const T w2 = (T)1 - (u + v);  // rasterization.py:213-216
-  weights[3 * p] = u;
-  weights[3 * p + 1] = v;
-  weights[3 * p + 2] = w2;
+  store3(weights + 3 * p, u, v, w2);
   // .long() truncates toward zero; ids are exact integers in nvdiffrast's buffer
   const int64_t f = (id >= (T)1 && id <= (T)F) ? (int64_t)id - 1 : -1;
   face_idx[p] = f;
   T *out = interp + p * D;
   if (f < 0) {
-    for (int d = 0; d < D; ++d) out[d] = (T)0;
+    if (D == 2)
+      store2(out, (T)0, (T)0);
+    else
+      for (int d = 0; d < D; ++d) out[d] = (T)0;
     return;
   }
-  const int64_t b = p / HW;
+  // (the launcher keeps P < 2^31: a 32-bit division)
+  const int64_t b = (int64_t)((uint32_t)p / (uint32_t)HW);
   const T *a = feat + ((b * F + f) * 3) * (int64_t)D;
-  for (int d = 0; d < D; ++d) out[d] = u * a[d] + v * a[D + d] + w2 * a[2 * D + d];
+  if (D == 2)
+    store2(out, u * a[0] + v * a[2] + w2 * a[4], u * a[1] + v * a[3] + w2 * a[5]);
+  else
+    for (int d = 0; d < D; ++d) out[d] = u * a[d] + v * a[D + d] + w2 * a[2 * D + d];
 }
 
 template <typename T>
@@ -53,6 +68,7 @@ static int rast_interp(int B, int H, int W, int64_t F, int D, const T *rast, con
   KD_CHECK_ARG(F < (1ll << 24), "triangle ids above 2^24 are not exact in a float rast buffer");
   const int64_t P = (int64_t)B * H * W;
   if (P == 0) return KD_OK;
+  KD_CHECK_ARG(P < (1ll << 31), "rasterize_from_rast: more than 2^31 pixels");
   KD_CHECK_ARG(rast && face_idx && weights && (D == 0 || (interp && feat)), "NULL buffer");
   {
     ProfScope prof(K_RAST_INTERP, stream);

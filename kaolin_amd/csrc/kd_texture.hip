@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kBlock) void kd_tex_fwd(TexArgs<T> a) {
     const bool vy0 = y0 >= 0 && y0 < a.Ht, vy1 = y1 >= 0 && y1 < a.Ht;
     const T *t = tex + (int64_t)y0 * a.Wt + x0;
     // ix, iy are clipped to the texture: x0, y0 are in range, x1 / y1 at most one past it
-    for (int c = 0; c < a.C; ++c) {
+    auto channel = [&](int c) {
       const T *tc = t + c * plane;
       T nw, ne, sw = (T)0, se = (T)0;
       tex_pair(tc, vx1, nw, ne);
@@ -131,7 +131,13 @@ __global__ __launch_bounds__(kBlock) void kd_tex_fwd(TexArgs<T> a) {
       if (vy0 && vx1) acc = acc + ne * wne;
       if (vy1 && vx0) acc = acc + sw * wsw;
       if (vy1 && vx1) acc = acc + se * wse;
-      out[c] = acc;
+      return acc;
+    };
+    if (a.C == 3) {  // (RGB: the three channels' loads together, one row store)
+      const T c0 = channel(0), c1 = channel(1), c2 = channel(2);
+      store3(out, c0, c1, c2);
+    } else {
+      for (int c = 0; c < a.C; ++c) out[c] = channel(c);
     }
   }
 }
